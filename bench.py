@@ -1,0 +1,184 @@
+#!/usr/bin/env python3
+"""Benchmark: unique states/sec of Stateright's `spawn_bfs` on 2pc N=9 (BASELINE.json), MI355X engine.
+
+One "step" = one complete breadth-first check of TwoPhaseSys{rms: 0..9} (10 340 352 unique /
+123 558 402 generated states, 28 levels), spawn -> join, on device-resident buffers (the device
+allocator caches the visited set and frontiers across steps; the per-step memset of the visited
+set is inside the timed region).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+
+N > 1 runs under torch.distributed.run, one process per GPU. The search itself is not yet
+partitioned across GPUs in this round, so every rank checks its own full replica ("replicas",
+weak scaling); value = total unique states checked by all ranks / max-over-ranks time.
+
+Prints ONE JSON line on rank 0 with `roofline` (dominant kernel = the expand kernel, HIP-event
+timed on its own stream inside the engine) and `cpu_baseline` (the CPU restatement of the
+reference `spawn_bfs`, oracle/bfs_cli, timed on this host's cores on a bounded sample).
+"""
+import argparse
+import json
+import os
+import re
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--rm-count", type=int, default=9)
+    ap.add_argument("--order", default="fast", choices=["fast", "fifo"])
+    ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU restatement (rank 0, N=1)")
+    ap.add_argument("--cpu-threads", type=int, default=16, help="host threads for the CPU baseline")
+    ap.add_argument("--cpu-rm-count", type=int, default=8, help="2pc size of the bounded CPU sample")
+    return ap.parse_args()
+
+
+def cpu_baseline(args):
+    """The oracle's restatement of the multi-threaded reference BFS (oracle/bfs_cli), bounded sample."""
+    cli = os.path.join(ROOT, "oracle", "bfs_cli")
+    if not os.path.exists(cli):
+        subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
+    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    out = subprocess.run([cli, "2pc", str(args.cpu_rm_count), str(threads)], capture_output=True, text=True,
+                         timeout=600, check=True).stdout
+    m = re.search(r"RESULT state_count=(\d+) unique=(\d+) max_depth=(\d+) threads=(\d+) sec=([\d.e+-]+)", out)
+    sc, uq, _, th, sec = int(m[1]), int(m[2]), int(m[3]), int(m[4]), float(m[5])
+    return {
+        "value": uq / sec,
+        "unit": "unique states/s",
+        "cores": th,
+        "kind": "port",
+        "sample": f"full 2pc N={args.cpu_rm_count} check ({uq} unique / {sc} generated states) in {sec:.2f} s "
+                  f"on {th} host threads: C++ restatement of src/checker/bfs.rs (job market, sharded "
+                  f"visited map, shared state_count atomic); the Rust reference cannot be built here",
+    }
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl")
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.cuda.current_device()
+
+    from stateright_amd import TwoPhaseSys
+    n = args.rm_count
+    expect_unique = 6 ** n + 4 ** n + 2 ** n
+
+    def step(profile=False):
+        b = TwoPhaseSys(n).checker().order(args.order).capacity_hint(expect_unique).device(dev)
+        if profile:
+            b = b.profile()
+        c = b.spawn_bfs().join()
+        if c.unique_state_count() != expect_unique:
+            raise SystemExit(f"wrong unique count {c.unique_state_count()} != {expect_unique}")
+        return c
+
+    for _ in range(args.warmup):
+        step()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    barrier()
+    t0 = time.perf_counter()
+    kernel_ms = 0.0
+    launches = 0
+    alg_bytes = 0
+    unique = 0
+    last = None
+    for _ in range(args.steps):
+        c = step(profile=True)
+        st = c.stats()
+        kernel_ms += st["expand_kernel_ms"]
+        launches += st["expand_launches"]
+        alg_bytes += st["algorithmic_bytes"]
+        unique += c.unique_state_count()
+        last = (c, st)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        u = torch.tensor([unique], dtype=torch.float64, device="cuda")
+        dist.all_reduce(u)
+        unique_total = float(u.item())
+    else:
+        unique_total = float(unique)
+
+    if rank != 0:
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+
+    c, st = last
+    avg_launch_ms = kernel_ms / max(1, launches)
+    achieved_gbps = alg_bytes / (kernel_ms * 1e-3) / 1e9 if kernel_ms else 0.0
+    res = {
+        "metric": "unique states/sec (whole node) + HBM GB/s, 2pc N=9 at 1/2/4/8 MI355X",
+        "value": unique_total / elapsed,
+        "unit": "unique states/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u64",
+        "data": "synthetic: the 2pc model's own state space (no dataset)",
+        "config": {
+            "workload": f"2pc N={n} spawn_bfs, full check per step ({expect_unique} unique states)",
+            "model": "2pc",
+            "rm_count": n,
+            "order": args.order,
+            "parallelism": f"replicas{world}" if world > 1 else "1 GPU",
+        },
+        "state_count_per_sec": float(c.state_count()) * world * args.steps / elapsed,
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "expand_fast (expand + fingerprint + visited-set insert + append + properties)",
+            "achieved": achieved_gbps,
+            "peak": HBM_PEAK_GBPS,
+            "unit": "GB/s",
+            "frac": achieved_gbps / HBM_PEAK_GBPS,
+            "traffic": None,
+            "avg_launch_ms": avg_launch_ms,
+            "launches_per_step": launches / args.steps,
+            "algorithmic_bytes_per_step": alg_bytes / args.steps,
+        },
+        "engine": {k: st[k] for k in ("levels", "table_capacity", "rehashes", "level_loop_sec", "total_sec")},
+    }
+    if args.cpu_baseline and world == 1:
+        try:
+            res["cpu_baseline"] = cpu_baseline(args)
+        except Exception as e:  # the GPU number stands on its own
+            res["cpu_baseline"] = {"error": str(e)}
+    print(json.dumps(res))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,153 @@
+/*
+ * stateright_gpu.h — C ABI of the MI355X breadth-first model-checking engine.
+ *
+ * This is the drop-in boundary for Stateright's `CheckerBuilder::spawn_bfs` path. Each entry point
+ * replaces one piece of the reference's Rust interface (crate `stateright` 0.28.0, paths relative to
+ * the reference repository):
+ *
+ *   sr_gpu_bfs_spawn              <- CheckerBuilder::spawn_bfs        src/checker.rs:124-129
+ *                                    BfsChecker::spawn                src/checker/bfs.rs:36-163
+ *                                    (builder options threads/target_state_count/visitor:
+ *                                     src/checker.rs:35-51,162-177, mirrored by sr_opts)
+ *   sr_gpu_bfs_join               <- Checker::join                    src/checker/bfs.rs:300-305
+ *   sr_gpu_bfs_is_done            <- Checker::is_done                 src/checker/bfs.rs:307-311
+ *   sr_gpu_bfs_state_count        <- Checker::state_count             src/checker/bfs.rs:283-285
+ *   sr_gpu_bfs_unique_state_count <- Checker::unique_state_count      src/checker/bfs.rs:287
+ *   sr_gpu_bfs_max_depth          <- (new: BFS depth metric, SURVEY.md §5 "no depth metric")
+ *   sr_gpu_bfs_property_*         <- Model::properties / Property     src/lib.rs:214-300
+ *   sr_gpu_bfs_discovery          <- discoveries() + reconstruct_path src/checker/bfs.rs:289-298,314-342
+ *   sr_gpu_bfs_discovery_path     <- Path::from_fingerprints          src/checker/path.rs:20-86
+ *   sr_gpu_bfs_replay             <- Path::from_actions (assert_discovery) src/checker/path.rs:90-112,
+ *                                                                     src/checker.rs:292-337
+ *   sr_gpu_bfs_visits             <- StateRecorder visitor            src/checker/visitor.rs:70-99
+ *   sr_gpu_bfs_free               <- Drop of the checker (join(self) consumes it in Rust)
+ *   sr_last_error                 <- the reference panics; see "Errors" below
+ *
+ * Models: device code cannot call host function pointers, so `impl Model` becomes a registry of
+ * compiled-in GpuModel encodings selected by `model_id` + integer parameters (SR_MODEL_*). Each
+ * encoding packs one state into fixed-width 64-bit words and enumerates the reference's
+ * `actions()` in order as action slots.
+ *
+ * Errors: the reference panics (zero fingerprint src/lib.rs:310, path nondeterminism
+ * src/checker/path.rs:35-79, worker panics src/checker/bfs.rs:302). Here every call returns a
+ * status (SR_OK or a negative SR_ERR_*) and sr_last_error() describes the last failure on the
+ * calling thread.
+ *
+ * Threading: spawn returns immediately; the level loop runs on a host driver thread bound to one
+ * HIP device. Counters are readable while it runs (like the reference's atomics).
+ */
+#ifndef STATERIGHT_GPU_H
+#define STATERIGHT_GPU_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Model registry (params in parentheses). */
+enum sr_model_id {
+    SR_MODEL_LINEAR_EQUATION = 1, /* (a, b, c)      src/test_util.rs:140-188            */
+    SR_MODEL_BINARY_CLOCK = 2,    /* ()             src/test_util.rs:4-45               */
+    SR_MODEL_2PC = 3,             /* (rm_count<=14) examples/2pc.rs:10-121              */
+    SR_MODEL_INCREMENT = 4,       /* (threads<=15)  examples/increment.rs:109-197       */
+    SR_MODEL_INCREMENT_LOCK = 5,  /* (threads<=12)  examples/increment_lock.rs:3-107    */
+    SR_MODEL_DGRAPH = 6           /* (expectation, len, v.., len, v..) src/test_util.rs:47-116 */
+};
+
+/* Visit order inside a BFS level. */
+enum sr_order {
+    SR_ORDER_AUTO = 0, /* FAST; rerun as FIFO if an early exit makes counts order-dependent */
+    SR_ORDER_FIFO = 1, /* exactly the single-threaded reference order (pop_back/push_front)   */
+    SR_ORDER_FAST = 2  /* any order inside a level: wave-aggregated append, no ordering pass  */
+};
+
+enum sr_expectation { SR_ALWAYS = 0, SR_EVENTUALLY = 1, SR_SOMETIMES = 2 }; /* src/lib.rs:293-300 */
+
+enum sr_status {
+    SR_OK = 0,
+    SR_ERR_ARG = -1,
+    SR_ERR_HIP = -2,
+    SR_ERR_CAPACITY = -3,
+    SR_ERR_UNSUPPORTED = -4,
+    SR_ERR_NO_DEVICE = -5,
+    SR_ERR_NONDETERMINISM = -6
+};
+
+typedef struct sr_opts {
+    uint32_t struct_size;        /* sizeof(sr_opts)                                              */
+    int32_t device;              /* HIP device ordinal                                           */
+    uint64_t target_state_count; /* 0 = None; `CheckerBuilder::target_state_count` checker.rs:164 */
+    int32_t order;               /* enum sr_order                                                */
+    int32_t record_visits;       /* keep every visited state (a StateRecorder visitor)           */
+    uint64_t capacity_hint;      /* expected unique states; 0 = grow the visited table on demand */
+    int32_t profile;             /* time every expand launch with HIP events                     */
+    int32_t verbose;             /* per-level log lines on stderr                                */
+} sr_opts;
+
+/* Timing/throughput counters of a finished run (sr_gpu_bfs_stats). */
+typedef struct sr_stats {
+    double level_loop_sec;       /* first expand launch .. last level synchronised              */
+    double total_sec;            /* spawn .. done, excluding one-time device allocation          */
+    double expand_kernel_ms;     /* sum of expand-kernel HIP-event durations (profile=1)         */
+    uint64_t expand_launches;
+    uint64_t levels;
+    uint64_t table_capacity;     /* visited-set slots                                            */
+    uint64_t rehashes;
+    uint64_t algorithmic_bytes;  /* 8 B per successor probe + 16 B per insert +
+                                    8*W B frontier write + 8*W B frontier read per state         */
+    uint64_t successors;         /* == state_count - init states                                 */
+    uint32_t words_per_state;
+    uint32_t order_used;         /* enum sr_order actually used for the reported counts          */
+} sr_stats;
+
+typedef struct sr_bfs sr_bfs;
+
+void sr_opts_init(sr_opts* opts);
+const char* sr_last_error(void);
+int sr_device_count(void);
+
+/* Spawns the checker; returns NULL on error (see sr_last_error). Non-blocking. */
+sr_bfs* sr_gpu_bfs_spawn(int32_t model_id, const int64_t* params, int32_t nparams, const sr_opts* opts);
+int32_t sr_gpu_bfs_join(sr_bfs* bfs);
+int32_t sr_gpu_bfs_is_done(const sr_bfs* bfs);
+/* 1 while the driver thread is still searching (for `report`'s polling loop, src/checker.rs:223). */
+int32_t sr_gpu_bfs_is_running(const sr_bfs* bfs);
+uint64_t sr_gpu_bfs_state_count(const sr_bfs* bfs);
+uint64_t sr_gpu_bfs_unique_state_count(const sr_bfs* bfs);
+uint32_t sr_gpu_bfs_max_depth(const sr_bfs* bfs);
+int32_t sr_gpu_bfs_stats(const sr_bfs* bfs, sr_stats* out);
+
+int32_t sr_gpu_bfs_property_count(const sr_bfs* bfs);
+/* Copies the property name (NUL-terminated) and its expectation; returns the name length. */
+int32_t sr_gpu_bfs_property(const sr_bfs* bfs, int32_t prop, char* name, int32_t cap, int32_t* expectation);
+
+/* Discovery of property `prop`: writes the fingerprint chain init..discovered state (the
+ * reference's `reconstruct_path` input) and returns its length; 0 = no discovery. */
+int32_t sr_gpu_bfs_discovery(const sr_bfs* bfs, int32_t prop, uint64_t* fp_chain, uint32_t cap);
+/* Replays that chain on the host model (`Path::from_fingerprints`): canonical action ids
+ * (len = chain-1) and states (chain * describe_width int64s). Returns the number of actions,
+ * -1 if no discovery, or a negative SR_ERR_*. */
+int32_t sr_gpu_bfs_discovery_path(const sr_bfs* bfs, int32_t prop, int64_t* action_ids, int32_t cap_actions,
+                                  int64_t* states, int64_t cap_states);
+int32_t sr_gpu_bfs_describe_width(const sr_bfs* bfs);
+/* Reference `Debug` text of a canonical action id (e.g. "RmPrepare(3)"). */
+int32_t sr_gpu_bfs_action_name(const sr_bfs* bfs, int64_t action_id, char* buf, int32_t cap);
+/* Upper bound (exclusive) on canonical action ids of the model, for name lookups. */
+int64_t sr_gpu_bfs_action_id_bound(const sr_bfs* bfs);
+/* Number of init states (`Model::init_states`, src/lib.rs:163). */
+int32_t sr_gpu_bfs_init_count(const sr_bfs* bfs);
+/* `Path::from_actions` (src/checker/path.rs:90-112) from init state `init_index` on the host copy
+ * of the model: writes the states (describe_width int64s each) and, per property, whether its
+ * CONDITION holds on the last state. Returns the number of actions applied, or -1 if an action is
+ * not enabled along the way (the reference returns None). */
+int32_t sr_gpu_bfs_replay(const sr_bfs* bfs, int32_t init_index, const int64_t* action_ids, int32_t n_actions,
+                          int64_t* states, int64_t cap_states, int32_t* conditions, int32_t cap_conditions);
+/* Visited states in visit order (record_visits=1), describe_width int64s each; returns count*width. */
+int64_t sr_gpu_bfs_visits(const sr_bfs* bfs, int64_t* out, int64_t cap);
+void sr_gpu_bfs_free(sr_bfs* bfs);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* STATERIGHT_GPU_H */

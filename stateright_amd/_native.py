@@ -1,0 +1,107 @@
+"""ctypes binding to the MI355X engine's C ABI (include/stateright_gpu.h).
+
+The shared library `stateright_amd/libstateright_gpu.so` is built in-tree by
+`stateright_amd.build.build()` (hipcc --offload-arch=gfx950). There is no fallback: if the library
+is missing, or no HIP device is visible, every checker call raises.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libstateright_gpu.so")
+
+SR_MODEL_LINEAR_EQUATION = 1
+SR_MODEL_BINARY_CLOCK = 2
+SR_MODEL_2PC = 3
+SR_MODEL_INCREMENT = 4
+SR_MODEL_INCREMENT_LOCK = 5
+SR_MODEL_DGRAPH = 6
+
+SR_ORDER_AUTO, SR_ORDER_FIFO, SR_ORDER_FAST = 0, 1, 2
+SR_ALWAYS, SR_EVENTUALLY, SR_SOMETIMES = 0, 1, 2
+
+
+class sr_opts(ctypes.Structure):
+    _fields_ = [
+        ("struct_size", ctypes.c_uint32),
+        ("device", ctypes.c_int32),
+        ("target_state_count", ctypes.c_uint64),
+        ("order", ctypes.c_int32),
+        ("record_visits", ctypes.c_int32),
+        ("capacity_hint", ctypes.c_uint64),
+        ("profile", ctypes.c_int32),
+        ("verbose", ctypes.c_int32),
+    ]
+
+
+class sr_stats(ctypes.Structure):
+    _fields_ = [
+        ("level_loop_sec", ctypes.c_double),
+        ("total_sec", ctypes.c_double),
+        ("expand_kernel_ms", ctypes.c_double),
+        ("expand_launches", ctypes.c_uint64),
+        ("levels", ctypes.c_uint64),
+        ("table_capacity", ctypes.c_uint64),
+        ("rehashes", ctypes.c_uint64),
+        ("algorithmic_bytes", ctypes.c_uint64),
+        ("successors", ctypes.c_uint64),
+        ("words_per_state", ctypes.c_uint32),
+        ("order_used", ctypes.c_uint32),
+    ]
+
+    def as_dict(self):
+        return {name: getattr(self, name) for name, _ in self._fields_}
+
+
+# (name, restype, argtypes) of every exported entry point; tests check this list against the header.
+_P = ctypes.c_void_p
+_I64P = ctypes.POINTER(ctypes.c_int64)
+SIGNATURES = [
+    ("sr_opts_init", None, [ctypes.POINTER(sr_opts)]),
+    ("sr_last_error", ctypes.c_char_p, []),
+    ("sr_device_count", ctypes.c_int, []),
+    ("sr_gpu_bfs_spawn", _P, [ctypes.c_int32, _I64P, ctypes.c_int32, ctypes.POINTER(sr_opts)]),
+    ("sr_gpu_bfs_join", ctypes.c_int32, [_P]),
+    ("sr_gpu_bfs_is_done", ctypes.c_int32, [_P]),
+    ("sr_gpu_bfs_is_running", ctypes.c_int32, [_P]),
+    ("sr_gpu_bfs_state_count", ctypes.c_uint64, [_P]),
+    ("sr_gpu_bfs_unique_state_count", ctypes.c_uint64, [_P]),
+    ("sr_gpu_bfs_max_depth", ctypes.c_uint32, [_P]),
+    ("sr_gpu_bfs_stats", ctypes.c_int32, [_P, ctypes.POINTER(sr_stats)]),
+    ("sr_gpu_bfs_property_count", ctypes.c_int32, [_P]),
+    ("sr_gpu_bfs_property", ctypes.c_int32, [_P, ctypes.c_int32, ctypes.c_char_p, ctypes.c_int32,
+                                             ctypes.POINTER(ctypes.c_int32)]),
+    ("sr_gpu_bfs_discovery", ctypes.c_int32, [_P, ctypes.c_int32, ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint32]),
+    ("sr_gpu_bfs_discovery_path", ctypes.c_int32, [_P, ctypes.c_int32, _I64P, ctypes.c_int32, _I64P, ctypes.c_int64]),
+    ("sr_gpu_bfs_describe_width", ctypes.c_int32, [_P]),
+    ("sr_gpu_bfs_action_name", ctypes.c_int32, [_P, ctypes.c_int64, ctypes.c_char_p, ctypes.c_int32]),
+    ("sr_gpu_bfs_action_id_bound", ctypes.c_int64, [_P]),
+    ("sr_gpu_bfs_init_count", ctypes.c_int32, [_P]),
+    ("sr_gpu_bfs_replay", ctypes.c_int32, [_P, ctypes.c_int32, _I64P, ctypes.c_int32, _I64P, ctypes.c_int64,
+                                           ctypes.POINTER(ctypes.c_int32), ctypes.c_int32]),
+    ("sr_gpu_bfs_visits", ctypes.c_int64, [_P, _I64P, ctypes.c_int64]),
+    ("sr_gpu_bfs_free", None, [_P]),
+]
+
+_lib = None
+
+
+def load():
+    """Loads the engine library; raises if it has not been built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"MI355X engine library not found at {LIB_PATH}; build it with "
+                "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc --offload-arch=gfx950)")
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, res, args in SIGNATURES:
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    return _lib
+
+
+def last_error():
+    return load().sr_last_error().decode(errors="replace")

@@ -1,0 +1,346 @@
+"""Host-side mirror of Stateright's checker API over the MI355X engine.
+
+Mirrors, name for name, the reference's `CheckerBuilder` (src/checker.rs:35-178), the `Checker`
+trait (src/checker.rs:184-338) and `Path` (src/checker/path.rs), so that code written against
+`model.checker().spawn_bfs().join()` reads the same. Every call goes through the C ABI in
+include/stateright_gpu.h; there is no CPU fallback.
+"""
+import ctypes
+import enum
+import sys
+import time
+
+from . import _native as N
+
+
+class Expectation(enum.IntEnum):
+    """`Expectation` (src/lib.rs:293-300)."""
+    Always = N.SR_ALWAYS
+    Eventually = N.SR_EVENTUALLY
+    Sometimes = N.SR_SOMETIMES
+
+
+class CheckerError(RuntimeError):
+    """A failed engine call (the reference panics in these cases)."""
+
+    def __init__(self, what, code=None):
+        super().__init__(f"{what}: {N.last_error()}" + (f" (status {code})" if code is not None else ""))
+        self.code = code
+
+
+class Path:
+    """`Path<State, Action>` (src/checker/path.rs:16): states with the action taken from each.
+
+    States are the canonical integer descriptions shared with the CPU oracle; actions are their
+    `Debug` text (e.g. "RmPrepare(3)"), with the canonical ids in `action_ids`.
+    """
+
+    def __init__(self, states, action_ids, action_names):
+        self.states = [tuple(s) for s in states]
+        self.action_ids = list(action_ids)
+        self.action_names = list(action_names)
+
+    def last_state(self):
+        return self.states[-1]
+
+    def into_states(self):
+        return list(self.states)
+
+    def into_actions(self):
+        return list(self.action_names)
+
+    def into_vec(self):
+        acts = self.action_names + [None]
+        return list(zip(self.states, acts))
+
+    def __len__(self):
+        return len(self.action_ids)
+
+    def __str__(self):  # `impl Display for Path` (src/checker/path.rs:174-187)
+        return f"Path[{len(self.action_ids)}]:\n" + "".join(f"- {a}\n" for a in self.action_names)
+
+    def __repr__(self):
+        return f"Path({self.action_names!r})"
+
+
+class StateRecorder:
+    """`StateRecorder` visitor (src/checker/visitor.rs:70-99): records every visited state."""
+
+    def __init__(self):
+        self.states = []
+
+    @classmethod
+    def new_with_accessor(cls):
+        r = cls()
+        return r, (lambda: list(r.states))
+
+
+class CheckerBuilder:
+    """`CheckerBuilder` (src/checker.rs:35-178) for a registered GpuModel."""
+
+    def __init__(self, model):
+        self._model = model
+        self._opts = N.sr_opts()
+        self._opts.struct_size = ctypes.sizeof(N.sr_opts)
+        self._threads = 1
+        self._visitor = None
+
+    # --- options mirrored from the reference ---------------------------------------------------
+    def threads(self, thread_count):
+        """`threads` (src/checker.rs:170-172). The engine runs one host driver thread per GPU;
+        the value is kept for API compatibility and does not change results."""
+        self._threads = int(thread_count)
+        return self
+
+    def target_state_count(self, count):
+        """`target_state_count` (src/checker.rs:164-166): stop at the first 1500-pop block
+        boundary of the single-threaded reference order at which state_count >= count."""
+        self._opts.target_state_count = int(count)
+        return self
+
+    def visitor(self, visitor):
+        """`visitor` (src/checker.rs:175-177); only `StateRecorder` is supported (batched export)."""
+        if not isinstance(visitor, StateRecorder):
+            raise TypeError("the GPU engine exports visits in bulk: pass a StateRecorder")
+        self._visitor = visitor
+        self._opts.record_visits = 1
+        return self
+
+    def symmetry(self):
+        # BfsChecker ignores symmetry (src/checker/bfs.rs:36-74 never reads options.symmetry).
+        return self
+
+    # --- engine-specific options ---------------------------------------------------------------
+    def order(self, order):
+        """"auto" (default), "fifo" (exact reference visit order) or "fast"."""
+        self._opts.order = {"auto": N.SR_ORDER_AUTO, "fifo": N.SR_ORDER_FIFO, "fast": N.SR_ORDER_FAST}[order]
+        return self
+
+    def capacity_hint(self, unique_states):
+        self._opts.capacity_hint = int(unique_states)
+        return self
+
+    def device(self, ordinal):
+        self._opts.device = int(ordinal)
+        return self
+
+    def profile(self, on=True):
+        self._opts.profile = int(bool(on))
+        return self
+
+    def verbose(self, on=True):
+        self._opts.verbose = int(bool(on))
+        return self
+
+    # --- spawn ---------------------------------------------------------------------------------
+    def spawn_bfs(self):
+        """`spawn_bfs` (src/checker.rs:124-129): non-blocking; call `join()`."""
+        return GpuBfsChecker(self._model, self._opts, self._visitor)
+
+    spawn_gpu_bfs = spawn_bfs
+
+    def serve(self, *_):
+        raise NotImplementedError("Explorer is out of scope for the GPU engine (SURVEY.md §2)")
+
+
+class GpuBfsChecker:
+    """The `Checker` trait (src/checker.rs:184-338) implemented by the MI355X engine."""
+
+    def __init__(self, model, opts, visitor=None):
+        lib = N.load()
+        self._lib = lib
+        self._model = model
+        self._visitor = visitor
+        params = list(model.params())
+        arr = (ctypes.c_int64 * max(1, len(params)))(*params)
+        self._h = lib.sr_gpu_bfs_spawn(model.MODEL_ID, arr, len(params), ctypes.byref(opts))
+        if not self._h:
+            raise CheckerError("sr_gpu_bfs_spawn")
+        self._joined = False
+        self._props = None
+        self._names = {}
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            self._lib.sr_gpu_bfs_free(h)
+            self._h = None
+
+    # --- Checker trait -------------------------------------------------------------------------
+    def model(self):
+        return self._model
+
+    def state_count(self):
+        return self._lib.sr_gpu_bfs_state_count(self._h)
+
+    def unique_state_count(self):
+        return self._lib.sr_gpu_bfs_unique_state_count(self._h)
+
+    def max_depth(self):
+        return self._lib.sr_gpu_bfs_max_depth(self._h)
+
+    def join(self):
+        if not self._joined:
+            st = self._lib.sr_gpu_bfs_join(self._h)
+            self._joined = True
+            if st != 0:
+                raise CheckerError("sr_gpu_bfs_join", st)
+            if self._visitor is not None:
+                self._visitor.states.extend(self.visits())
+        return self
+
+    def is_done(self):
+        return bool(self._lib.sr_gpu_bfs_is_done(self._h))
+
+    def properties(self):
+        if self._props is None:
+            out = []
+            buf = ctypes.create_string_buffer(256)
+            exp = ctypes.c_int32()
+            for i in range(self._lib.sr_gpu_bfs_property_count(self._h)):
+                self._lib.sr_gpu_bfs_property(self._h, i, buf, 256, ctypes.byref(exp))
+                out.append((buf.value.decode(), Expectation(exp.value)))
+            self._props = out
+        return self._props
+
+    def _prop_index(self, name):
+        for i, (n, _) in enumerate(self.properties()):
+            if n == name:
+                return i
+        raise KeyError(f"Unknown property. requested={name}, available={[n for n, _ in self.properties()]}")
+
+    def action_name(self, action_id):
+        if action_id not in self._names:
+            buf = ctypes.create_string_buffer(256)
+            self._lib.sr_gpu_bfs_action_name(self._h, action_id, buf, 256)
+            self._names[action_id] = buf.value.decode()
+        return self._names[action_id]
+
+    def action_id(self, action):
+        if isinstance(action, int):
+            return action
+        for i in range(self._lib.sr_gpu_bfs_action_id_bound(self._h)):
+            if self.action_name(i) == action:
+                return i
+        raise KeyError(f"unknown action {action!r}")
+
+    def discovery_fingerprints(self, name):
+        """The fingerprint chain init..discovery (`reconstruct_path` input, bfs.rs:314-342)."""
+        i = self._prop_index(name)
+        buf = (ctypes.c_uint64 * 65536)()
+        n = self._lib.sr_gpu_bfs_discovery(self._h, i, buf, 65536)
+        if n < 0:
+            raise CheckerError("sr_gpu_bfs_discovery", n)
+        return list(buf[:n])
+
+    def discovery(self, name):
+        """`discovery` (src/checker.rs:211-213): the Path for `name`, or None."""
+        i = self._prop_index(name)
+        acts = (ctypes.c_int64 * 65536)()
+        width = self._lib.sr_gpu_bfs_describe_width(self._h)
+        states = (ctypes.c_int64 * (65536 * max(1, width)))()
+        n = self._lib.sr_gpu_bfs_discovery_path(self._h, i, acts, 65536, states, 65536 * max(1, width))
+        if n == -1:
+            return None
+        if n < 0:
+            raise CheckerError("sr_gpu_bfs_discovery_path", n)
+        flat = list(states[:(n + 1) * width])
+        st = [tuple(flat[k:k + width]) for k in range(0, len(flat), width)]
+        ids = list(acts[:n])
+        return Path(st, ids, [self.action_name(a) for a in ids])
+
+    def discoveries(self):
+        """`discoveries` (src/checker/bfs.rs:289-298): property name -> Path."""
+        out = {}
+        for name, _ in self.properties():
+            p = self.discovery(name)
+            if p is not None:
+                out[name] = p
+        return out
+
+    def visits(self):
+        width = self._lib.sr_gpu_bfs_describe_width(self._h)
+        n = self._lib.sr_gpu_bfs_visits(self._h, None, 0)
+        buf = (ctypes.c_int64 * max(1, n))()
+        self._lib.sr_gpu_bfs_visits(self._h, buf, n)
+        flat = list(buf[:n])
+        return [tuple(flat[k:k + width]) for k in range(0, n, width)]
+
+    def stats(self):
+        s = N.sr_stats()
+        self._lib.sr_gpu_bfs_stats(self._h, ctypes.byref(s))
+        return s.as_dict()
+
+    # --- report / asserts (src/checker.rs:216-337) ---------------------------------------------
+    def discovery_classification(self, name):
+        exp = dict(self.properties())[name]
+        return "example" if exp == Expectation.Sometimes else "counterexample"
+
+    def report(self, w=None):
+        w = w or sys.stdout
+        start = time.monotonic()
+        # `report` polls once per second while checking (src/checker.rs:223-228).
+        while not self._joined and not self.is_done():
+            w.write(f"Checking. states={self.state_count()}, unique={self.unique_state_count()}\n")
+            for _ in range(100):
+                if not self._lib.sr_gpu_bfs_is_running(self._h):
+                    break
+                time.sleep(0.01)
+            if not self._lib.sr_gpu_bfs_is_running(self._h):
+                break
+        self.join()
+        w.write(f"Done. states={self.state_count()}, unique={self.unique_state_count()}, "
+                f"sec={int(time.monotonic() - start)}\n")
+        for name, path in self.discoveries().items():
+            w.write(f'Discovered "{name}" {self.discovery_classification(name)} {path}')
+        return self
+
+    def assert_properties(self):
+        for name, exp in self.properties():
+            if exp == Expectation.Sometimes:
+                self.assert_any_discovery(name)
+            else:
+                self.assert_no_discovery(name)
+
+    def assert_any_discovery(self, name):
+        found = self.discovery(name)
+        if found is not None:
+            return found
+        assert self.is_done(), f'Discovery for "{name}" not found, but model checking is incomplete.'
+        raise AssertionError(f'Discovery for "{name}" not found.')
+
+    def assert_no_discovery(self, name):
+        found = self.discovery(name)
+        if found is not None:
+            raise AssertionError(f'Unexpected "{name}" {self.discovery_classification(name)} {found}'
+                                 f"Last state: {found.last_state()}\n")
+        assert self.is_done(), f'Discovery for "{name}" not found, but model checking is incomplete.'
+
+    def replay(self, actions, init_index=0):
+        """`Path::from_actions` on the host copy of the model: (states, conditions) or None."""
+        ids = [self.action_id(a) for a in actions]
+        arr = (ctypes.c_int64 * max(1, len(ids)))(*ids)
+        width = self._lib.sr_gpu_bfs_describe_width(self._h)
+        states = (ctypes.c_int64 * ((len(ids) + 1) * width))()
+        conds = (ctypes.c_int32 * 64)()
+        n = self._lib.sr_gpu_bfs_replay(self._h, init_index, arr, len(ids), states, (len(ids) + 1) * width, conds, 64)
+        if n < 0:
+            return None
+        flat = list(states)
+        return [tuple(flat[k:k + width]) for k in range(0, len(flat), width)], list(conds[:len(self.properties())])
+
+    def assert_discovery(self, name, actions):
+        """`assert_discovery` (src/checker.rs:292-337) for always/sometimes properties."""
+        found = self.assert_any_discovery(name)
+        i = self._prop_index(name)
+        exp = self.properties()[i][1]
+        for init in range(self._lib.sr_gpu_bfs_init_count(self._h)):
+            r = self.replay(actions, init)
+            if r is None:
+                continue
+            holds = r[1][i]
+            if exp == Expectation.Always and not holds:
+                return
+            if exp == Expectation.Sometimes and holds:
+                return
+        raise AssertionError(f'Invalid discovery for "{name}", but a valid one was found. found={found.into_actions()}')

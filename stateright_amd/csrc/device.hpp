@@ -1,0 +1,111 @@
+// Device plumbing for the engine: HIP error handling, a caching device allocator (buffers are
+// reused across runs so repeated checks pay no hipMalloc), and the HBM visited-set view.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <map>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+namespace sr {
+
+struct Error : std::runtime_error {
+    int code;
+    Error(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+#define SR_HIP(expr)                                                                              \
+    do {                                                                                          \
+        hipError_t e_ = (expr);                                                                   \
+        if (e_ != hipSuccess)                                                                     \
+            throw ::sr::Error(-2, std::string(#expr) + ": " + hipGetErrorString(e_) + " at " +   \
+                                      __FILE__ + ":" + std::to_string(__LINE__));                 \
+    } while (0)
+
+// Process-wide caching allocator: freed blocks go to a per-(device, size) free list. Sizes are
+// rounded up to 2 MiB (or a power of two below that) so that a run with a slightly different
+// frontier reuses the same blocks.
+class DevicePool {
+  public:
+    static DevicePool& get() {
+        static DevicePool p;
+        return p;
+    }
+    void* alloc(int dev, size_t bytes) {
+        bytes = round(bytes);
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            auto& fl = free_[{dev, bytes}];
+            if (!fl.empty()) {
+                void* p = fl.back();
+                fl.pop_back();
+                return p;
+            }
+        }
+        void* p = nullptr;
+        hipError_t e = hipMalloc(&p, bytes);
+        if (e != hipSuccess) {
+            release_all(dev);  // retry once with the cache emptied
+            (void)hipGetLastError();
+            SR_HIP(hipMalloc(&p, bytes));
+        }
+        return p;
+    }
+    void free(int dev, void* p, size_t bytes) {
+        if (!p) return;
+        std::lock_guard<std::mutex> g(mu_);
+        free_[{dev, round(bytes)}].push_back(p);
+    }
+    void release_all(int dev) {
+        std::lock_guard<std::mutex> g(mu_);
+        for (auto& [k, v] : free_)
+            if (k.first == dev) {
+                for (void* p : v) (void)hipFree(p);
+                v.clear();
+            }
+    }
+    static size_t round(size_t b) {
+        if (b < 256) return 256;
+        if (b >= (2u << 20)) return (b + (2u << 20) - 1) & ~(size_t)((2u << 20) - 1);
+        size_t r = 256;
+        while (r < b) r <<= 1;
+        return r;
+    }
+
+  private:
+    std::mutex mu_;
+    std::map<std::pair<int, size_t>, std::vector<void*>> free_;
+};
+
+// RAII device buffer backed by the pool.
+template <class T>
+struct DBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    int dev = 0;
+    DBuf() = default;
+    DBuf(const DBuf&) = delete;
+    DBuf& operator=(const DBuf&) = delete;
+    ~DBuf() { reset(); }
+    void reset() {
+        if (p) DevicePool::get().free(dev, p, n * sizeof(T));
+        p = nullptr;
+        n = 0;
+    }
+    void alloc(int d, size_t count) {
+        reset();
+        dev = d;
+        n = count ? count : 1;
+        p = static_cast<T*>(DevicePool::get().alloc(d, n * sizeof(T)));
+    }
+    void swap(DBuf& o) {
+        std::swap(p, o.p);
+        std::swap(n, o.n);
+        std::swap(dev, o.dev);
+    }
+};
+
+}  // namespace sr

@@ -1,0 +1,683 @@
+// MI355X breadth-first model-checking engine: host level loop + C ABI (include/stateright_gpu.h).
+//
+// Replaces `BfsChecker` (src/checker/bfs.rs). The reference's T worker threads, job market and
+// 1500-state blocks (bfs.rs:75-152) become one host driver thread per GPU that runs the search
+// level by level; each level is one pass of HIP kernels over the frontier held in HBM (kernels.hpp).
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/stateright_gpu.h"
+#include "device.hpp"
+#include "kernels.hpp"
+
+namespace sr {
+
+static thread_local std::string g_last_error;
+static void set_error(const std::string& e) { g_last_error = e; }
+
+using Clock = std::chrono::steady_clock;
+static double secs(Clock::time_point a, Clock::time_point b) { return std::chrono::duration<double>(b - a).count(); }
+
+static inline u32 blocks_for(u64 n, u32 bs) { return (u32)((n + bs - 1) / bs); }
+
+struct DiscoveryRec {
+    bool found = false;
+    u32 level = 0, rank = 0;
+    u64 fp = 0;
+};
+
+class EngineBase {
+  public:
+    virtual ~EngineBase() = default;
+    virtual void run() = 0;
+    virtual int nprops() const = 0;
+    virtual const char* prop_name(int p) const = 0;
+    virtual int expectation(int p) const = 0;
+    virtual int width() const = 0;
+    virtual std::string action_name(i64 id) const = 0;
+    virtual int chain(int p, std::vector<u64>& out) = 0;
+    virtual int path(int p, std::vector<i64>& actions, std::vector<i64>& states) = 0;
+    virtual std::vector<i64> visits() const = 0;
+    virtual i64 action_id_bound() const = 0;
+    virtual int init_count() const = 0;
+    virtual int replay(int init, const i64* ids, int n, std::vector<i64>& states, std::vector<int>& conds) const = 0;
+
+    std::atomic<u64> state_count{0}, unique{0};
+    std::atomic<u32> max_depth{0};
+    std::atomic<bool> finished{false};
+    bool reference_done = false;  // `is_done` (bfs.rs:307-311): explored all or discovered all
+    int status = SR_OK;
+    std::string error;
+    sr_stats stats{};
+    std::vector<DiscoveryRec> disc;
+};
+
+template <class M>
+class Engine final : public EngineBase {
+    static constexpr int W = M::W;
+
+  public:
+    Engine(M m, const sr_opts& o) : m_(m), o_(o), A_((u32)m.max_actions()), D_((u32)m.max_out_degree()) {
+        disc.resize(M::NPROPS);
+    }
+    ~Engine() override {
+        if (stream_) (void)hipStreamDestroy(stream_);
+        for (auto* e : {ev0_, ev1_})
+            if (e) (void)hipEventDestroy(e);
+    }
+
+    int nprops() const override { return M::NPROPS; }
+    const char* prop_name(int p) const override { return m_.prop_name(p); }
+    int expectation(int p) const override { return m_.expectation(p); }
+    int width() const override { return m_.describe_width(); }
+    std::string action_name(i64 id) const override { return m_.action_name(id); }
+
+    void run() override {
+        SR_HIP(hipSetDevice(o_.device));
+        SR_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+        SR_HIP(hipEventCreate(&ev0_));
+        SR_HIP(hipEventCreate(&ev1_));
+        SR_HIP(hipMalloc(&lc_d_, sizeof(LevelCounters)));
+        int order = o_.order;
+        if (order == SR_ORDER_AUTO) order = o_.target_state_count ? SR_ORDER_FIFO : SR_ORDER_FAST;
+        bool order_dependent = run_order(order);
+        if (order_dependent && o_.order == SR_ORDER_AUTO && order == SR_ORDER_FAST) {
+            // An early exit inside a level makes counts depend on the visit order: redo the
+            // check in the reference's exact FIFO order.
+            if (o_.verbose) std::fprintf(stderr, "[sr] early exit in FAST order; re-running in FIFO order\n");
+            run_order(SR_ORDER_FIFO);
+        }
+        SR_HIP(hipFree(lc_d_));
+        lc_d_ = nullptr;
+    }
+
+    int chain(int p, std::vector<u64>& out) override {
+        out.clear();
+        if (p < 0 || p >= M::NPROPS || !disc[p].found) return 0;
+        SR_HIP(hipSetDevice(o_.device));
+        DBuf<u64> buf;
+        DBuf<u32> len;
+        const u32 cap = 1u << 16;
+        buf.alloc(o_.device, cap);
+        len.alloc(o_.device, 1);
+        trace_chain<<<1, 1, 0, stream_>>>(view(), disc[p].fp, buf.p, cap, len.p);
+        SR_HIP(hipGetLastError());
+        u32 n = 0;
+        SR_HIP(hipMemcpyAsync(&n, len.p, sizeof(u32), hipMemcpyDeviceToHost, stream_));
+        SR_HIP(hipStreamSynchronize(stream_));
+        out.resize(n);
+        SR_HIP(hipMemcpy(out.data(), buf.p, n * sizeof(u64), hipMemcpyDeviceToHost));
+        std::reverse(out.begin(), out.end());  // init .. discovered
+        return (int)n;
+    }
+
+    // `Path::from_fingerprints` (src/checker/path.rs:20-86) on the host copy of the GpuModel.
+    int path(int p, std::vector<i64>& actions, std::vector<i64>& states) override {
+        std::vector<u64> fps;
+        if (chain(p, fps) == 0) return -1;
+        const int wd = m_.describe_width();
+        u64 inits[8 * W];
+        int k = m_.init_states(inits);
+        std::vector<u64> cur;
+        for (int i = 0; i < k && cur.empty(); ++i)
+            if (fingerprint<W>(&inits[i * W]) == fps[0]) cur.assign(&inits[i * W], &inits[i * W] + W);
+        if (cur.empty()) throw Error(SR_ERR_NONDETERMINISM, "Unable to reconstruct a `Path`: no init state has the expected fingerprint");
+        auto emit = [&](const u64* s) {
+            size_t o = states.size();
+            states.resize(o + wd);
+            m_.describe(s, &states[o]);
+        };
+        for (size_t i = 1; i < fps.size(); ++i) {
+            u64 mask[M::MW];
+            m_.enabled(cur.data(), mask);
+            bool found = false;
+            for (int w = 0; w < M::MW && !found; ++w)
+                for (u64 bits = mask[w]; bits && !found; bits &= bits - 1) {
+                    int a = w * 64 + __builtin_ctzll(bits);
+                    u64 ns[W];
+                    if (!m_.apply(cur.data(), a, ns)) continue;
+                    if (fingerprint<W>(ns) == fps[i]) {
+                        emit(cur.data());
+                        actions.push_back(m_.action_id(cur.data(), a));
+                        cur.assign(ns, ns + W);
+                        found = true;
+                    }
+                }
+            if (!found)
+                throw Error(SR_ERR_NONDETERMINISM, "Unable to reconstruct a `Path`: " + std::to_string(i) +
+                                                       " previous state(s) reconstructed but no successor has the next fingerprint");
+        }
+        emit(cur.data());
+        return (int)actions.size();
+    }
+
+    i64 action_id_bound() const override { return m_.action_id_bound(); }
+    int init_count() const override {
+        u64 inits[8 * W];
+        return m_.init_states(inits);
+    }
+    int replay(int init, const i64* ids, int n, std::vector<i64>& states, std::vector<int>& conds) const override {
+        u64 inits[8 * W];
+        int k = m_.init_states(inits);
+        if (init < 0 || init >= k) return -1;
+        const int wd = m_.describe_width();
+        std::vector<u64> cur(&inits[init * W], &inits[init * W] + W);
+        auto emit = [&](const u64* s) {
+            size_t o = states.size();
+            states.resize(o + wd);
+            m_.describe(s, &states[o]);
+        };
+        for (int i = 0; i < n; ++i) {
+            u64 mask[M::MW];
+            m_.enabled(cur.data(), mask);
+            bool found = false;
+            for (int w = 0; w < M::MW && !found; ++w)
+                for (u64 bits = mask[w]; bits && !found; bits &= bits - 1) {
+                    int a = w * 64 + __builtin_ctzll(bits);
+                    if (m_.action_id(cur.data(), a) != ids[i]) continue;
+                    u64 ns[W];
+                    if (!m_.apply(cur.data(), a, ns)) continue;
+                    emit(cur.data());
+                    cur.assign(ns, ns + W);
+                    found = true;
+                }
+            if (!found) return -1;
+        }
+        emit(cur.data());
+        conds.assign(M::NPROPS, 0);
+        for (int p = 0; p < M::NPROPS; ++p) {
+            bool d = m_.discovers(p, cur.data());
+            conds[p] = m_.expectation(p) == SOMETIMES ? d : !d;
+        }
+        return n;
+    }
+
+    std::vector<i64> visits() const override {
+        const int wd = m_.describe_width();
+        std::vector<i64> out(visits_.size() / W * wd);
+        for (size_t i = 0; i < visits_.size() / W; ++i) m_.describe(&visits_[i * W], &out[i * wd]);
+        return out;
+    }
+
+  private:
+    TableView view() const { return TableView{keys_.p, parents_.p, fifo_ ? meta_.p : nullptr, cap_ - 1}; }
+
+    void alloc_table(u64 cap) {
+        cap_ = cap;
+        keys_.alloc(o_.device, cap);
+        parents_.alloc(o_.device, cap);
+        SR_HIP(hipMemsetAsync(keys_.p, 0, cap * sizeof(u64), stream_));
+        if (fifo_) {
+            meta_.alloc(o_.device, cap);
+            SR_HIP(hipMemsetAsync(meta_.p, 0xff, cap * sizeof(u64), stream_));
+        }
+    }
+
+    // Doubles the visited set. In FIFO order the level's candidate slots (cand) are remapped to
+    // the new table, since the rehash moves every entry.
+    void grow_table(u32* cand = nullptr, u64 cand_n = 0) {
+        DBuf<u64> ok, op, om;
+        ok.swap(keys_);
+        op.swap(parents_);
+        if (fifo_) om.swap(meta_);
+        TableView from{ok.p, op.p, fifo_ ? om.p : nullptr, cap_ - 1};
+        u64 old_cap = cap_;
+        alloc_table(cap_ * 2);
+        rehash<<<blocks_for(old_cap, 256), 256, 0, stream_>>>(from, old_cap, view(), lc_d_);
+        SR_HIP(hipGetLastError());
+        if (cand && cand_n) {
+            remap_slots<<<blocks_for(cand_n, 256), 256, 0, stream_>>>(cand, cand_n, ok.p, view());
+            SR_HIP(hipGetLastError());
+        }
+        SR_HIP(hipStreamSynchronize(stream_));
+        stats.rehashes++;
+    }
+
+    void ensure_frontier(DBuf<u64>& b, u64 states, u64 keep_states) {
+        if (b.n >= states * W) return;
+        DBuf<u64> nb;
+        nb.alloc(o_.device, std::max<u64>(states, b.n / W * 2) * W);
+        if (keep_states) SR_HIP(hipMemcpyAsync(nb.p, b.p, keep_states * W * sizeof(u64), hipMemcpyDeviceToDevice, stream_));
+        b.swap(nb);
+        SR_HIP(hipStreamSynchronize(stream_));
+    }
+
+    void reset_counters() {
+        std::memset(&lc_, 0, sizeof(lc_));
+        for (auto& d : lc_.disc) d = ~0u;
+        SR_HIP(hipMemcpyAsync(lc_d_, &lc_, sizeof(lc_), hipMemcpyHostToDevice, stream_));
+    }
+    void read_counters() {
+        SR_HIP(hipMemcpyAsync(&lc_, lc_d_, sizeof(lc_), hipMemcpyDeviceToHost, stream_));
+        SR_HIP(hipStreamSynchronize(stream_));
+        if (lc_.err & ERR_TABLE_FULL) throw Error(SR_ERR_CAPACITY, "visited set probe limit exceeded");
+        if (lc_.err & ERR_FRONTIER_OVERFLOW) throw Error(SR_ERR_CAPACITY, "frontier overflow");
+    }
+
+    template <class F>
+    void timed(F&& launch) {
+        if (o_.profile) SR_HIP(hipEventRecord(ev0_, stream_));
+        launch();
+        SR_HIP(hipGetLastError());
+        if (o_.profile) {
+            SR_HIP(hipEventRecord(ev1_, stream_));
+            SR_HIP(hipEventSynchronize(ev1_));
+            float ms = 0;
+            SR_HIP(hipEventElapsedTime(&ms, ev0_, ev1_));
+            stats.expand_kernel_ms += ms;
+        }
+        stats.expand_launches++;
+    }
+
+    // Returns true when the run stopped early inside a level in an order-dependent way.
+    bool run_order(int order) {
+        auto t_start = Clock::now();
+        fifo_ = order == SR_ORDER_FIFO;
+        state_count = 0;
+        unique = 0;
+        max_depth = 0;
+        for (auto& d : disc) d = DiscoveryRec{};
+        visits_.clear();
+        stats = sr_stats{};
+        stats.words_per_state = W;
+        stats.order_used = (u32)order;
+
+        // Visited set sized for <= 50% load at the hinted unique count.
+        u64 cap = 1u << 20;
+        if (o_.capacity_hint) while (cap < 2 * o_.capacity_hint) cap <<= 1;
+        alloc_table(cap);
+
+        // Init states (bfs.rs:43-66): all of them are counted and queued (duplicates too), the
+        // visited set keeps distinct ones; `pending` pops from the back, so level 0 is visited in
+        // REVERSE init order.
+        u64 inits[8 * W];
+        int k = m_.init_states(inits);
+        std::vector<u64> f0(inits, inits + k * W);
+        std::vector<u64> rev(k * W);
+        for (int i = 0; i < k; ++i) std::copy(&f0[i * W], &f0[i * W] + W, &rev[(k - 1 - i) * W]);
+        cur_.alloc(o_.device, std::max<u64>(1024, (u64)k) * W);
+        SR_HIP(hipMemcpyAsync(cur_.p, rev.data(), rev.size() * sizeof(u64), hipMemcpyHostToDevice, stream_));
+        reset_counters();
+        insert_roots<M><<<blocks_for(k, 64), 64, 0, stream_>>>(view(), cur_.p, (u32)k, lc_d_);
+        eval_roots<M><<<blocks_for(k, 64), 64, 0, stream_>>>(m_, cur_.p, (u32)k, lc_d_, (1u << M::NPROPS) - 1);
+        SR_HIP(hipGetLastError());
+        read_counters();
+        state_count = (u64)k;
+        unique = lc_.claims;
+
+        u32 undiscovered = (1u << M::NPROPS) - 1;
+        u64 n = (u64)k, popped_before = 0;
+        u32 level = 0;
+        bool order_dependent = false;
+        auto t_loop = Clock::now();
+        for (;;) {
+            // 1. Discoveries among this level's states (evaluated when they were produced).
+            u32 newly = 0, max_rank = 0;
+            for (int p = 0; p < M::NPROPS; ++p)
+                if ((undiscovered >> p & 1) && lc_.disc[p] != ~0u) {
+                    newly |= 1u << p;
+                    max_rank = std::max(max_rank, lc_.disc[p]);
+                    disc[p].found = true;
+                    disc[p].level = level;
+                    disc[p].rank = lc_.disc[p];
+                    u64 s[W];
+                    SR_HIP(hipMemcpy(s, cur_.p + (u64)lc_.disc[p] * W, W * sizeof(u64), hipMemcpyDeviceToHost));
+                    disc[p].fp = fingerprint<W>(s);
+                }
+            u64 limit = n, visited = n;
+            bool stop = false;
+            if (M::NPROPS == 0) {
+                limit = 0;
+                visited = std::min<u64>(1, n);
+                stop = true;
+            } else if (newly && newly == undiscovered) {
+                // The pop of rank max_rank completes the discoveries: check_block returns without
+                // expanding it (bfs.rs:226) and the worker shuts down (bfs.rs:121-128).
+                limit = max_rank;
+                visited = (u64)max_rank + 1;
+                stop = true;
+                order_dependent = true;
+            }
+            undiscovered &= ~newly;
+
+            // 2. target_state_count: the reference checks it after each 1500-pop block (bfs.rs:113-135).
+            bool target_stop = false;
+            if (o_.target_state_count && state_count + limit * D_ >= o_.target_state_count) {
+                u64 lt = target_limit(n, popped_before, limit);
+                if (lt != ~0ull) {
+                    limit = lt;
+                    visited = lt;
+                    target_stop = true;
+                    stop = true;
+                    order_dependent = true;
+                }
+            }
+
+            if (o_.record_visits && visited) {
+                size_t o = visits_.size();
+                visits_.resize(o + visited * W);
+                SR_HIP(hipMemcpy(&visits_[o], cur_.p, visited * W * sizeof(u64), hipMemcpyDeviceToHost));
+            }
+
+            // 3. Expand ranks [0, limit).
+            u64 produced = 0;
+            if (limit) {
+                produced = expand_level(level, n, limit, undiscovered);
+            } else {
+                std::memset(&lc_, 0, sizeof(lc_));
+            }
+            state_count += lc_.successors;
+            unique += lc_.claims;
+            stats.successors += lc_.successors;
+            stats.algorithmic_bytes += limit * 8 * W + lc_.successors * 8 + (u64)lc_.claims * (16 + 8 * W);
+            stats.levels++;
+            if (produced) max_depth = level + 1;
+            if (o_.verbose)
+                std::fprintf(stderr, "[sr] level %u: frontier %llu expanded %llu succ %llu new %llu unique %llu cap %llu\n",
+                             level, (unsigned long long)n, (unsigned long long)limit,
+                             (unsigned long long)lc_.successors, (unsigned long long)produced,
+                             (unsigned long long)unique.load(), (unsigned long long)cap_);
+            popped_before += visited;
+            if (stop || produced == 0) {
+                if (target_stop) reference_done = false;  // the worker returns without waiting
+                else if (stop) reference_done = true;     // all properties discovered
+                else  // exhausted: the last (partial) block still checks the target (bfs.rs:129-135)
+                    reference_done = !(o_.target_state_count && state_count >= o_.target_state_count);
+                break;
+            }
+            cur_.swap(next_);
+            n = produced;
+            ++level;
+        }
+        auto t_end = Clock::now();
+        stats.level_loop_sec = secs(t_loop, t_end);
+        stats.total_sec = secs(t_start, t_end);
+        stats.table_capacity = cap_;
+        return order_dependent && !fifo_;
+    }
+
+    // Smallest 1500-pop block boundary inside this level at which state_count >= target.
+    u64 target_limit(u64 n, u64 popped_before, u64 limit) {
+        DBuf<u32> counts;
+        counts.alloc(o_.device, n);
+        count_successors<M><<<blocks_for(n, 256), 256, 0, stream_>>>(m_, cur_.p, (u32)n, counts.p);
+        SR_HIP(hipGetLastError());
+        std::vector<u32> h(n);
+        SR_HIP(hipMemcpyAsync(h.data(), counts.p, n * sizeof(u32), hipMemcpyDeviceToHost, stream_));
+        SR_HIP(hipStreamSynchronize(stream_));
+        u64 sc = state_count;
+        u64 r = 0;
+        for (u64 k = popped_before / 1500 + 1;; ++k) {
+            u64 b = k * 1500 - popped_before;  // pops of this level at the block boundary
+            if (b > n || b > limit) return ~0ull;
+            for (; r < b; ++r) sc += h[r];
+            if (sc >= o_.target_state_count) return b;
+        }
+    }
+
+    // Expands frontier ranks [0, limit) of `level` into next_; returns the next frontier size.
+    u64 expand_level(u32 level, u64 n, u64 limit, u32 undiscovered) {
+        const u32 A = A_;  // action slots (FIFO candidate layout)
+        reset_counters();
+        u64 claims = 0;
+        DBuf<u32> cand;
+        if (fifo_) {
+            cand.alloc(o_.device, limit * A);
+            SR_HIP(hipMemsetAsync(cand.p, 0xff, limit * A * sizeof(u32), stream_));
+        }
+        for (u64 lo = 0; lo < limit;) {
+            // Chunk so the visited set stays under 75% load even if every successor is new.
+            u64 head = (u64)(0.8 * (double)cap_) - std::min<u64>((u64)(0.8 * (double)cap_), unique + claims);
+            u64 c = std::min<u64>(limit - lo, head / std::max<u32>(D_, 1));
+            if (c < std::min<u64>(limit - lo, 1u << 16)) {
+                grow_table(fifo_ ? cand.p : nullptr, fifo_ ? limit * A : 0);
+                continue;
+            }
+            if (!fifo_) ensure_frontier(next_, claims + c * D_, claims);
+            const u32 ulo = (u32)lo, uhi = (u32)(lo + c);
+            if (fifo_) {
+                timed([&] {
+                    expand_fifo<M><<<blocks_for(c, 256), 256, 0, stream_>>>(m_, cur_.p, ulo, uhi, (u32)limit, view(), cand.p, A, level, lc_d_);
+                });
+            } else {
+                timed([&] {
+                    expand_fast<M><<<blocks_for(c, 256), 256, 0, stream_>>>(m_, cur_.p, ulo, uhi, view(), next_.p,
+                                                                            (u32)std::min<u64>(next_.n / W, 0xffffffffu), lc_d_, undiscovered);
+                });
+            }
+            read_counters();
+            claims = lc_.claims;
+            lo += c;
+        }
+        if (!fifo_) return claims;
+
+        // FIFO passes 2-3: owners per parent, exclusive scan, ordered scatter.
+        ensure_frontier(next_, claims, 0);
+        DBuf<u32> counts, offs, sums, total;
+        counts.alloc(o_.device, limit);
+        offs.alloc(o_.device, limit);
+        u32 tiles = blocks_for(limit, SCAN_TILE);
+        sums.alloc(o_.device, tiles);
+        total.alloc(o_.device, 1);
+        timed([&] { own_count<M><<<blocks_for(limit, 256), 256, 0, stream_>>>(cand.p, (u32)limit, A, level, view(), counts.p); });
+        scan_tile_sums<<<tiles, SCAN_BLOCK, 0, stream_>>>(counts.p, (u32)limit, sums.p);
+        scan_sums<<<1, SCAN_BLOCK, 0, stream_>>>(sums.p, tiles, total.p);
+        scan_tiles<<<tiles, SCAN_BLOCK, 0, stream_>>>(counts.p, (u32)limit, sums.p, offs.p);
+        SR_HIP(hipGetLastError());
+        timed([&] {
+            scatter_fifo<M><<<blocks_for(limit, 256), 256, 0, stream_>>>(m_, cur_.p, cand.p, offs.p, (u32)limit, A, level,
+                                                                         view(), next_.p, lc_d_, undiscovered);
+        });
+        u32 owners = 0;
+        SR_HIP(hipMemcpyAsync(&owners, total.p, sizeof(u32), hipMemcpyDeviceToHost, stream_));
+        read_counters();
+        if (owners != claims) throw Error(SR_ERR_CAPACITY, "FIFO ownership mismatch: owners " + std::to_string(owners) + " claims " + std::to_string(claims));
+        return owners;
+    }
+
+    M m_;
+    sr_opts o_;
+    u32 A_;  // action slots
+    u32 D_;  // max successors of one state (bounds the new states a chunk can create)
+    bool fifo_ = false;
+    hipStream_t stream_ = nullptr;
+    hipEvent_t ev0_ = nullptr, ev1_ = nullptr;
+    LevelCounters lc_{};
+    LevelCounters* lc_d_ = nullptr;
+    u64 cap_ = 0;
+    DBuf<u64> keys_, parents_, meta_, cur_, next_;
+    std::vector<u64> visits_;
+};
+
+static std::unique_ptr<EngineBase> make_engine(int model, const i64* p, int np, const sr_opts& o) {
+    auto need = [&](int k) {
+        if (np < k) throw Error(SR_ERR_ARG, "model " + std::to_string(model) + " needs " + std::to_string(k) + " params");
+    };
+    switch (model) {
+        case SR_MODEL_LINEAR_EQUATION:
+            need(3);
+            return std::make_unique<Engine<LinearEquation>>(LinearEquation{(u32)(p[0] & 0xff), (u32)(p[1] & 0xff), (u32)(p[2] & 0xff)}, o);
+        case SR_MODEL_BINARY_CLOCK:
+            return std::make_unique<Engine<BinaryClock>>(BinaryClock{}, o);
+        case SR_MODEL_2PC:
+            need(1);
+            if (p[0] < 1 || p[0] > 14) throw Error(SR_ERR_UNSUPPORTED, "2pc: rm_count must be in 1..=14 (4n+4 <= 63 bits)");
+            return std::make_unique<Engine<TwoPhase>>(TwoPhase{(int)p[0]}, o);
+        case SR_MODEL_INCREMENT:
+            need(1);
+            if (p[0] < 1 || p[0] > 15) throw Error(SR_ERR_UNSUPPORTED, "increment: threads must be in 1..=15");
+            if (p[0] <= 9) return std::make_unique<Engine<Increment<1>>>(Increment<1>{(int)p[0]}, o);
+            return std::make_unique<Engine<Increment<2>>>(Increment<2>{(int)p[0]}, o);
+        case SR_MODEL_INCREMENT_LOCK:
+            need(1);
+            if (p[0] < 1 || p[0] > 12) throw Error(SR_ERR_UNSUPPORTED, "increment_lock: threads must be in 1..=12");
+            if (p[0] <= 8) return std::make_unique<Engine<IncrementLock<1>>>(IncrementLock<1>{(int)p[0]}, o);
+            return std::make_unique<Engine<IncrementLock<2>>>(IncrementLock<2>{(int)p[0]}, o);
+        case SR_MODEL_DGRAPH:
+            throw Error(SR_ERR_UNSUPPORTED, "dgraph: `eventually` properties are not supported by the GPU engine yet");
+    }
+    throw Error(SR_ERR_ARG, "unknown model id " + std::to_string(model));
+}
+
+}  // namespace sr
+
+using namespace sr;
+
+struct sr_bfs {
+    std::unique_ptr<EngineBase> e;
+    std::thread th;
+    bool joined = false;
+};
+
+extern "C" {
+
+void sr_opts_init(sr_opts* o) {
+    std::memset(o, 0, sizeof(*o));
+    o->struct_size = sizeof(sr_opts);
+}
+
+const char* sr_last_error(void) { return g_last_error.c_str(); }
+
+int sr_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+sr_bfs* sr_gpu_bfs_spawn(int32_t model_id, const int64_t* params, int32_t nparams, const sr_opts* opts) {
+    try {
+        sr_opts o;
+        sr_opts_init(&o);
+        if (opts) std::memcpy(&o, opts, std::min<size_t>(sizeof(o), opts->struct_size ? opts->struct_size : sizeof(o)));
+        if (sr_device_count() <= 0) throw Error(SR_ERR_NO_DEVICE, "no HIP device visible");
+        auto b = std::make_unique<sr_bfs>();
+        b->e = make_engine(model_id, params, nparams, o);
+        EngineBase* e = b->e.get();
+        b->th = std::thread([e] {
+            try {
+                e->run();
+            } catch (const Error& x) {
+                e->status = x.code;
+                e->error = x.what();
+            } catch (const std::exception& x) {
+                e->status = SR_ERR_HIP;
+                e->error = x.what();
+            }
+            e->finished = true;
+        });
+        return b.release();
+    } catch (const Error& x) {
+        set_error(x.what());
+        return nullptr;
+    } catch (const std::exception& x) {
+        set_error(x.what());
+        return nullptr;
+    }
+}
+
+int32_t sr_gpu_bfs_join(sr_bfs* b) {
+    if (!b) return SR_ERR_ARG;
+    if (!b->joined) {
+        b->th.join();
+        b->joined = true;
+    }
+    if (b->e->status != SR_OK) set_error(b->e->error);
+    return b->e->status;
+}
+
+int32_t sr_gpu_bfs_is_done(const sr_bfs* b) { return b && b->e->finished && b->e->reference_done ? 1 : 0; }
+int32_t sr_gpu_bfs_is_running(const sr_bfs* b) { return b && !b->e->finished ? 1 : 0; }
+uint64_t sr_gpu_bfs_state_count(const sr_bfs* b) { return b ? b->e->state_count.load() : 0; }
+uint64_t sr_gpu_bfs_unique_state_count(const sr_bfs* b) { return b ? b->e->unique.load() : 0; }
+uint32_t sr_gpu_bfs_max_depth(const sr_bfs* b) { return b ? b->e->max_depth.load() : 0; }
+
+int32_t sr_gpu_bfs_stats(const sr_bfs* b, sr_stats* out) {
+    if (!b || !out) return SR_ERR_ARG;
+    *out = b->e->stats;
+    return SR_OK;
+}
+
+int32_t sr_gpu_bfs_property_count(const sr_bfs* b) { return b ? b->e->nprops() : 0; }
+
+int32_t sr_gpu_bfs_property(const sr_bfs* b, int32_t p, char* name, int32_t cap, int32_t* expectation) {
+    if (!b || p < 0 || p >= b->e->nprops()) return SR_ERR_ARG;
+    const char* n = b->e->prop_name(p);
+    if (name && cap > 0) std::snprintf(name, (size_t)cap, "%s", n);
+    if (expectation) *expectation = b->e->expectation(p);
+    return (int32_t)std::strlen(n);
+}
+
+int32_t sr_gpu_bfs_discovery(const sr_bfs* b, int32_t p, uint64_t* fp_chain, uint32_t cap) {
+    try {
+        if (!b) return SR_ERR_ARG;
+        std::vector<u64> c;
+        b->e->chain(p, c);
+        if (fp_chain) std::memcpy(fp_chain, c.data(), std::min<size_t>(cap, c.size()) * sizeof(u64));
+        return (int32_t)c.size();
+    } catch (const Error& x) {
+        set_error(x.what());
+        return x.code;
+    }
+}
+
+int32_t sr_gpu_bfs_discovery_path(const sr_bfs* b, int32_t p, int64_t* action_ids, int32_t cap_actions,
+                                  int64_t* states, int64_t cap_states) {
+    try {
+        if (!b) return SR_ERR_ARG;
+        std::vector<i64> a, s;
+        int n = b->e->path(p, a, s);
+        if (n < 0) return -1;
+        if (action_ids) std::memcpy(action_ids, a.data(), std::min<size_t>((size_t)cap_actions, a.size()) * sizeof(i64));
+        if (states) std::memcpy(states, s.data(), std::min<size_t>((size_t)cap_states, s.size()) * sizeof(i64));
+        return n;
+    } catch (const Error& x) {
+        set_error(x.what());
+        return x.code;
+    }
+}
+
+int32_t sr_gpu_bfs_describe_width(const sr_bfs* b) { return b ? b->e->width() : 0; }
+
+int32_t sr_gpu_bfs_action_name(const sr_bfs* b, int64_t id, char* buf, int32_t cap) {
+    if (!b) return SR_ERR_ARG;
+    std::string s = b->e->action_name(id);
+    if (buf && cap > 0) std::snprintf(buf, (size_t)cap, "%s", s.c_str());
+    return (int32_t)s.size();
+}
+
+int64_t sr_gpu_bfs_visits(const sr_bfs* b, int64_t* out, int64_t cap) {
+    if (!b) return SR_ERR_ARG;
+    auto v = b->e->visits();
+    if (out) std::memcpy(out, v.data(), (size_t)std::min<int64_t>(cap, (int64_t)v.size()) * sizeof(int64_t));
+    return (int64_t)v.size();
+}
+
+int64_t sr_gpu_bfs_action_id_bound(const sr_bfs* b) { return b ? b->e->action_id_bound() : 0; }
+int32_t sr_gpu_bfs_init_count(const sr_bfs* b) { return b ? b->e->init_count() : 0; }
+
+int32_t sr_gpu_bfs_replay(const sr_bfs* b, int32_t init, const int64_t* ids, int32_t n, int64_t* states, int64_t cap_states,
+                          int32_t* conds, int32_t cap_conds) {
+    if (!b) return SR_ERR_ARG;
+    std::vector<i64> s;
+    std::vector<int> c;
+    int r = b->e->replay(init, ids, n, s, c);
+    if (r < 0) return -1;
+    if (states) std::memcpy(states, s.data(), (size_t)std::min<int64_t>(cap_states, (int64_t)s.size()) * sizeof(int64_t));
+    for (int i = 0; i < (int)c.size() && i < cap_conds; ++i) conds[i] = c[i];
+    return r;
+}
+
+void sr_gpu_bfs_free(sr_bfs* b) {
+    if (!b) return;
+    if (!b->joined && b->th.joinable()) b->th.join();
+    delete b;
+}
+
+}  // extern "C"

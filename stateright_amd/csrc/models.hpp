@@ -1,0 +1,349 @@
+// GpuModel encodings: the device-side counterpart of `impl Model for X` (src/lib.rs:155-237).
+//
+// A GpuModel packs one state into W 64-bit words (equal states <=> equal words) and exposes the
+// reference's `actions()` list as ACTION SLOTS 0..max_actions-1 in the reference's own order:
+//   enabled(s, mask)   bit a of mask = slot a appears in `actions(s)`
+//   apply(s, a, out)   `next_state(s, action)` is Some AND `within_boundary` holds -> out
+//   discovers(p, s)    property p yields a discovery at s (always: !cond, sometimes: cond)
+// Host-only helpers give init states, property names/expectations, the canonical description of a
+// state (shared with the CPU oracle for set/order/path comparison) and canonical action ids.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace sr {
+
+using u8 = uint8_t;
+using u32 = uint32_t;
+using u64 = uint64_t;
+using i64 = int64_t;
+
+#define SR_HD __host__ __device__ __forceinline__
+
+enum Expect { ALWAYS = 0, EVENTUALLY = 1, SOMETIMES = 2 };
+
+// murmur3 fmix64: a bijection on u64 with fmix64(0) == 0.
+SR_HD u64 fmix64(u64 k) {
+    k ^= k >> 33;
+    k *= 0xff51afd7ed558ccdull;
+    k ^= k >> 33;
+    k *= 0xc4ceb9fe1a85ec53ull;
+    k ^= k >> 33;
+    return k;
+}
+
+// 64-bit state fingerprint (`fingerprint`, src/lib.rs:306-311). For W == 1 the packed state
+// uses at most 63 bits, so XOR-ing bit 63 and mixing is a BIJECTION that is never zero: the
+// visited set is then exact (no fingerprint collisions at all). For W > 1 it is a 64-bit hash
+// like the reference's (collisions possible at ~n^2/2^65); zero is remapped to 1 where the
+// reference would panic (src/lib.rs:310).
+template <int W>
+SR_HD u64 fingerprint(const u64* s) {
+    if constexpr (W == 1) {
+        return fmix64(s[0] ^ 0x8000000000000000ull);
+    } else {
+        u64 h = 0x9E3779B97F4A7C15ull;
+#pragma unroll
+        for (int i = 0; i < W; ++i) h = fmix64(h ^ (s[i] + 0x632BE59BD9B4E019ull * (u64)(i + 1)));
+        return h ? h : 1;
+    }
+}
+
+SR_HD u64 getb(const u64* s, int off, int width) {
+    // bit field [off, off+width) of a little-endian multi-word state; width <= 8, no word crossing
+    return (s[off >> 6] >> (off & 63)) & ((1ull << width) - 1);
+}
+SR_HD void setb(u64* s, int off, int width, u64 v) {
+    u64 m = ((1ull << width) - 1) << (off & 63);
+    s[off >> 6] = (s[off >> 6] & ~m) | ((v << (off & 63)) & m);
+}
+
+// -----------------------------------------------------------------------------------------------
+// LinearEquation (src/test_util.rs:140-188): state (x: u8, y: u8); actions IncreaseX, IncreaseY.
+// -----------------------------------------------------------------------------------------------
+struct LinearEquation {
+    static constexpr int W = 1, MW = 1, NPROPS = 1;
+    u32 a, b, c;
+    int max_actions() const { return 2; }
+    int max_out_degree() const { return 2; }
+    SR_HD void enabled(const u64*, u64* m) const { m[0] = 3; }
+    SR_HD bool apply(const u64* s, int a_, u64* o) const {
+        u64 x = s[0] & 0xff, y = (s[0] >> 8) & 0xff;
+        if (a_ == 0) x = (x + 1) & 0xff; else y = (y + 1) & 0xff;
+        o[0] = x | (y << 8);
+        return true;
+    }
+    SR_HD bool discovers(int, const u64* s) const {  // sometimes "solvable": a*x + b*y == c (u8)
+        u64 x = s[0] & 0xff, y = (s[0] >> 8) & 0xff;
+        return ((a * x + b * y) & 0xff) == c;
+    }
+    int init_states(u64* out) const { out[0] = 0; return 1; }
+    int expectation(int) const { return SOMETIMES; }
+    const char* prop_name(int) const { return "solvable"; }
+    int describe_width() const { return 2; }
+    void describe(const u64* s, i64* d) const { d[0] = (i64)(s[0] & 0xff); d[1] = (i64)((s[0] >> 8) & 0xff); }
+    i64 action_id(const u64*, int a_) const { return a_; }
+    std::string action_name(i64 id) const { return id == 0 ? "IncreaseX" : "IncreaseY"; }
+    i64 action_id_bound() const { return 2; }
+};
+
+// -----------------------------------------------------------------------------------------------
+// BinaryClock (src/test_util.rs:4-45): i8 state in {0, 1}; one action (GoHigh at 0, GoLow at 1).
+// -----------------------------------------------------------------------------------------------
+struct BinaryClock {
+    static constexpr int W = 1, MW = 1, NPROPS = 1;
+    int max_actions() const { return 1; }
+    int max_out_degree() const { return 1; }
+    SR_HD void enabled(const u64*, u64* m) const { m[0] = 1; }
+    SR_HD bool apply(const u64* s, int, u64* o) const { o[0] = (s[0] & 0xff) == 0 ? 1 : 0; return true; }
+    SR_HD bool discovers(int, const u64* s) const {  // always "in [0, 1]"
+        int8_t v = (int8_t)(s[0] & 0xff);
+        return !(0 <= v && v <= 1);
+    }
+    int init_states(u64* out) const { out[0] = 0; out[1] = 1; return 2; }
+    int expectation(int) const { return ALWAYS; }
+    const char* prop_name(int) const { return "in [0, 1]"; }
+    int describe_width() const { return 1; }
+    void describe(const u64* s, i64* d) const { d[0] = (int8_t)(s[0] & 0xff); }
+    i64 action_id(const u64* s, int) const { return (s[0] & 0xff) == 0 ? 1 : 0; }  // GoLow=0, GoHigh=1
+    std::string action_name(i64 id) const { return id == 0 ? "GoLow" : "GoHigh"; }
+    i64 action_id_bound() const { return 2; }
+};
+
+// -----------------------------------------------------------------------------------------------
+// Two-phase commit (examples/2pc.rs:10-121), n <= 14 resource managers, 4n+4 bits:
+//   [0,2n)      rm_state[rm]   (Working 0, Prepared 1, Committed 2, Aborted 3)
+//   [2n,2n+2)   tm_state       (Init 0, Committed 1, Aborted 2)
+//   [2n+2,3n+2) tm_prepared[rm]
+//   [3n+2,4n+2) msgs ∋ Prepared{rm}
+//   4n+2        msgs ∋ Commit;  4n+3  msgs ∋ Abort
+// Slots follow `actions()` (examples/2pc.rs:56-81): 0 TmCommit, 1 TmAbort, then for each rm
+// 2+5rm+{0 TmRcvPrepared, 1 RmPrepare, 2 RmChooseToAbort, 3 RmRcvCommitMsg, 4 RmRcvAbortMsg}.
+// Every action returns Some (examples/2pc.rs:83-104), self-loops included.
+// -----------------------------------------------------------------------------------------------
+struct TwoPhase {
+    static constexpr int W = 1, MW = 2, NPROPS = 3;
+    int n;
+    int max_actions() const { return 2 + 5 * n; }
+    // Per rm at most three of its five slots (a Working rm after TmAbort: Prepare, ChooseToAbort,
+    // RcvAbort); TmCommit/TmAbort only while the TM is Init (then at most two per rm).
+    int max_out_degree() const { return 2 + 3 * n; }
+    SR_HD u64 rmask() const { return (1ull << n) - 1; }
+    // per-rm bit vectors
+    SR_HD u64 working(u64 s) const {  // rm_state == 0
+        u64 w = 0;
+        for (int rm = 0; rm < n; ++rm) w |= (u64)(((s >> (2 * rm)) & 3) == 0) << rm;
+        return w;
+    }
+    SR_HD void enabled(const u64* sp, u64* m) const {
+        u64 s = sp[0];
+        u64 tm = (s >> (2 * n)) & 3;
+        u64 prepared = (s >> (2 * n + 2)) & rmask();
+        u64 msgp = (s >> (3 * n + 2)) & rmask();
+        u64 commit = (s >> (4 * n + 2)) & 1, abort = (s >> (4 * n + 3)) & 1;
+        u64 work = working(s);
+        u64 lo = 0, hi = 0;
+        auto set = [&](int a) { if (a < 64) lo |= 1ull << a; else hi |= 1ull << (a - 64); };
+        if (tm == 0 && prepared == rmask()) set(0);
+        if (tm == 0) set(1);
+        for (int rm = 0; rm < n; ++rm) {
+            int b = 2 + 5 * rm;
+            if (tm == 0 && ((msgp >> rm) & 1)) set(b);
+            if ((work >> rm) & 1) { set(b + 1); set(b + 2); }
+            if (commit) set(b + 3);
+            if (abort) set(b + 4);
+        }
+        m[0] = lo;
+        m[1] = hi;
+    }
+    SR_HD bool apply(const u64* sp, int a, u64* o) const {
+        u64 s = sp[0];
+        if (a == 0) {  // TmCommit
+            s = (s & ~(3ull << (2 * n))) | (1ull << (2 * n));
+            s |= 1ull << (4 * n + 2);
+        } else if (a == 1) {  // TmAbort
+            s = (s & ~(3ull << (2 * n))) | (2ull << (2 * n));
+            s |= 1ull << (4 * n + 3);
+        } else {
+            int rm = (a - 2) / 5, k = (a - 2) % 5;
+            u64 clr = ~(3ull << (2 * rm));
+            switch (k) {
+                case 0: s |= 1ull << (2 * n + 2 + rm); break;                               // TmRcvPrepared
+                case 1: s = (s & clr) | (1ull << (2 * rm)); s |= 1ull << (3 * n + 2 + rm); break;  // RmPrepare
+                case 2: s = (s & clr) | (3ull << (2 * rm)); break;                          // RmChooseToAbort
+                case 3: s = (s & clr) | (2ull << (2 * rm)); break;                          // RmRcvCommitMsg
+                default: s = (s & clr) | (3ull << (2 * rm)); break;                         // RmRcvAbortMsg
+            }
+        }
+        o[0] = s;
+        return true;
+    }
+    SR_HD bool discovers(int p, const u64* sp) const {
+        u64 s = sp[0];
+        u64 aborted = 0, committed = 0;
+        for (int rm = 0; rm < n; ++rm) {
+            u64 r = (s >> (2 * rm)) & 3;
+            aborted |= (u64)(r == 3) << rm;
+            committed |= (u64)(r == 2) << rm;
+        }
+        if (p == 0) return aborted == rmask();         // sometimes "abort agreement"
+        if (p == 1) return committed == rmask();       // sometimes "commit agreement"
+        return aborted != 0 && committed != 0;         // always "consistent" violated
+    }
+    int init_states(u64* out) const { out[0] = 0; return 1; }
+    int expectation(int p) const { return p == 2 ? ALWAYS : SOMETIMES; }
+    const char* prop_name(int p) const {
+        return p == 0 ? "abort agreement" : p == 1 ? "commit agreement" : "consistent";
+    }
+    int describe_width() const { return 3 * n + 3; }
+    void describe(const u64* sp, i64* d) const {
+        u64 s = sp[0];
+        int k = 0;
+        for (int rm = 0; rm < n; ++rm) d[k++] = (i64)((s >> (2 * rm)) & 3);
+        d[k++] = (i64)((s >> (2 * n)) & 3);
+        for (int rm = 0; rm < n; ++rm) d[k++] = (i64)((s >> (2 * n + 2 + rm)) & 1);
+        for (int rm = 0; rm < n; ++rm) d[k++] = (i64)((s >> (3 * n + 2 + rm)) & 1);
+        d[k++] = (i64)((s >> (4 * n + 2)) & 1);
+        d[k++] = (i64)((s >> (4 * n + 3)) & 1);
+    }
+    i64 action_id(const u64*, int a) const { return a; }
+    i64 action_id_bound() const { return 2 + 5 * n; }
+    std::string action_name(i64 id) const {
+        if (id == 0) return "TmCommit";
+        if (id == 1) return "TmAbort";
+        const char* names[] = {"TmRcvPrepared", "RmPrepare", "RmChooseToAbort", "RmRcvCommitMsg", "RmRcvAbortMsg"};
+        return std::string(names[(id - 2) % 5]) + "(" + std::to_string((id - 2) / 5) + ")";
+    }
+};
+
+// -----------------------------------------------------------------------------------------------
+// Increment (examples/increment.rs:109-197), n <= 15 threads: i (4 bits) then per thread
+// t (4 bits) + pc (2 bits, values 1..3). 4+6n bits; W = 1 for n <= 9, else 2.
+// Slot = thread id (each thread has at most one enabled action: Read at pc 1, Write at pc 2).
+// -----------------------------------------------------------------------------------------------
+template <int W_>
+struct Increment {
+    static constexpr int W = W_, MW = 1, NPROPS = 1;
+    int n;
+    int max_actions() const { return n; }
+    int max_out_degree() const { return n; }
+    SR_HD static int toff(int t) { return 4 + 6 * t; }
+    SR_HD void enabled(const u64* s, u64* m) const {
+        u64 r = 0;
+        for (int t = 0; t < n; ++t) {
+            u64 pc = getb(s, toff(t) + 4, 2);
+            r |= (u64)(pc == 1 || pc == 2) << t;
+        }
+        m[0] = r;
+    }
+    SR_HD bool apply(const u64* s, int t, u64* o) const {
+#pragma unroll
+        for (int i = 0; i < W; ++i) o[i] = s[i];
+        u64 pc = getb(s, toff(t) + 4, 2);
+        if (pc == 1) {  // Read: s[t] = {t: i, pc: 2}
+            setb(o, toff(t), 4, getb(s, 0, 4));
+            setb(o, toff(t) + 4, 2, 2);
+        } else {  // Write: pc = 3; i = t + 1
+            setb(o, toff(t) + 4, 2, 3);
+            setb(o, 0, 4, getb(s, toff(t), 4) + 1);
+        }
+        return true;
+    }
+    SR_HD bool discovers(int, const u64* s) const {  // always "fin": #(pc == 3) == i
+        u64 c = 0;
+        for (int t = 0; t < n; ++t) c += getb(s, toff(t) + 4, 2) == 3;
+        return c != getb(s, 0, 4);
+    }
+    int init_states(u64* out) const {
+        for (int i = 0; i < W; ++i) out[i] = 0;
+        for (int t = 0; t < n; ++t) setb(out, toff(t) + 4, 2, 1);
+        return 1;
+    }
+    int expectation(int) const { return ALWAYS; }
+    const char* prop_name(int) const { return "fin"; }
+    int describe_width() const { return 1 + 2 * n; }
+    void describe(const u64* s, i64* d) const {
+        d[0] = (i64)getb(s, 0, 4);
+        for (int t = 0; t < n; ++t) {
+            d[1 + 2 * t] = (i64)getb(s, toff(t), 4);
+            d[2 + 2 * t] = (i64)getb(s, toff(t) + 4, 2);
+        }
+    }
+    i64 action_id(const u64* s, int t) const { return 2 * t + (getb(s, toff(t) + 4, 2) == 2 ? 1 : 0); }
+    i64 action_id_bound() const { return 2 * n; }
+    std::string action_name(i64 id) const {
+        return std::string(id % 2 ? "Write(" : "Read(") + std::to_string(id / 2) + ")";
+    }
+};
+
+// -----------------------------------------------------------------------------------------------
+// IncrementLock (examples/increment_lock.rs:3-107), n <= 12 threads: i (4 bits), lock (1 bit),
+// then per thread t (4 bits) + pc (3 bits, 0..4); 5+7n bits, W = 1 for n <= 8, else 2.
+// Per-thread fields are placed so that none crosses a word boundary.
+// -----------------------------------------------------------------------------------------------
+template <int W_>
+struct IncrementLock {
+    static constexpr int W = W_, MW = 1, NPROPS = 2;
+    int n;
+    int max_actions() const { return n; }
+    int max_out_degree() const { return n; }
+    // threads 0..7 live in word 0 (bits 5..60), threads 8.. in word 1 (bits 0..)
+    SR_HD static int toff(int t) { return t < 8 ? 5 + 7 * t : 64 + 7 * (t - 8); }
+    SR_HD void enabled(const u64* s, u64* m) const {
+        u64 lock = getb(s, 4, 1), r = 0;
+        for (int t = 0; t < n; ++t) {
+            u64 pc = getb(s, toff(t) + 4, 3);
+            bool en = (pc == 0 && !lock) || pc == 1 || pc == 2 || (pc == 3 && lock);
+            r |= (u64)en << t;
+        }
+        m[0] = r;
+    }
+    SR_HD bool apply(const u64* s, int t, u64* o) const {
+#pragma unroll
+        for (int i = 0; i < W; ++i) o[i] = s[i];
+        u64 pc = getb(s, toff(t) + 4, 3);
+        switch (pc) {
+            case 0: setb(o, toff(t) + 4, 3, 1); setb(o, 4, 1, 1); break;                    // Lock
+            case 1: setb(o, toff(t) + 4, 3, 2); setb(o, toff(t), 4, getb(s, 0, 4)); break;  // Read
+            case 2: setb(o, toff(t) + 4, 3, 3); setb(o, 0, 4, getb(s, toff(t), 4) + 1); break; // Write
+            default: setb(o, toff(t) + 4, 3, 4); setb(o, 4, 1, 0); break;                  // Release
+        }
+        return true;
+    }
+    SR_HD bool discovers(int p, const u64* s) const {
+        u64 fin = 0, crit = 0;
+        for (int t = 0; t < n; ++t) {
+            u64 pc = getb(s, toff(t) + 4, 3);
+            fin += pc >= 3;
+            crit += pc >= 1 && pc < 4;
+        }
+        if (p == 0) return fin != getb(s, 0, 4);  // always "fin"
+        return crit > 1;                          // always "mutex"
+    }
+    int init_states(u64* out) const {
+        for (int i = 0; i < W; ++i) out[i] = 0;
+        return 1;
+    }
+    int expectation(int) const { return ALWAYS; }
+    const char* prop_name(int p) const { return p == 0 ? "fin" : "mutex"; }
+    int describe_width() const { return 2 + 2 * n; }
+    void describe(const u64* s, i64* d) const {
+        d[0] = (i64)getb(s, 0, 4);
+        d[1] = (i64)getb(s, 4, 1);
+        for (int t = 0; t < n; ++t) {
+            d[2 + 2 * t] = (i64)getb(s, toff(t), 4);
+            d[3 + 2 * t] = (i64)getb(s, toff(t) + 4, 3);
+        }
+    }
+    i64 action_id(const u64* s, int t) const { return 4 * t + (i64)getb(s, toff(t) + 4, 3); }
+    i64 action_id_bound() const { return 4 * n; }
+    std::string action_name(i64 id) const {
+        const char* names[] = {"Lock", "Read", "Write", "Release"};
+        return std::string(names[id % 4]) + "(" + std::to_string(id / 4) + ")";
+    }
+};
+
+}  // namespace sr

@@ -1,0 +1,62 @@
+"""CPU-side checks of the drop-in boundary: the C-ABI library loads and exports every symbol that
+include/stateright_gpu.h declares (no compute calls: there is no GPU here)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "stateright_gpu.h")
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r"\b(sr_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_header_declares_entry_points():
+    names = declared_functions()
+    for must in ("sr_gpu_bfs_spawn", "sr_gpu_bfs_join", "sr_gpu_bfs_is_done", "sr_gpu_bfs_state_count",
+                 "sr_gpu_bfs_unique_state_count", "sr_gpu_bfs_max_depth", "sr_gpu_bfs_discovery",
+                 "sr_gpu_bfs_free"):
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol():
+    from stateright_amd import _native
+    lib = _native.load()
+    for name in declared_functions():
+        assert hasattr(lib, name), f"{name} declared in the header but not exported"
+
+
+def test_python_signatures_match_header():
+    from stateright_amd import _native
+    bound = {n for n, _, _ in _native.SIGNATURES}
+    assert bound == set(declared_functions())
+
+
+def test_struct_layouts():
+    from stateright_amd import _native
+    lib = _native.load()
+    o = _native.sr_opts()
+    lib.sr_opts_init(ctypes.byref(o))
+    assert o.struct_size == ctypes.sizeof(_native.sr_opts)
+
+
+def test_spawn_without_device_fails_loudly():
+    from stateright_amd import TwoPhaseSys, CheckerError
+    from stateright_amd import _native
+    if _native.load().sr_device_count() > 0:
+        pytest.skip("a GPU is visible")
+    with pytest.raises(CheckerError):
+        TwoPhaseSys(3).checker().spawn_bfs()
+
+
+def test_unsupported_parameters_rejected():
+    from stateright_amd import _native
+    lib = _native.load()
+    if lib.sr_device_count() > 0:
+        pytest.skip("a GPU is visible; covered by the gpu tests")
+    arr = (ctypes.c_int64 * 1)(99)
+    assert not lib.sr_gpu_bfs_spawn(_native.SR_MODEL_2PC, arr, 1, None)
