@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstring>
 #include <map>
 #include <mutex>
 #include <stdexcept>
@@ -106,6 +107,70 @@ struct DBuf {
         std::swap(n, o.n);
         std::swap(dev, o.dev);
     }
+};
+
+// A per-device execution context, created once and reused by every check on that device: the
+// stream, the device counters, the pinned host mirror they are published to, and a pool of HIP
+// events for per-launch timing. Contexts are pooled (a context is used by one check at a time).
+template <class Counters, class HostMirror>
+struct DeviceContext {
+    int dev = 0;
+    hipStream_t stream = nullptr;
+    Counters* lc = nullptr;        // device
+    HostMirror* hc = nullptr;      // pinned, host pointer
+    HostMirror* hc_dev = nullptr;  // the same memory, device pointer
+    uint32_t seq = 0;
+    std::vector<hipEvent_t> events;
+
+    void init(int d) {
+        dev = d;
+        SR_HIP(hipSetDevice(d));
+        SR_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+        SR_HIP(hipMalloc(&lc, sizeof(Counters)));
+        SR_HIP(hipHostMalloc(&hc, sizeof(HostMirror), hipHostMallocCoherent | hipHostMallocMapped));
+        SR_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&hc_dev), hc, 0));
+        std::memset(hc, 0, sizeof(HostMirror));
+    }
+    hipEvent_t event(size_t i) {
+        while (events.size() <= i) {
+            hipEvent_t e;
+            SR_HIP(hipEventCreate(&e));
+            events.push_back(e);
+        }
+        return events[i];
+    }
+};
+
+template <class Ctx>
+class ContextPool {
+  public:
+    static ContextPool& get() {
+        static ContextPool p;
+        return p;
+    }
+    Ctx* acquire(int dev) {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            auto& fl = free_[dev];
+            if (!fl.empty()) {
+                Ctx* c = fl.back();
+                fl.pop_back();
+                return c;
+            }
+        }
+        auto* c = new Ctx();
+        c->init(dev);
+        return c;
+    }
+    void release(Ctx* c) {
+        if (!c) return;
+        std::lock_guard<std::mutex> g(mu_);
+        free_[c->dev].push_back(c);
+    }
+
+  private:
+    std::mutex mu_;
+    std::map<int, std::vector<Ctx*>> free_;
 };
 
 }  // namespace sr

@@ -6,8 +6,11 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <immintrin.h>
 #include <memory>
 #include <string>
 #include <thread>
@@ -26,6 +29,16 @@ using Clock = std::chrono::steady_clock;
 static double secs(Clock::time_point a, Clock::time_point b) { return std::chrono::duration<double>(b - a).count(); }
 
 static inline u32 blocks_for(u64 n, u32 bs) { return (u32)((n + bs - 1) / bs); }
+
+using Ctx = DeviceContext<LevelCounters, HostCounters>;
+using CtxPool = ContextPool<Ctx>;
+
+// Holds a pooled device context for the duration of a scope.
+struct CtxLease {
+    Ctx* c;
+    explicit CtxLease(int dev) : c(CtxPool::get().acquire(dev)) {}
+    ~CtxLease() { CtxPool::get().release(c); }
+};
 
 struct DiscoveryRec {
     bool found = false;
@@ -66,12 +79,12 @@ class Engine final : public EngineBase {
   public:
     Engine(M m, const sr_opts& o) : m_(m), o_(o), A_((u32)m.max_actions()), D_((u32)m.max_out_degree()) {
         disc.resize(M::NPROPS);
+        // Internal tuning knobs (not part of the ABI): successors per lane per probe round and
+        // the visited-set load factor the capacity hint is sized for.
+        if (const char* e = std::getenv("SR_PROBE_BATCH")) probe_batch_ = std::atoi(e);
+        if (const char* e = std::getenv("SR_TABLE_LOAD")) table_load_ = std::atof(e);
     }
-    ~Engine() override {
-        if (stream_) (void)hipStreamDestroy(stream_);
-        for (auto* e : {ev0_, ev1_})
-            if (e) (void)hipEventDestroy(e);
-    }
+    ~Engine() override = default;
 
     int nprops() const override { return M::NPROPS; }
     const char* prop_name(int p) const override { return m_.prop_name(p); }
@@ -81,41 +94,66 @@ class Engine final : public EngineBase {
 
     void run() override {
         SR_HIP(hipSetDevice(o_.device));
-        SR_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
-        SR_HIP(hipEventCreate(&ev0_));
-        SR_HIP(hipEventCreate(&ev1_));
-        SR_HIP(hipMalloc(&lc_d_, sizeof(LevelCounters)));
+        CtxLease lease(o_.device);
+        bind(lease.c);
         int order = o_.order;
         if (order == SR_ORDER_AUTO) order = o_.target_state_count ? SR_ORDER_FIFO : SR_ORDER_FAST;
-        bool order_dependent = run_order(order);
+        bool order_dependent = run_with_restart(order);
         if (order_dependent && o_.order == SR_ORDER_AUTO && order == SR_ORDER_FAST) {
             // An early exit inside a level makes counts depend on the visit order: redo the
             // check in the reference's exact FIFO order.
             if (o_.verbose) std::fprintf(stderr, "[sr] early exit in FAST order; re-running in FIFO order\n");
-            run_order(SR_ORDER_FIFO);
+            run_with_restart(SR_ORDER_FIFO);
         }
-        SR_HIP(hipFree(lc_d_));
-        lc_d_ = nullptr;
+        bind(nullptr);
     }
 
+    // Capacity planning is optimistic (a chunk is sized for twice the previous level's growth, not
+    // for every successor being new). If a level ever outgrows it, the device reports a full table
+    // or arena and the check restarts from scratch in the pessimistic mode with larger buffers.
+    bool run_with_restart(int order) {
+        for (int attempt = 0;; ++attempt) {
+            try {
+                return run_order(order);
+            } catch (const Error& e) {
+                if (e.code != SR_ERR_CAPACITY || attempt >= 3) throw;
+                if (o_.verbose) std::fprintf(stderr, "[sr] %s; restarting with larger buffers\n", e.what());
+                pessimistic_ = true;
+                grow_factor_ *= 4;
+                (void)hipStreamSynchronize(stream_);
+                init_counters();
+            }
+        }
+    }
+
+    // `reconstruct_path` (src/checker/bfs.rs:314-342): the discovery's fingerprint chain, found by
+    // walking parent ranks back through the BFS-tree arena.
     int chain(int p, std::vector<u64>& out) override {
         out.clear();
         if (p < 0 || p >= M::NPROPS || !disc[p].found) return 0;
         SR_HIP(hipSetDevice(o_.device));
-        DBuf<u64> buf;
-        DBuf<u32> len;
-        const u32 cap = 1u << 16;
-        buf.alloc(o_.device, cap);
-        len.alloc(o_.device, 1);
-        trace_chain<<<1, 1, 0, stream_>>>(view(), disc[p].fp, buf.p, cap, len.p);
-        SR_HIP(hipGetLastError());
-        u32 n = 0;
-        SR_HIP(hipMemcpyAsync(&n, len.p, sizeof(u32), hipMemcpyDeviceToHost, stream_));
-        SR_HIP(hipStreamSynchronize(stream_));
-        out.resize(n);
-        SR_HIP(hipMemcpy(out.data(), buf.p, n * sizeof(u64), hipMemcpyDeviceToHost));
-        std::reverse(out.begin(), out.end());  // init .. discovered
-        return (int)n;
+        std::vector<u64> st;
+        tree_path(disc[p].level, disc[p].rank, st);
+        for (size_t i = 0; i < st.size() / W; ++i) out.push_back(fingerprint<W>(&st[i * W]));
+        return (int)out.size();
+    }
+
+    // States (W words each) from the init state down to (level, rank).
+    void tree_path(u32 level, u32 rank, std::vector<u64>& st) {
+        std::vector<u64> idx;
+        u64 r = rank;
+        for (int d = (int)level;; --d) {
+            u64 a = lstart_[d] + r;
+            idx.push_back(a);
+            if (d == 0) break;
+            u32 pr = 0;
+            SR_HIP(hipMemcpy(&pr, apar_.p + a, sizeof(u32), hipMemcpyDeviceToHost));
+            r = pr;
+        }
+        std::reverse(idx.begin(), idx.end());
+        st.resize(idx.size() * W);
+        for (size_t i = 0; i < idx.size(); ++i)
+            SR_HIP(hipMemcpy(&st[i * W], arena_.p + idx[i] * W, W * sizeof(u64), hipMemcpyDeviceToHost));
     }
 
     // `Path::from_fingerprints` (src/checker/path.rs:20-86) on the host copy of the GpuModel.
@@ -201,18 +239,24 @@ class Engine final : public EngineBase {
 
     std::vector<i64> visits() const override {
         const int wd = m_.describe_width();
-        std::vector<i64> out(visits_.size() / W * wd);
-        for (size_t i = 0; i < visits_.size() / W; ++i) m_.describe(&visits_[i * W], &out[i * wd]);
+        std::vector<u64> st;
+        for (size_t d = 0; d < lvisited_.size(); ++d) {
+            size_t o = st.size();
+            st.resize(o + lvisited_[d] * W);
+            if (lvisited_[d])
+                SR_HIP(hipMemcpy(&st[o], arena_.p + lstart_[d] * W, lvisited_[d] * W * sizeof(u64), hipMemcpyDeviceToHost));
+        }
+        std::vector<i64> out(st.size() / W * wd);
+        for (size_t i = 0; i < st.size() / W; ++i) m_.describe(&st[i * W], &out[i * wd]);
         return out;
     }
 
   private:
-    TableView view() const { return TableView{keys_.p, parents_.p, fifo_ ? meta_.p : nullptr, cap_ - 1}; }
+    TableView view() const { return TableView{keys_.p, fifo_ ? meta_.p : nullptr, cap_ - 1}; }
 
     void alloc_table(u64 cap) {
         cap_ = cap;
         keys_.alloc(o_.device, cap);
-        parents_.alloc(o_.device, cap);
         SR_HIP(hipMemsetAsync(keys_.p, 0, cap * sizeof(u64), stream_));
         if (fifo_) {
             meta_.alloc(o_.device, cap);
@@ -223,11 +267,10 @@ class Engine final : public EngineBase {
     // Doubles the visited set. In FIFO order the level's candidate slots (cand) are remapped to
     // the new table, since the rehash moves every entry.
     void grow_table(u32* cand = nullptr, u64 cand_n = 0) {
-        DBuf<u64> ok, op, om;
+        DBuf<u64> ok, om;
         ok.swap(keys_);
-        op.swap(parents_);
         if (fifo_) om.swap(meta_);
-        TableView from{ok.p, op.p, fifo_ ? om.p : nullptr, cap_ - 1};
+        TableView from{ok.p, fifo_ ? om.p : nullptr, cap_ - 1};
         u64 old_cap = cap_;
         alloc_table(cap_ * 2);
         rehash<<<blocks_for(old_cap, 256), 256, 0, stream_>>>(from, old_cap, view(), lc_d_);
@@ -240,40 +283,86 @@ class Engine final : public EngineBase {
         stats.rehashes++;
     }
 
-    void ensure_frontier(DBuf<u64>& b, u64 states, u64 keep_states) {
-        if (b.n >= states * W) return;
-        DBuf<u64> nb;
-        nb.alloc(o_.device, std::max<u64>(states, b.n / W * 2) * W);
-        if (keep_states) SR_HIP(hipMemcpyAsync(nb.p, b.p, keep_states * W * sizeof(u64), hipMemcpyDeviceToDevice, stream_));
-        b.swap(nb);
+    // The BFS-tree arena holds every level's states (visit order) and their parent ranks; grows
+    // by copying the used prefix.
+    void ensure_arena(u64 states, u64 used) {
+        if (arena_cap_ >= states) return;
+        u64 cap = std::max<u64>(states, arena_cap_ * 2);
+        DBuf<u64> na;
+        DBuf<u32> np;
+        na.alloc(o_.device, cap * W);
+        np.alloc(o_.device, cap);
+        if (used) {
+            SR_HIP(hipMemcpyAsync(na.p, arena_.p, used * W * sizeof(u64), hipMemcpyDeviceToDevice, stream_));
+            SR_HIP(hipMemcpyAsync(np.p, apar_.p, used * sizeof(u32), hipMemcpyDeviceToDevice, stream_));
+        }
+        arena_.swap(na);
+        apar_.swap(np);
+        arena_cap_ = cap;
         SR_HIP(hipStreamSynchronize(stream_));
     }
 
-    void reset_counters() {
-        std::memset(&lc_, 0, sizeof(lc_));
-        for (auto& d : lc_.disc) d = ~0u;
-        SR_HIP(hipMemcpyAsync(lc_d_, &lc_, sizeof(lc_), hipMemcpyHostToDevice, stream_));
+    void bind(Ctx* c) {
+        ctx_ = c;
+        stream_ = c ? c->stream : nullptr;
+        lc_d_ = c ? c->lc : nullptr;
     }
-    void read_counters() {
-        SR_HIP(hipMemcpyAsync(&lc_, lc_d_, sizeof(lc_), hipMemcpyDeviceToHost, stream_));
+
+    // Device counters to their level-start values (once per run; afterwards the publishing
+    // workgroup of each level resets them).
+    void init_counters() {
+        LevelCounters z;
+        std::memset(&z, 0, sizeof(z));
+        for (auto& d : z.disc) d = ~0u;
+        SR_HIP(hipMemcpyAsync(lc_d_, &z, sizeof(z), hipMemcpyHostToDevice, stream_));
         SR_HIP(hipStreamSynchronize(stream_));
+    }
+    u32 next_seq() { return ++ctx_->seq; }
+
+    // Waits until the launch tagged `seq` has published its counters to pinned host memory: a
+    // spin on one host word (no stream synchronisation, no copy), with a periodic stream query
+    // so that a failed launch cannot hang the host.
+    void wait_publish(u32 seq) {
+        volatile u32* flag = &ctx_->hc->seq;
+        for (u64 spin = 1;; ++spin) {
+            if (*flag == seq) break;
+            if ((spin & 4095) == 0) {
+                hipError_t e = hipStreamQuery(stream_);
+                if (e != hipSuccess && e != hipErrorNotReady) SR_HIP(e);
+                if (e == hipSuccess && *flag != seq) {
+                    if (*flag == seq) break;
+                    throw Error(SR_ERR_HIP, "launch finished without publishing its counters");
+                }
+            }
+            _mm_pause();
+        }
+        std::atomic_thread_fence(std::memory_order_acquire);
+        std::memcpy(&lc_, (const void*)ctx_->hc, sizeof(lc_));
         if (lc_.err & ERR_TABLE_FULL) throw Error(SR_ERR_CAPACITY, "visited set probe limit exceeded");
         if (lc_.err & ERR_FRONTIER_OVERFLOW) throw Error(SR_ERR_CAPACITY, "frontier overflow");
     }
 
+    // Launch bracketed by pooled events (profile=1); durations are summed once at the end of the
+    // run, so timing adds no synchronisation to the level loop.
     template <class F>
     void timed(F&& launch) {
-        if (o_.profile) SR_HIP(hipEventRecord(ev0_, stream_));
+        size_t i = 2 * stats.expand_launches;
+        if (o_.profile) SR_HIP(hipEventRecord(ctx_->event(i), stream_));
         launch();
         SR_HIP(hipGetLastError());
-        if (o_.profile) {
-            SR_HIP(hipEventRecord(ev1_, stream_));
-            SR_HIP(hipEventSynchronize(ev1_));
-            float ms = 0;
-            SR_HIP(hipEventElapsedTime(&ms, ev0_, ev1_));
-            stats.expand_kernel_ms += ms;
-        }
+        if (o_.profile) SR_HIP(hipEventRecord(ctx_->event(i + 1), stream_));
         stats.expand_launches++;
+    }
+    void collect_timing() {
+        if (!o_.profile || !stats.expand_launches) return;
+        SR_HIP(hipEventSynchronize(ctx_->event(2 * stats.expand_launches - 1)));
+        double ms = 0;
+        for (u64 i = 0; i < stats.expand_launches; ++i) {
+            float t = 0;
+            SR_HIP(hipEventElapsedTime(&t, ctx_->event(2 * i), ctx_->event(2 * i + 1)));
+            ms += t;
+        }
+        stats.expand_kernel_ms = ms;
     }
 
     // Returns true when the run stopped early inside a level in an order-dependent way.
@@ -284,14 +373,14 @@ class Engine final : public EngineBase {
         unique = 0;
         max_depth = 0;
         for (auto& d : disc) d = DiscoveryRec{};
-        visits_.clear();
         stats = sr_stats{};
         stats.words_per_state = W;
         stats.order_used = (u32)order;
 
-        // Visited set sized for <= 50% load at the hinted unique count.
-        u64 cap = 1u << 20;
-        if (o_.capacity_hint) while (cap < 2 * o_.capacity_hint) cap <<= 1;
+        // Visited set sized for <= table_load_ load at the hinted unique count.
+        u64 cap = (u64)(1u << 20) * grow_factor_;
+        if (o_.capacity_hint) while ((double)cap * table_load_ < (double)o_.capacity_hint * grow_factor_) cap <<= 1;
+        ratio_ = (double)D_;
         alloc_table(cap);
 
         // Init states (bfs.rs:43-66): all of them are counted and queued (duplicates too), the
@@ -302,13 +391,19 @@ class Engine final : public EngineBase {
         std::vector<u64> f0(inits, inits + k * W);
         std::vector<u64> rev(k * W);
         for (int i = 0; i < k; ++i) std::copy(&f0[i * W], &f0[i * W] + W, &rev[(k - 1 - i) * W]);
-        cur_.alloc(o_.device, std::max<u64>(1024, (u64)k) * W);
-        SR_HIP(hipMemcpyAsync(cur_.p, rev.data(), rev.size() * sizeof(u64), hipMemcpyHostToDevice, stream_));
-        reset_counters();
-        insert_roots<M><<<blocks_for(k, 64), 64, 0, stream_>>>(view(), cur_.p, (u32)k, lc_d_);
-        eval_roots<M><<<blocks_for(k, 64), 64, 0, stream_>>>(m_, cur_.p, (u32)k, lc_d_, (1u << M::NPROPS) - 1);
+        arena_cap_ = 0;
+        ensure_arena(std::max<u64>(1u << 16, (o_.capacity_hint + o_.capacity_hint / 8 + 1024) * grow_factor_), 0);
+        lstart_.assign({0, (u64)k});
+        lvisited_.clear();
+        SR_HIP(hipMemcpyAsync(arena_.p, rev.data(), rev.size() * sizeof(u64), hipMemcpyHostToDevice, stream_));
+        SR_HIP(hipMemsetAsync(apar_.p, 0xff, (size_t)k * sizeof(u32), stream_));
+        init_counters();
+        insert_roots<M><<<blocks_for(k, 64), 64, 0, stream_>>>(view(), arena_.p, (u32)k, lc_d_);
+        eval_roots<M><<<blocks_for(k, 64), 64, 0, stream_>>>(m_, arena_.p, (u32)k, lc_d_, (1u << M::NPROPS) - 1);
+        u32 sq = next_seq();
+        publish_kernel<<<1, 64, 0, stream_>>>(lc_d_, ctx_->hc_dev, sq, 1, nullptr);
         SR_HIP(hipGetLastError());
-        read_counters();
+        wait_publish(sq);
         state_count = (u64)k;
         unique = lc_.claims;
 
@@ -328,7 +423,7 @@ class Engine final : public EngineBase {
                     disc[p].level = level;
                     disc[p].rank = lc_.disc[p];
                     u64 s[W];
-                    SR_HIP(hipMemcpy(s, cur_.p + (u64)lc_.disc[p] * W, W * sizeof(u64), hipMemcpyDeviceToHost));
+                    SR_HIP(hipMemcpy(s, arena_.p + (lstart_[level] + lc_.disc[p]) * W, W * sizeof(u64), hipMemcpyDeviceToHost));
                     disc[p].fp = fingerprint<W>(s);
                 }
             u64 limit = n, visited = n;
@@ -360,11 +455,7 @@ class Engine final : public EngineBase {
                 }
             }
 
-            if (o_.record_visits && visited) {
-                size_t o = visits_.size();
-                visits_.resize(o + visited * W);
-                SR_HIP(hipMemcpy(&visits_[o], cur_.p, visited * W * sizeof(u64), hipMemcpyDeviceToHost));
-            }
+            lvisited_.push_back(visited);
 
             // 3. Expand ranks [0, limit).
             u64 produced = 0;
@@ -392,11 +483,12 @@ class Engine final : public EngineBase {
                     reference_done = !(o_.target_state_count && state_count >= o_.target_state_count);
                 break;
             }
-            cur_.swap(next_);
+            lstart_.push_back(lstart_.back() + produced);
             n = produced;
             ++level;
         }
         auto t_end = Clock::now();
+        collect_timing();
         stats.level_loop_sec = secs(t_loop, t_end);
         stats.total_sec = secs(t_start, t_end);
         stats.table_capacity = cap_;
@@ -407,7 +499,7 @@ class Engine final : public EngineBase {
     u64 target_limit(u64 n, u64 popped_before, u64 limit) {
         DBuf<u32> counts;
         counts.alloc(o_.device, n);
-        count_successors<M><<<blocks_for(n, 256), 256, 0, stream_>>>(m_, cur_.p, (u32)n, counts.p);
+        count_successors<M><<<blocks_for(n, 256), 256, 0, stream_>>>(m_, cur(), (u32)n, counts.p);
         SR_HIP(hipGetLastError());
         std::vector<u32> h(n);
         SR_HIP(hipMemcpyAsync(h.data(), counts.p, n * sizeof(u32), hipMemcpyDeviceToHost, stream_));
@@ -425,41 +517,58 @@ class Engine final : public EngineBase {
     // Expands frontier ranks [0, limit) of `level` into next_; returns the next frontier size.
     u64 expand_level(u32 level, u64 n, u64 limit, u32 undiscovered) {
         const u32 A = A_;  // action slots (FIFO candidate layout)
-        reset_counters();
         u64 claims = 0;
         DBuf<u32> cand;
         if (fifo_) {
             cand.alloc(o_.device, limit * A);
             SR_HIP(hipMemsetAsync(cand.p, 0xff, limit * A * sizeof(u32), stream_));
         }
+        const u64 nbase = lstart_.back();  // arena offset of the next level
+        // New states per parent assumed when sizing a chunk: twice the last level's growth (the
+        // model's max out-degree D in pessimistic mode); see run_with_restart.
+        const u64 d_eff = pessimistic_ ? D_ : std::min<u64>(D_, (u64)std::ceil(2.0 * ratio_ + 1.0));
         for (u64 lo = 0; lo < limit;) {
-            // Chunk so the visited set stays under 75% load even if every successor is new.
+            // Chunk so the visited set stays under 80% load.
             u64 head = (u64)(0.8 * (double)cap_) - std::min<u64>((u64)(0.8 * (double)cap_), unique + claims);
-            u64 c = std::min<u64>(limit - lo, head / std::max<u32>(D_, 1));
+            u64 c = std::min<u64>(limit - lo, head / std::max<u64>(d_eff, 1));
             if (c < std::min<u64>(limit - lo, 1u << 16)) {
                 grow_table(fifo_ ? cand.p : nullptr, fifo_ ? limit * A : 0);
                 continue;
             }
-            if (!fifo_) ensure_frontier(next_, claims + c * D_, claims);
+            if (!fifo_) ensure_arena(nbase + claims + c * d_eff, nbase + claims);
             const u32 ulo = (u32)lo, uhi = (u32)(lo + c);
+            const bool last = lo + c == limit;
+            const u32 sq = next_seq();
             if (fifo_) {
                 timed([&] {
-                    expand_fifo<M><<<blocks_for(c, 256), 256, 0, stream_>>>(m_, cur_.p, ulo, uhi, (u32)limit, view(), cand.p, A, level, lc_d_);
+                    expand_fifo<M><<<blocks_for(c, 256), 256, 0, stream_>>>(m_, cur(), ulo, uhi, (u32)limit, view(), cand.p,
+                                                                            A, level, lc_d_, ctx_->hc_dev, sq);
                 });
             } else {
+                const u32 ncap = (u32)std::min<u64>(arena_cap_ - nbase, 0xffffffffu);
+                u64* next = arena_.p + nbase * W;
+                u32* npar = apar_.p + nbase;
                 timed([&] {
-                    expand_fast<M><<<blocks_for(c, 256), 256, 0, stream_>>>(m_, cur_.p, ulo, uhi, view(), next_.p,
-                                                                            (u32)std::min<u64>(next_.n / W, 0xffffffffu), lc_d_, undiscovered);
+                    auto launch = [&](auto kern) {
+                        kern<<<blocks_for(c, 256), 256, 0, stream_>>>(m_, cur(), ulo, uhi, view(), next, npar, ncap, lc_d_,
+                                                                      undiscovered, ctx_->hc_dev, sq, last ? 1u : 0u);
+                    };
+                    switch (probe_batch_) {
+                        case 2: launch(expand_fast<M, 2>); break;
+                        case 4: launch(expand_fast<M, 4>); break;
+                        default: launch(expand_fast<M, 1>); break;
+                    }
                 });
             }
-            read_counters();
+            wait_publish(sq);
             claims = lc_.claims;
             lo += c;
         }
+        ratio_ = (double)claims / (double)limit;
         if (!fifo_) return claims;
 
         // FIFO passes 2-3: owners per parent, exclusive scan, ordered scatter.
-        ensure_frontier(next_, claims, 0);
+        ensure_arena(nbase + claims, nbase);
         DBuf<u32> counts, offs, sums, total;
         counts.alloc(o_.device, limit);
         offs.alloc(o_.device, limit);
@@ -471,29 +580,42 @@ class Engine final : public EngineBase {
         scan_sums<<<1, SCAN_BLOCK, 0, stream_>>>(sums.p, tiles, total.p);
         scan_tiles<<<tiles, SCAN_BLOCK, 0, stream_>>>(counts.p, (u32)limit, sums.p, offs.p);
         SR_HIP(hipGetLastError());
+        const u32 sq = next_seq();
         timed([&] {
-            scatter_fifo<M><<<blocks_for(limit, 256), 256, 0, stream_>>>(m_, cur_.p, cand.p, offs.p, (u32)limit, A, level,
-                                                                         view(), next_.p, lc_d_, undiscovered);
+            scatter_fifo<M><<<blocks_for(limit, 256), 256, 0, stream_>>>(m_, cur(), cand.p, offs.p, (u32)limit, A, level,
+                                                                         view(), arena_.p + nbase * W, apar_.p + nbase, lc_d_,
+                                                                         undiscovered, ctx_->hc_dev, sq, total.p);
         });
-        u32 owners = 0;
-        SR_HIP(hipMemcpyAsync(&owners, total.p, sizeof(u32), hipMemcpyDeviceToHost, stream_));
-        read_counters();
+        wait_publish(sq);
+        const u32 owners = lc_.aux;
         if (owners != claims) throw Error(SR_ERR_CAPACITY, "FIFO ownership mismatch: owners " + std::to_string(owners) + " claims " + std::to_string(claims));
         return owners;
     }
+
+    // The frontier being expanded: the arena's second-to-last level.
+    const u64* cur() const { return arena_.p + lstart_[lstart_.size() - 2] * W; }
 
     M m_;
     sr_opts o_;
     u32 A_;  // action slots
     u32 D_;  // max successors of one state (bounds the new states a chunk can create)
     bool fifo_ = false;
+    int probe_batch_ = 1;
+    bool pessimistic_ = false;  // size chunks for max out-degree new states per parent
+    u64 grow_factor_ = 1;       // initial-capacity multiplier after a capacity restart
+    double ratio_ = 1.0;        // new states per expanded parent in the last level
+    double table_load_ = 0.5;
+    Ctx* ctx_ = nullptr;
     hipStream_t stream_ = nullptr;
-    hipEvent_t ev0_ = nullptr, ev1_ = nullptr;
-    LevelCounters lc_{};
+    HostCounters lc_{};  // host copy of the last published counters
     LevelCounters* lc_d_ = nullptr;
     u64 cap_ = 0;
-    DBuf<u64> keys_, parents_, meta_, cur_, next_;
-    std::vector<u64> visits_;
+    DBuf<u64> keys_, meta_;      // visited set
+    DBuf<u64> arena_;            // BFS tree: every level's states in visit order
+    DBuf<u32> apar_;             // parent rank (in the previous level) of each arena state
+    u64 arena_cap_ = 0;          // states
+    std::vector<u64> lstart_;    // arena offset of each level (+ one past the newest)
+    std::vector<u64> lvisited_;  // states of each level that the reference would pop
 };
 
 static std::unique_ptr<EngineBase> make_engine(int model, const i64* p, int np, const sr_opts& o) {

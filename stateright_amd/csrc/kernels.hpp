@@ -2,17 +2,20 @@
 // roofline each kernel is priced against.
 //
 // Visited set (replaces `generated: DashMap<Fingerprint, Option<Fingerprint>>`,
-// src/checker/bfs.rs:26): open addressing in HBM, struct-of-arrays so that probes touch only the
-// key array:
+// src/checker/bfs.rs:26): open addressing over a KEYS-ONLY array in HBM,
 //   keys[cap]    u64 fingerprint, 0 = vacant (fingerprints are non-zero, src/lib.rs:303)
-//   parents[cap] u64 parent fingerprint, 0 = None (an init state)
-//   meta[cap]    u64 (FIFO mode only) min over this level's generators of
+//   meta[cap]    u64 (FIFO order only) min over this level's generators of
 //                (level+1) << 44 | (parent_rank * A + action_slot): the generator that the
 //                reference's single-threaded FIFO would have seen first owns the new state.
+// The `Option<Fingerprint>` parent half of the reference map lives in the BFS tree instead: every
+// level's frontier is kept in one arena (states in visit order) next to a u32 array of parent
+// ranks in the previous level, both written coalesced. A path is rank -> parent rank -> ... .
+//
 // Linear probing from fp & mask; a probe reads the key with a plain load first (duplicates are
-// ~92% of successors on 2pc and never need an atomic; a stale EMPTY only falls through to the
+// ~90% of successors on 2pc and never need an atomic; a stale EMPTY only falls through to the
 // CAS, which is the arbiter, because a slot goes EMPTY -> key exactly once), and only a vacant
-// slot costs a 64-bit atomicCAS.
+// slot costs a 64-bit atomicCAS. A successor equal to its parent (a self-loop: 37% of 2pc's
+// successors) is a duplicate by construction and is counted without touching the table.
 #pragma once
 #include "models.hpp"
 
@@ -28,27 +31,76 @@ enum ErrBits { ERR_TABLE_FULL = 1, ERR_FRONTIER_OVERFLOW = 2 };
 
 struct TableView {
     u64* keys;
-    u64* parents;
     u64* meta;
     u64 mask;
 };
 
-// Per-level device counters, copied back once per chunk/level. The hot counters sit on separate
-// 128-byte lines (one returning atomic per workgroup each).
+constexpr u32 NO_PARENT = 0xffffffffu;
+
+// Per-level device counters. The hot counters sit on separate 128-byte lines (one returning
+// atomic per workgroup each). The last workgroup of a launch (ticket) publishes a snapshot to
+// pinned host memory, so the host learns the level's outcome without a copy or a stream sync.
 struct LevelCounters {
     u64 successors;        // successors within boundary (state_count increments, bfs.rs:235)
     u64 pad0[15];
     u32 claims;            // new states inserted into the visited set (= next-frontier cursor)
     u32 pad1[31];
+    u32 ticket;            // workgroups finished in this launch
+    u32 pad2[31];
     u32 err;               // ErrBits
     u32 disc[MAX_PROPS];   // min rank of a discovering state in the frontier being produced
 };
 
-// Find `key` or claim a vacant slot for it. Returns the slot; *is_new tells whether we claimed it.
-__device__ __forceinline__ u64 find_or_claim(const TableView& t, u64 key, bool* is_new, u32* err) {
-    u64 i = key & t.mask;
+// Host-visible snapshot (hipHostMalloc'd), written by the publishing workgroup.
+struct HostCounters {
+    u64 successors;
+    u32 claims;
+    u32 err;
+    u32 aux;               // launch-specific value (FIFO: number of owners from the scan)
+    u32 disc[MAX_PROPS];
+    u32 seq;               // written last: the launch's sequence number
+};
+
+__device__ __forceinline__ void reset_counters(LevelCounters* lc) {
+    lc->successors = 0;
+    lc->claims = 0;
+    lc->err = 0;
+#pragma unroll
+    for (int p = 0; p < MAX_PROPS; ++p) lc->disc[p] = ~0u;
+}
+
+// Called by every workgroup after its last counter update (all threads). The workgroup that
+// arrives last copies the counters to host memory, optionally resets them for the next level,
+// and finally stores `seq` (Guideline 16: release before the ticket, acquire after it).
+__device__ __forceinline__ void publish(LevelCounters* lc, HostCounters* h, u32 seq, bool reset, const u32* aux) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    u32 t = atomicAdd(&lc->ticket, 1u);
+    if (t != gridDim.x - 1) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    h->successors = __hip_atomic_load(&lc->successors, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    h->claims = __hip_atomic_load(&lc->claims, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    h->err = __hip_atomic_load(&lc->err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    h->aux = aux ? __hip_atomic_load(aux, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+    for (int p = 0; p < MAX_PROPS; ++p) h->disc[p] = __hip_atomic_load(&lc->disc[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (reset) reset_counters(lc);
+    lc->ticket = 0;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: host memory
+    __hip_atomic_store(&h->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Standalone publish (after kernels that do not publish themselves).
+__global__ void publish_kernel(LevelCounters* lc, HostCounters* h, u32 seq, u32 reset, const u32* aux) {
+    publish(lc, h, seq, reset != 0, aux);
+}
+
+// Find `key` or claim a vacant slot for it, starting at slot i whose key `cur` was already loaded.
+// Returns the slot; *is_new tells whether we claimed it.
+__device__ __forceinline__ u64 find_or_claim_from(const TableView& t, u64 key, u64 i, u64 cur, bool* is_new, u32* err) {
     for (int probe = 0; probe < MAX_PROBE; ++probe) {
-        u64 cur = t.keys[i];
         if (cur == key) {
             *is_new = false;
             return i;
@@ -66,10 +118,16 @@ __device__ __forceinline__ u64 find_or_claim(const TableView& t, u64 key, bool* 
             }
         }
         i = (i + 1) & t.mask;
+        cur = t.keys[i];
     }
     atomicOr(err, (u32)ERR_TABLE_FULL);
     *is_new = false;
     return ~0ull;
+}
+
+__device__ __forceinline__ u64 find_or_claim(const TableView& t, u64 key, bool* is_new, u32* err) {
+    u64 i = key & t.mask;
+    return find_or_claim_from(t, key, i, t.keys[i], is_new, err);
 }
 
 // Lookup only (path reconstruction).
@@ -121,6 +179,14 @@ __device__ __forceinline__ void store_state(u64* base, u64 r, const u64* s) {
     }
 }
 
+template <int W>
+__device__ __forceinline__ bool same_state(const u64* a, const u64* b) {
+    bool eq = true;
+#pragma unroll
+    for (int i = 0; i < W; ++i) eq &= a[i] == b[i];
+    return eq;
+}
+
 // Insert the (distinct) init states with parent None (`generated.insert(fp, None)`, bfs.rs:47-51).
 template <class M>
 __global__ void insert_roots(TableView t, const u64* states, u32 n, LevelCounters* lc) {
@@ -131,7 +197,6 @@ __global__ void insert_roots(TableView t, const u64* states, u32 n, LevelCounter
     bool is_new;
     u64 slot = find_or_claim(t, fingerprint<M::W>(s), &is_new, &lc->err);
     if (is_new) {
-        t.parents[slot] = 0;
         if (t.meta) t.meta[slot] = 0;  // level 0
         atomicAdd(&lc->claims, 1u);
     }
@@ -159,44 +224,146 @@ __device__ __forceinline__ u32 block_sum(u32 v, u32* scratch) {
     return t;
 }
 
-// FAST order: expand parents [lo, hi) of the frontier. Every successor within boundary counts
-// toward state_count (bfs.rs:235); one that claims a vacant slot is new: its parent pointer is
-// written and the state is staged in LDS. At the end the workgroup reserves its span of the next
-// frontier with ONE global atomic, copies the staged states out contiguously, and evaluates the
-// properties there (rank = frontier position). A workgroup that stages more than STAGE states
-// appends the overflow directly (per-wave aggregated atomics).
-template <class M>
-__global__ void __launch_bounds__(256) expand_fast(M m, const u64* __restrict__ frontier, u32 lo, u32 hi,
-                                                   TableView t, u64* __restrict__ next, u32 next_cap,
-                                                   LevelCounters* lc, u32 undiscovered) {
-    constexpr int STAGE = 2048 / M::W;
-    __shared__ u64 stage[STAGE * M::W];
-    __shared__ u32 stage_n, base, scratch[4];
-    if (threadIdx.x == 0) stage_n = 0;
-    __syncthreads();
-    const u32 r = lo + blockIdx.x * blockDim.x + threadIdx.x;
-    u32 succ = 0;
-    if (r < hi) {
-        u64 s[M::W];
-        load_state<M::W>(frontier, r, s);
-        const u64 pfp = fingerprint<M::W>(s);
-        for_each_successor(m, s, [&](int, const u64* ns) {
-            ++succ;
-            bool is_new;
-            u64 slot = find_or_claim(t, fingerprint<M::W>(ns), &is_new, &lc->err);
-            if (!is_new) return;
-            t.parents[slot] = pfp;
-            u32 k = atomicAdd(&stage_n, 1u);
-            if (k < (u32)STAGE) {
+// k-th set bit (0-based) of a 64-bit mask with popcount(m) > k.
+__device__ __forceinline__ u32 select_bit(u64 m, u32 k) {
+    u32 pos = 0;
 #pragma unroll
-                for (int i = 0; i < M::W; ++i) stage[k * M::W + i] = ns[i];
+    for (int w = 32; w >= 1; w >>= 1) {
+        u64 low = m & ((1ull << w) - 1);
+        u32 c = __popcll(low);
+        if (k >= c) {
+            k -= c;
+            m >>= w;
+            pos += w;
+        }
+    }
+    return pos;
+}
+
+// FAST order: expand parents [lo, hi) of the frontier.
+//
+// Load-balanced over SUCCESSORS: each wave loads 64 parents, counts their enabled actions, and
+// then its 64 lanes walk the concatenated successor list (parent found by binary search over the
+// wave's prefix sums, action = k-th set bit of that parent's mask). Lanes stay busy whatever the
+// out-degree spread, and a lone parent's successors are probed in parallel. Each lane takes
+// PB successors per round and issues their first visited-set probes back to back (PB loads in
+// flight per lane) before resolving any of them.
+//
+// Every successor within boundary counts toward state_count (bfs.rs:235); one that claims a
+// vacant slot is new: its parent pointer is written and the state is staged in LDS. At the end
+// the workgroup reserves its span of the next frontier with ONE global atomic, copies the staged
+// states out contiguously, and evaluates the properties there (rank = frontier position). A
+// workgroup that stages more than STAGE states appends the overflow directly.
+template <class M, int PB>
+__global__ void __launch_bounds__(256) expand_fast(M m, const u64* __restrict__ frontier, u32 lo, u32 hi,
+                                                   TableView t, u64* __restrict__ next, u32* __restrict__ next_par,
+                                                   u32 next_cap, LevelCounters* lc, u32 undiscovered,
+                                                   HostCounters* hc, u32 seq, u32 reset) {
+    constexpr int W = M::W, MW = M::MW;
+    constexpr int STAGE = 1024 / W;
+    __shared__ u64 stage[STAGE * W];
+    __shared__ u32 stage_par[STAGE];
+    __shared__ u64 pst[4][64 * W];      // parent states of each wave
+    __shared__ u64 pmask[4][64 * MW];   // their enabled-action masks
+    __shared__ u32 pexcl[4][64];        // exclusive prefix of their successor counts
+    __shared__ u32 stage_n, base, scratch[4];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (threadIdx.x == 0) stage_n = 0;
+
+    const u32 r = lo + blockIdx.x * blockDim.x + threadIdx.x;
+    u32 cnt = 0;
+    if (r < hi) {
+        u64 s[W], mk[MW];
+        load_state<W>(frontier, r, s);
+        m.enabled(s, mk);
+#pragma unroll
+        for (int i = 0; i < W; ++i) pst[wid][lane * W + i] = s[i];
+#pragma unroll
+        for (int i = 0; i < MW; ++i) {
+            pmask[wid][lane * MW + i] = mk[i];
+            cnt += __popcll(mk[i]);
+        }
+    }
+    // wave-inclusive scan of the counts
+    u32 incl = cnt;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        u32 y = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += y;
+    }
+    pexcl[wid][lane] = incl - cnt;
+    const u32 total = __shfl(incl, 63, 64);
+    __syncthreads();
+
+    u32 succ = 0;
+    for (u32 it = 0; it < total; it += 64 * PB) {
+        u64 ns[PB][W], key[PB], idx[PB], cur[PB];
+        u32 par[PB];
+        bool ok[PB];
+#pragma unroll
+        for (int j = 0; j < PB; ++j) {
+            const u32 i = it + j * 64 + lane;
+            ok[j] = i < total;
+            par[j] = 0;
+            if (ok[j]) {
+                // parent p: last lane with pexcl[p] <= i (zero-count lanes share their successor's
+                // prefix; the last of them has a non-zero count because i < its inclusive prefix)
+                u32 p = 0;
+#pragma unroll
+                for (int step = 32; step >= 1; step >>= 1)
+                    if (pexcl[wid][p + step] <= i) p += step;
+                u32 k = i - pexcl[wid][p];
+                u32 a = 0;
+#pragma unroll
+                for (int w = 0; w < MW; ++w) {
+                    u64 mw = pmask[wid][p * MW + w];
+                    u32 c = __popcll(mw);
+                    if (k < c) {
+                        a = w * 64 + select_bit(mw, k);
+                        break;
+                    }
+                    k -= c;
+                }
+                u64 ps[W];
+#pragma unroll
+                for (int x = 0; x < W; ++x) ps[x] = pst[wid][p * W + x];
+                ok[j] = m.apply(ps, (int)a, ns[j]);
+                par[j] = p;
+                if (ok[j] && same_state<W>(ns[j], ps)) {  // self-loop: counted, never probed
+                    ++succ;
+                    ok[j] = false;
+                }
+            }
+            key[j] = ok[j] ? fingerprint<W>(ns[j]) : 0;
+            idx[j] = key[j] & t.mask;
+        }
+#pragma unroll
+        for (int j = 0; j < PB; ++j) cur[j] = ok[j] ? t.keys[idx[j]] : 0;
+#pragma unroll
+        for (int j = 0; j < PB; ++j) {
+            if (!ok[j]) continue;
+            ++succ;
+            if (cur[j] == key[j]) continue;  // the common case: an already visited state
+            bool is_new;
+            find_or_claim_from(t, key[j], idx[j], cur[j], &is_new, &lc->err);
+            if (!is_new) continue;
+            const u32 pr = lo + blockIdx.x * blockDim.x + wid * 64 + par[j];  // parent rank
+            u32 kk = atomicAdd(&stage_n, 1u);
+            if (kk < (u32)STAGE) {
+#pragma unroll
+                for (int x = 0; x < W; ++x) stage[kk * W + x] = ns[j][x];
+                stage_par[kk] = pr;
             } else {
                 u32 pos = atomicAdd(&lc->claims, 1u);
-                if (pos < next_cap) store_state<M::W>(next, pos, ns);
-                else atomicOr(&lc->err, (u32)ERR_FRONTIER_OVERFLOW);
-                eval_props(m, ns, pos, undiscovered, lc);
+                if (pos < next_cap) {
+                    store_state<W>(next, pos, ns[j]);
+                    next_par[pos] = pr;
+                } else {
+                    atomicOr(&lc->err, (u32)ERR_FRONTIER_OVERFLOW);
+                }
+                eval_props(m, ns[j], pos, undiscovered, lc);
             }
-        });
+        }
     }
     u32 total_succ = block_sum(succ, scratch);
     const u32 n = min(stage_n, (u32)STAGE);
@@ -207,13 +374,18 @@ __global__ void __launch_bounds__(256) expand_fast(M m, const u64* __restrict__ 
     __syncthreads();
     for (u32 i = threadIdx.x; i < n; i += blockDim.x) {
         u32 pos = base + i;
-        u64 ns[M::W];
+        u64 ns[W];
 #pragma unroll
-        for (int w = 0; w < M::W; ++w) ns[w] = stage[i * M::W + w];
-        if (pos < next_cap) store_state<M::W>(next, pos, ns);
-        else atomicOr(&lc->err, (u32)ERR_FRONTIER_OVERFLOW);
+        for (int x = 0; x < W; ++x) ns[x] = stage[i * W + x];
+        if (pos < next_cap) {
+            store_state<W>(next, pos, ns);
+            next_par[pos] = stage_par[i];
+        } else {
+            atomicOr(&lc->err, (u32)ERR_FRONTIER_OVERFLOW);
+        }
         eval_props(m, ns, pos, undiscovered, lc);
     }
+    publish(lc, hc, seq, reset != 0, nullptr);
 }
 
 // FIFO order, pass 1: insert-or-find every successor and record (level, parent rank, slot) in
@@ -224,7 +396,7 @@ __global__ void __launch_bounds__(256) expand_fast(M m, const u64* __restrict__ 
 template <class M>
 __global__ void __launch_bounds__(256) expand_fifo(M m, const u64* __restrict__ frontier, u32 lo, u32 hi, u32 n,
                                                    TableView t, u32* __restrict__ cand, u32 A, u32 level,
-                                                   LevelCounters* lc) {
+                                                   LevelCounters* lc, HostCounters* hc, u32 seq) {
     __shared__ u32 scratch[4];
     const u32 r = lo + blockIdx.x * blockDim.x + threadIdx.x;
     u32 succ = 0, claims = 0;
@@ -234,6 +406,7 @@ __global__ void __launch_bounds__(256) expand_fifo(M m, const u64* __restrict__ 
         const u64 lvl = (u64)(level + 1) << META_SHIFT;
         for_each_successor(m, s, [&](int a, const u64* ns) {
             ++succ;
+            if (same_state<M::W>(ns, s)) return;  // self-loop: the parent is visited already
             bool is_new;
             u64 slot = find_or_claim(t, fingerprint<M::W>(ns), &is_new, &lc->err);
             if (slot == ~0ull) return;
@@ -251,6 +424,7 @@ __global__ void __launch_bounds__(256) expand_fifo(M m, const u64* __restrict__ 
         if (ts) atomicAdd(reinterpret_cast<unsigned long long*>(&lc->successors), (unsigned long long)ts);
         if (tc) atomicAdd(&lc->claims, tc);
     }
+    publish(lc, hc, seq, false, nullptr);
 }
 
 // FIFO pass 2: number of successors each parent owns.
@@ -271,33 +445,42 @@ __global__ void __launch_bounds__(256) own_count(const u32* __restrict__ cand, u
 // FIFO pass 3: write owned successors at offs[r] + j in (parent rank, action slot) order — the
 // reference's FIFO order — set their parent pointer, and evaluate properties at that rank.
 template <class M>
-__global__ void __launch_bounds__(256) scatter_fifo(M m, const u64* __restrict__ frontier, const u32* __restrict__ cand,
-                                                    const u32* __restrict__ offs, u32 n, u32 A, u32 level,
-                                                    TableView t, u64* __restrict__ next, LevelCounters* lc,
-                                                    u32 undiscovered) {
+__device__ __forceinline__ void scatter_fifo_body(M m, const u64* __restrict__ frontier, const u32* __restrict__ cand,
+                                                  const u32* __restrict__ offs, u32 n, u32 A, u32 level,
+                                                  TableView t, u64* __restrict__ next, u32* __restrict__ next_par,
+                                                  LevelCounters* lc, u32 undiscovered) {
     u32 r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= n) return;
     const u64 lvl = (u64)(level + 1) << META_SHIFT;
     u64 s[M::W];
     bool loaded = false;
-    u64 pfp = 0;
     u32 j = offs[r];
     for (u32 a = 0; a < A; ++a) {
         u32 slot = cand[(u64)a * n + r];
         if (slot == CAND_NONE || t.meta[slot] != (lvl | ((u64)r * A + a))) continue;
         if (!loaded) {
             load_state<M::W>(frontier, r, s);
-            pfp = fingerprint<M::W>(s);
             loaded = true;
         }
         u64 ns[M::W];
         m.apply(s, (int)a, ns);
         store_state<M::W>(next, j, ns);
-        t.parents[slot] = pfp;
+        next_par[j] = r;
         eval_props(m, ns, j, undiscovered, lc);
         ++j;
     }
 }
+
+template <class M>
+__global__ void __launch_bounds__(256) scatter_fifo(M m, const u64* __restrict__ frontier, const u32* __restrict__ cand,
+                                                    const u32* __restrict__ offs, u32 n, u32 A, u32 level,
+                                                    TableView t, u64* __restrict__ next, u32* __restrict__ next_par,
+                                                    LevelCounters* lc, u32 undiscovered, HostCounters* hc, u32 seq,
+                                                    const u32* owners) {
+    scatter_fifo_body(m, frontier, cand, offs, n, A, level, t, next, next_par, lc, undiscovered);
+    publish(lc, hc, seq, true, owners);
+}
+
 
 // Successor count per parent, without inserting (used only on the level where a
 // `target_state_count` stop can fall, to find the exact 1500-pop block boundary, bfs.rs:113-135).
@@ -327,7 +510,7 @@ __global__ void eval_roots(M m, const u64* frontier, u32 n, LevelCounters* lc, u
     }
 }
 
-// Rehash into a table of twice the capacity (keys, parents and meta move together).
+// Rehash into a table of twice the capacity (keys and meta move together).
 __global__ void rehash(TableView from, u64 from_cap, TableView to, LevelCounters* lc) {
     u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= from_cap) return;
@@ -336,7 +519,6 @@ __global__ void rehash(TableView from, u64 from_cap, TableView to, LevelCounters
     bool is_new;
     u64 slot = find_or_claim(to, k, &is_new, &lc->err);
     if (slot == ~0ull) return;
-    to.parents[slot] = from.parents[i];
     if (to.meta) to.meta[slot] = from.meta[i];
 }
 
@@ -347,21 +529,6 @@ __global__ void remap_slots(u32* cand, u64 n, const u64* old_keys, TableView to)
     u32 s = cand[i];
     if (s == CAND_NONE) return;
     cand[i] = (u32)find_slot(to, old_keys[s]);
-}
-
-// Walks the parent chain of `fp` (reconstruct_path, bfs.rs:314-342); one thread.
-__global__ void trace_chain(TableView t, u64 fp, u64* out, u32 cap, u32* len) {
-    u32 k = 0;
-    u64 cur = fp;
-    while (k < cap) {
-        u64 slot = find_slot(t, cur);
-        if (slot == ~0ull) break;
-        out[k++] = cur;
-        u64 p = t.parents[slot];
-        if (p == 0) break;
-        cur = p;
-    }
-    *len = k;
 }
 
 // ---- exclusive scan of u32 counts (3-phase: tile sums, scan of sums, tile scan + carry) ----
