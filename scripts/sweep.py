@@ -30,16 +30,19 @@ def main():
     n = int(os.environ.get("N", "9"))
     exp = 6 ** n + 4 ** n + 2 ** n
     out = []
-    for pb, load in itertools.product([1, 2, 4], [0.25, 0.5, 0.7]):
+    for pb, load, pol, ppw in itertools.product([1, 2], [0.5], [0], [-1, 6]):
         os.environ["SR_PROBE_BATCH"] = str(pb)
         os.environ["SR_TABLE_LOAD"] = str(load)
+        os.environ["SR_PROBE_LOAD"] = str(pol)
+        os.environ["SR_PPW_LOG2"] = str(ppw)
         r = run(lambda: TwoPhaseSys(n).checker().order("fast").capacity_hint(exp), exp)
-        line = {"model": f"2pc{n}", "pb": pb, "load": load, "best_ms": r[0], "med_ms": r[1], "kernel_ms": r[2],
+        line = {"model": f"2pc{n}", "lib": os.environ.get("SR_LIB_PATH", "default")[-12:], "pb": pb, "load": load, "pol": pol, "ppw": ppw, "best_ms": r[0], "med_ms": r[1], "kernel_ms": r[2],
                 "cap": r[3], "launches": r[4], "unique_per_s": exp / r[0] * 1e3}
         print(json.dumps(line), flush=True)
         out.append(line)
-    os.environ["SR_PROBE_BATCH"] = "4"
+    os.environ["SR_PROBE_BATCH"] = "1"
     os.environ["SR_TABLE_LOAD"] = "0.5"
+    os.environ["SR_PROBE_LOAD"] = "0"
     il = 39456401
     r = run(lambda: IncrementLock(10).checker().order("fast").capacity_hint(il), il, reps=3, warm=1)
     print(json.dumps({"model": "inclock10", "best_ms": r[0], "kernel_ms": r[2], "unique_per_s": il / r[0] * 1e3}), flush=True)

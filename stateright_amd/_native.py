@@ -8,7 +8,7 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libstateright_gpu.so")
+LIB_PATH = os.environ.get("SR_LIB_PATH") or os.path.join(HERE, "libstateright_gpu.so")
 
 SR_MODEL_LINEAR_EQUATION = 1
 SR_MODEL_BINARY_CLOCK = 2

@@ -83,6 +83,8 @@ class Engine final : public EngineBase {
         // the visited-set load factor the capacity hint is sized for.
         if (const char* e = std::getenv("SR_PROBE_BATCH")) probe_batch_ = std::atoi(e);
         if (const char* e = std::getenv("SR_TABLE_LOAD")) table_load_ = std::atof(e);
+        if (const char* e = std::getenv("SR_PROBE_LOAD")) probe_load_ = std::atoi(e);
+        if (const char* e = std::getenv("SR_PPW_LOG2")) ppw_env_ = std::atoi(e);
     }
     ~Engine() override = default;
 
@@ -548,15 +550,22 @@ class Engine final : public EngineBase {
                 const u32 ncap = (u32)std::min<u64>(arena_cap_ - nbase, 0xffffffffu);
                 u64* next = arena_.p + nbase * W;
                 u32* npar = apar_.p + nbase;
+                // Parents per wave: 64 (measured: spreading small levels over more waves with fewer
+                // parents each is slower, SR_PPW_LOG2 sweep in profiles/).
+                u32 ppw_log2 = ppw_env_ >= 0 ? (u32)ppw_env_ : 6;
+                const u32 grid = blocks_for((c + (1u << ppw_log2) - 1) >> ppw_log2, 4);
                 timed([&] {
                     auto launch = [&](auto kern) {
-                        kern<<<blocks_for(c, 256), 256, 0, stream_>>>(m_, cur(), ulo, uhi, view(), next, npar, ncap, lc_d_,
-                                                                      undiscovered, ctx_->hc_dev, sq, last ? 1u : 0u);
+                        kern<<<grid, 256, 0, stream_>>>(m_, cur(), ulo, uhi, view(), next, npar, ncap, lc_d_,
+                                                        undiscovered, ctx_->hc_dev, sq, last ? 1u : 0u, ppw_log2);
                     };
-                    switch (probe_batch_) {
-                        case 2: launch(expand_fast<M, 2>); break;
-                        case 4: launch(expand_fast<M, 4>); break;
-                        default: launch(expand_fast<M, 1>); break;
+                    switch (probe_batch_ * 10 + probe_load_) {
+                        case 11: launch(expand_fast<M, 1, 1>); break;
+                        case 12: launch(expand_fast<M, 1, 2>); break;
+                        case 13: launch(expand_fast<M, 1, 3>); break;
+                        case 20: launch(expand_fast<M, 2, 0>); break;
+                        case 21: launch(expand_fast<M, 2, 1>); break;
+                        default: launch(expand_fast<M, 1, 0>); break;
                     }
                 });
             }
@@ -601,6 +610,8 @@ class Engine final : public EngineBase {
     u32 D_;  // max successors of one state (bounds the new states a chunk can create)
     bool fifo_ = false;
     int probe_batch_ = 1;
+    int probe_load_ = 0;
+    int ppw_env_ = -1;
     bool pessimistic_ = false;  // size chunks for max out-degree new states per parent
     u64 grow_factor_ = 1;       // initial-capacity multiplier after a capacity restart
     double ratio_ = 1.0;        // new states per expanded parent in the last level

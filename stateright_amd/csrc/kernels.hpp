@@ -61,17 +61,20 @@ struct HostCounters {
     u32 seq;               // written last: the launch's sequence number
 };
 
+template <int NP>
 __device__ __forceinline__ void reset_counters(LevelCounters* lc) {
     lc->successors = 0;
     lc->claims = 0;
     lc->err = 0;
 #pragma unroll
-    for (int p = 0; p < MAX_PROPS; ++p) lc->disc[p] = ~0u;
+    for (int p = 0; p < NP; ++p) lc->disc[p] = ~0u;
 }
 
 // Called by every workgroup after its last counter update (all threads). The workgroup that
 // arrives last copies the counters to host memory, optionally resets them for the next level,
-// and finally stores `seq` (Guideline 16: release before the ticket, acquire after it).
+// and finally stores `seq` (Guideline 16: release before the ticket, acquire after it). NP = the
+// number of properties whose discovery ranks are live.
+template <int NP>
 __device__ __forceinline__ void publish(LevelCounters* lc, HostCounters* h, u32 seq, bool reset, const u32* aux) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -85,8 +88,9 @@ __device__ __forceinline__ void publish(LevelCounters* lc, HostCounters* h, u32 
     h->claims = __hip_atomic_load(&lc->claims, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     h->err = __hip_atomic_load(&lc->err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     h->aux = aux ? __hip_atomic_load(aux, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
-    for (int p = 0; p < MAX_PROPS; ++p) h->disc[p] = __hip_atomic_load(&lc->disc[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (reset) reset_counters(lc);
+#pragma unroll
+    for (int p = 0; p < NP; ++p) h->disc[p] = __hip_atomic_load(&lc->disc[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (reset) reset_counters<NP>(lc);
     lc->ticket = 0;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: host memory
     __hip_atomic_store(&h->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -94,11 +98,22 @@ __device__ __forceinline__ void publish(LevelCounters* lc, HostCounters* h, u32 
 
 // Standalone publish (after kernels that do not publish themselves).
 __global__ void publish_kernel(LevelCounters* lc, HostCounters* h, u32 seq, u32 reset, const u32* aux) {
-    publish(lc, h, seq, reset != 0, aux);
+    publish<MAX_PROPS>(lc, h, seq, reset != 0, aux);
+}
+
+// Probe loads of the visited set. POL selects the cache policy of the plain probe load:
+// 0 default, 1 agent-scope relaxed atomic load (sc1), 2 non-temporal, 3 system-scope (sc0 sc1).
+template <int POL>
+__device__ __forceinline__ u64 probe_load(const u64* p) {
+    if constexpr (POL == 1) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else if constexpr (POL == 2) return __builtin_nontemporal_load(p);
+    else if constexpr (POL == 3) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    else return *p;
 }
 
 // Find `key` or claim a vacant slot for it, starting at slot i whose key `cur` was already loaded.
 // Returns the slot; *is_new tells whether we claimed it.
+template <int POL = 0>
 __device__ __forceinline__ u64 find_or_claim_from(const TableView& t, u64 key, u64 i, u64 cur, bool* is_new, u32* err) {
     for (int probe = 0; probe < MAX_PROBE; ++probe) {
         if (cur == key) {
@@ -118,7 +133,7 @@ __device__ __forceinline__ u64 find_or_claim_from(const TableView& t, u64 key, u
             }
         }
         i = (i + 1) & t.mask;
-        cur = t.keys[i];
+        cur = probe_load<POL>(&t.keys[i]);
     }
     atomicOr(err, (u32)ERR_TABLE_FULL);
     *is_new = false;
@@ -254,11 +269,11 @@ __device__ __forceinline__ u32 select_bit(u64 m, u32 k) {
 // the workgroup reserves its span of the next frontier with ONE global atomic, copies the staged
 // states out contiguously, and evaluates the properties there (rank = frontier position). A
 // workgroup that stages more than STAGE states appends the overflow directly.
-template <class M, int PB>
+template <class M, int PB, int POL>
 __global__ void __launch_bounds__(256) expand_fast(M m, const u64* __restrict__ frontier, u32 lo, u32 hi,
                                                    TableView t, u64* __restrict__ next, u32* __restrict__ next_par,
                                                    u32 next_cap, LevelCounters* lc, u32 undiscovered,
-                                                   HostCounters* hc, u32 seq, u32 reset) {
+                                                   HostCounters* hc, u32 seq, u32 reset, u32 ppw_log2) {
     constexpr int W = M::W, MW = M::MW;
     constexpr int STAGE = 1024 / W;
     __shared__ u64 stage[STAGE * W];
@@ -270,9 +285,13 @@ __global__ void __launch_bounds__(256) expand_fast(M m, const u64* __restrict__ 
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     if (threadIdx.x == 0) stage_n = 0;
 
-    const u32 r = lo + blockIdx.x * blockDim.x + threadIdx.x;
+    // Each wave takes ppw = 2^ppw_log2 <= 64 parents (small levels use fewer parents per wave so
+    // that their successors spread over more waves: shorter per-lane probe chains).
+    const u32 ppw = 1u << ppw_log2;
+    const u32 wave0 = lo + ((blockIdx.x * (blockDim.x >> 6) + wid) << ppw_log2);  // first parent of the wave
+    const u32 r = wave0 + lane;
     u32 cnt = 0;
-    if (r < hi) {
+    if (lane < ppw && r < hi) {
         u64 s[W], mk[MW];
         load_state<W>(frontier, r, s);
         m.enabled(s, mk);
@@ -338,16 +357,16 @@ __global__ void __launch_bounds__(256) expand_fast(M m, const u64* __restrict__ 
             idx[j] = key[j] & t.mask;
         }
 #pragma unroll
-        for (int j = 0; j < PB; ++j) cur[j] = ok[j] ? t.keys[idx[j]] : 0;
+        for (int j = 0; j < PB; ++j) cur[j] = ok[j] ? probe_load<POL>(&t.keys[idx[j]]) : 0;
 #pragma unroll
         for (int j = 0; j < PB; ++j) {
             if (!ok[j]) continue;
             ++succ;
             if (cur[j] == key[j]) continue;  // the common case: an already visited state
             bool is_new;
-            find_or_claim_from(t, key[j], idx[j], cur[j], &is_new, &lc->err);
+            find_or_claim_from<POL>(t, key[j], idx[j], cur[j], &is_new, &lc->err);
             if (!is_new) continue;
-            const u32 pr = lo + blockIdx.x * blockDim.x + wid * 64 + par[j];  // parent rank
+            const u32 pr = wave0 + par[j];  // parent rank
             u32 kk = atomicAdd(&stage_n, 1u);
             if (kk < (u32)STAGE) {
 #pragma unroll
@@ -385,7 +404,7 @@ __global__ void __launch_bounds__(256) expand_fast(M m, const u64* __restrict__ 
         }
         eval_props(m, ns, pos, undiscovered, lc);
     }
-    publish(lc, hc, seq, reset != 0, nullptr);
+    publish<M::NPROPS>(lc, hc, seq, reset != 0, nullptr);
 }
 
 // FIFO order, pass 1: insert-or-find every successor and record (level, parent rank, slot) in
@@ -424,7 +443,7 @@ __global__ void __launch_bounds__(256) expand_fifo(M m, const u64* __restrict__ 
         if (ts) atomicAdd(reinterpret_cast<unsigned long long*>(&lc->successors), (unsigned long long)ts);
         if (tc) atomicAdd(&lc->claims, tc);
     }
-    publish(lc, hc, seq, false, nullptr);
+    publish<M::NPROPS>(lc, hc, seq, false, nullptr);
 }
 
 // FIFO pass 2: number of successors each parent owns.
@@ -478,7 +497,7 @@ __global__ void __launch_bounds__(256) scatter_fifo(M m, const u64* __restrict__
                                                     LevelCounters* lc, u32 undiscovered, HostCounters* hc, u32 seq,
                                                     const u32* owners) {
     scatter_fifo_body(m, frontier, cand, offs, n, A, level, t, next, next_par, lc, undiscovered);
-    publish(lc, hc, seq, true, owners);
+    publish<M::NPROPS>(lc, hc, seq, true, owners);
 }
 
 
