@@ -22,6 +22,7 @@
  *   sr_gpu_bfs_visits             <- StateRecorder visitor            src/checker/visitor.rs:70-99
  *   sr_gpu_bfs_free               <- Drop of the checker (join(self) consumes it in Rust)
  *   sr_last_error                 <- the reference panics; see "Errors" below
+ *   sr_dist_* / sr_gpu_bfs_spawn_partitioned <- new: the visited set partitioned over GPUs
  *
  * Models: device code cannot call host function pointers, so `impl Model` becomes a registry of
  * compiled-in GpuModel encodings selected by `model_id` + integer parameters (SR_MODEL_*). Each
@@ -146,6 +147,23 @@ int32_t sr_gpu_bfs_replay(const sr_bfs* bfs, int32_t init_index, const int64_t* 
 /* Visited states in visit order (record_visits=1), describe_width int64s each; returns count*width. */
 int64_t sr_gpu_bfs_visits(const sr_bfs* bfs, int64_t* out, int64_t cap);
 void sr_gpu_bfs_free(sr_bfs* bfs);
+
+/* ---- Partitioned search over several GPUs (no counterpart in the reference,
+ * which is single-process shared-memory: src/checker/bfs.rs:70-152) ----
+ * One process per GPU. Rank 0 creates a unique id, every rank receives it out of band (e.g. a
+ * torch.distributed broadcast) and calls sr_dist_init with its rank; RCCL then carries one
+ * all-gather and one all-to-all of successor records per BFS level over xGMI. Counts reported by
+ * every rank are global. Discovery paths are collective: every rank must call
+ * sr_gpu_bfs_discovery(_path) for the same property in the same order. */
+#define SR_DIST_ID_BYTES 128
+typedef struct sr_dist sr_dist;
+int32_t sr_dist_unique_id(uint8_t* id_out);
+sr_dist* sr_dist_init(int32_t rank, int32_t world, const uint8_t* id, int32_t device);
+void sr_dist_free(sr_dist* comm);
+/* comm == NULL: `virtual_partitions` partitions in this process on opts->device (same protocol,
+ * device-copy exchange). FAST order only. */
+sr_bfs* sr_gpu_bfs_spawn_partitioned(sr_dist* comm, int32_t virtual_partitions, int32_t model_id,
+                                     const int64_t* params, int32_t nparams, const sr_opts* opts);
 
 #ifdef __cplusplus
 }

@@ -81,7 +81,14 @@ SIGNATURES = [
                                            ctypes.POINTER(ctypes.c_int32), ctypes.c_int32]),
     ("sr_gpu_bfs_visits", ctypes.c_int64, [_P, _I64P, ctypes.c_int64]),
     ("sr_gpu_bfs_free", None, [_P]),
+    ("sr_dist_unique_id", ctypes.c_int32, [ctypes.c_char_p]),
+    ("sr_dist_init", _P, [ctypes.c_int32, ctypes.c_int32, ctypes.c_char_p, ctypes.c_int32]),
+    ("sr_dist_free", None, [_P]),
+    ("sr_gpu_bfs_spawn_partitioned", _P, [_P, ctypes.c_int32, ctypes.c_int32, _I64P, ctypes.c_int32,
+                                          ctypes.POINTER(sr_opts)]),
 ]
+
+SR_DIST_ID_BYTES = 128
 
 _lib = None
 

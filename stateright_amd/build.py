@@ -4,7 +4,8 @@ import subprocess
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 SRC = os.path.join(HERE, "csrc", "engine.hip")
-DEPS = [os.path.join(HERE, "csrc", f) for f in ("engine.hip", "kernels.hpp", "models.hpp", "device.hpp")] + [
+DEPS = [os.path.join(HERE, "csrc", f) for f in ("engine.hip", "kernels.hpp", "kernels_dist.hpp", "dist.hpp",
+                                                "models.hpp", "device.hpp")] + [
     os.path.join(os.path.dirname(HERE), "include", "stateright_gpu.h")]
 OUT = os.path.join(HERE, "libstateright_gpu.so")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
@@ -14,7 +15,7 @@ def build(force=False, verbose=False):
     if not force and os.path.exists(OUT) and all(os.path.getmtime(OUT) >= os.path.getmtime(d) for d in DEPS):
         return OUT
     cmd = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
-           "-o", OUT + ".tmp", SRC]
+           "-o", OUT + ".tmp", SRC, "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
     if verbose:
         print(" ".join(cmd))
     subprocess.check_call(cmd)

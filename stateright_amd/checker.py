@@ -84,6 +84,8 @@ class CheckerBuilder:
         self._opts.struct_size = ctypes.sizeof(N.sr_opts)
         self._threads = 1
         self._visitor = None
+        self._partitions = 1
+        self._comm = None
 
     # --- options mirrored from the reference ---------------------------------------------------
     def threads(self, thread_count):
@@ -124,6 +126,18 @@ class CheckerBuilder:
         self._opts.device = int(ordinal)
         return self
 
+    def partitions(self, n):
+        """Partition the visited set into `n` virtual partitions on one GPU (the multi-GPU protocol
+        with a device-copy exchange; FAST order)."""
+        self._partitions = int(n)
+        return self
+
+    def comm(self, communicator):
+        """Partition the search over the GPUs of a `stateright_amd.distributed.Communicator`
+        (one process per GPU, RCCL all-to-all per level; FAST order)."""
+        self._comm = communicator
+        return self
+
     def profile(self, on=True):
         self._opts.profile = int(bool(on))
         return self
@@ -135,6 +149,10 @@ class CheckerBuilder:
     # --- spawn ---------------------------------------------------------------------------------
     def spawn_bfs(self):
         """`spawn_bfs` (src/checker.rs:124-129): non-blocking; call `join()`."""
+        if self._comm is not None or self._partitions > 1:
+            if self._visitor is not None:
+                raise NotImplementedError("visit recording is a single-GPU feature")
+            return GpuBfsChecker(self._model, self._opts, None, comm=self._comm, partitions=self._partitions)
         return GpuBfsChecker(self._model, self._opts, self._visitor)
 
     spawn_gpu_bfs = spawn_bfs
@@ -146,14 +164,19 @@ class CheckerBuilder:
 class GpuBfsChecker:
     """The `Checker` trait (src/checker.rs:184-338) implemented by the MI355X engine."""
 
-    def __init__(self, model, opts, visitor=None):
+    def __init__(self, model, opts, visitor=None, comm=None, partitions=1):
         lib = N.load()
         self._lib = lib
         self._model = model
         self._visitor = visitor
+        self._comm = comm
         params = list(model.params())
         arr = (ctypes.c_int64 * max(1, len(params)))(*params)
-        self._h = lib.sr_gpu_bfs_spawn(model.MODEL_ID, arr, len(params), ctypes.byref(opts))
+        if comm is not None or partitions > 1:
+            self._h = lib.sr_gpu_bfs_spawn_partitioned(comm.handle if comm is not None else None, partitions,
+                                                       model.MODEL_ID, arr, len(params), ctypes.byref(opts))
+        else:
+            self._h = lib.sr_gpu_bfs_spawn(model.MODEL_ID, arr, len(params), ctypes.byref(opts))
         if not self._h:
             raise CheckerError("sr_gpu_bfs_spawn")
         self._joined = False

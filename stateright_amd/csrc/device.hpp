@@ -90,6 +90,7 @@ struct DBuf {
     DBuf() = default;
     DBuf(const DBuf&) = delete;
     DBuf& operator=(const DBuf&) = delete;
+    DBuf(DBuf&& o) noexcept { swap(o); }
     ~DBuf() { reset(); }
     void reset() {
         if (p) DevicePool::get().free(dev, p, n * sizeof(T));

@@ -1,0 +1,520 @@
+// Partitioned breadth-first search over T visited-set partitions.
+//
+// One partition per GPU, one process per GPU, RCCL over xGMI (`Comm`), or T virtual partitions
+// in one process on one GPU (the same level loop with device copies as the exchange: this is how
+// the protocol is tested on a single device). FAST order only (the reference's single-threaded
+// FIFO order is a single-GPU mode).
+//
+// One level, per partition p:
+//   1. expand_route: local successors are inserted directly; the others become records for their
+//      owner's send bucket.
+//   2. one all-gather of a row per partition: records per destination, frontier size, successors,
+//      local claims, error bits, discovery ranks (every rank then knows the level's global totals
+//      and the full T x T record matrix).
+//   3. all-to-all of the records (ncclSend/ncclRecv in one group; a device copy to itself).
+//   4. insert_recv: owners insert what they received; the next frontier = local + received new.
+// Capacity planning is optimistic; an overflow on any partition is seen by every rank in the
+// next all-gather and all of them restart the check together with larger buffers.
+#pragma once
+#include <rccl/rccl.h>
+
+#include "kernels_dist.hpp"
+
+namespace sr {
+
+#define SR_NCCL(expr)                                                                         \
+    do {                                                                                      \
+        ncclResult_t r_ = (expr);                                                             \
+        if (r_ != ncclSuccess)                                                                \
+            throw ::sr::Error(SR_ERR_HIP, std::string(#expr) + ": " + ncclGetErrorString(r_)); \
+    } while (0)
+
+struct Comm {
+    int rank = 0, world = 1, device = 0;
+    ncclComm_t nccl = nullptr;
+};
+
+template <class M>
+class DistEngine final : public EngineBase {
+    static constexpr int W = M::W, REC = W + 1;
+    static constexpr u64 NONE = ~0ull;
+
+    struct Part {
+        u32 id = 0;                      // global partition id
+        DBuf<u64> keys;
+        u64 cap = 0;
+        DBuf<u64> arena;                 // owned states, every level, visit order
+        DBuf<u64> apar;                  // parent gid of each arena state
+        u64 arena_cap = 0;
+        std::vector<u64> lstart{0};      // arena offset of each level
+        DBuf<u64> send;                  // [T][bucket_cap][REC]
+        u64 bucket_cap = 0;
+        DBuf<u32> sendc;                 // [T] records per destination (device)
+        DBuf<u64> recv;
+        u64 recv_cap = 0;
+        LevelCounters* lc = nullptr;
+        HostCounters* hc = nullptr;      // pinned host
+        HostCounters* hc_dev = nullptr;
+        u32 seq = 0;
+        HostCounters last{};             // last published snapshot
+        u64 n = 0;                       // current frontier size
+        u64 uniq = 0;                    // states claimed in this partition's visited set
+        TableView view() const { return TableView{keys.p, nullptr, cap - 1}; }
+    };
+
+  public:
+    DistEngine(M m, const sr_opts& o, Comm* comm, int virtual_parts)
+        : m_(m), o_(o), comm_(comm), D_((u32)m.max_out_degree()) {
+        disc.resize(M::NPROPS);
+        T_ = comm_ ? (u32)comm_->world : (u32)std::max(1, virtual_parts);
+        if (T_ > (u32)MAX_PARTS) throw Error(SR_ERR_ARG, "at most 64 partitions");
+        const u32 L = comm_ ? 1 : T_;
+        parts_.resize(L);
+        for (u32 i = 0; i < L; ++i) parts_[i].id = comm_ ? (u32)comm_->rank : i;
+    }
+    ~DistEngine() override {
+        for (auto& p : parts_) {
+            if (p.lc) (void)hipFree(p.lc);
+            if (p.hc) (void)hipHostFree(p.hc);
+        }
+        if (stream_) (void)hipStreamDestroy(stream_);
+    }
+
+    int nprops() const override { return M::NPROPS; }
+    const char* prop_name(int p) const override { return m_.prop_name(p); }
+    int expectation(int p) const override { return m_.expectation(p); }
+    int width() const override { return m_.describe_width(); }
+    std::string action_name(i64 id) const override { return m_.action_name(id); }
+    i64 action_id_bound() const override { return m_.action_id_bound(); }
+    int init_count() const override {
+        u64 inits[8 * W];
+        return m_.init_states(inits);
+    }
+    int replay(int, const i64*, int, std::vector<i64>&, std::vector<int>&) const override { return -1; }
+    std::vector<i64> visits() const override { return {}; }
+    int partitions() const { return (int)T_; }
+    bool early_exit() const { return early_exit_; }
+
+    void run() override {
+        SR_HIP(hipSetDevice(o_.device));
+        if (!stream_) SR_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+        for (auto& p : parts_) {
+            if (!p.lc) {
+                SR_HIP(hipMalloc(&p.lc, sizeof(LevelCounters)));
+                SR_HIP(hipHostMalloc(&p.hc, sizeof(HostCounters), hipHostMallocCoherent | hipHostMallocMapped));
+                SR_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&p.hc_dev), p.hc, 0));
+                std::memset(p.hc, 0, sizeof(HostCounters));
+            }
+        }
+        for (int attempt = 0;; ++attempt) {
+            try {
+                run_once();
+                return;
+            } catch (const Error& e) {
+                if (e.code != SR_ERR_CAPACITY || attempt >= 3) throw;
+                if (o_.verbose) std::fprintf(stderr, "[sr] %s; restarting with larger buffers\n", e.what());
+                pessimistic_ = true;
+                grow_factor_ *= 4;
+                SR_HIP(hipStreamSynchronize(stream_));
+            }
+        }
+    }
+
+    // `reconstruct_path` across partitions: walk parent gids (collective in the RCCL mode: every
+    // rank must call it).
+    int chain(int p, std::vector<u64>& out) override {
+        out.clear();
+        std::vector<u64> st;
+        if (!tree_path(p, st)) return 0;
+        for (size_t i = 0; i < st.size() / W; ++i) out.push_back(fingerprint<W>(&st[i * W]));
+        return (int)out.size();
+    }
+    int path(int p, std::vector<i64>& actions, std::vector<i64>& states) override {
+        std::vector<u64> st;
+        if (!tree_path(p, st)) return -1;
+        const int wd = m_.describe_width();
+        const size_t len = st.size() / W;
+        for (size_t i = 0; i < len; ++i) {
+            size_t o = states.size();
+            states.resize(o + wd);
+            m_.describe(&st[i * W], &states[o]);
+            if (i + 1 == len) break;
+            // the first action (in `actions()` order) leading to the next state
+            u64 mask[M::MW];
+            m_.enabled(&st[i * W], mask);
+            bool found = false;
+            const u64 want = fingerprint<W>(&st[(i + 1) * W]);
+            for (int w = 0; w < M::MW && !found; ++w)
+                for (u64 bits = mask[w]; bits && !found; bits &= bits - 1) {
+                    int a = w * 64 + __builtin_ctzll(bits);
+                    u64 ns[W];
+                    if (m_.apply(&st[i * W], a, ns) && fingerprint<W>(ns) == want) {
+                        actions.push_back(m_.action_id(&st[i * W], a));
+                        found = true;
+                    }
+                }
+            if (!found) throw Error(SR_ERR_NONDETERMINISM, "Unable to reconstruct a `Path` across partitions");
+        }
+        return (int)actions.size();
+    }
+
+  private:
+    struct DiscAt {
+        bool found = false;
+        u32 level = 0, part = 0, rank = 0;
+    };
+
+    // ---- exchange ---------------------------------------------------------------------------
+    // All-gather of one row of `words` u64 per partition; returns rows of every partition.
+    std::vector<u64> allgather_rows(const std::vector<u64>& mine, size_t words) {
+        if (!comm_) return mine;  // virtual partitions: all rows are local already
+        DBuf<u64> dsend, drecv;
+        dsend.alloc(o_.device, words);
+        drecv.alloc(o_.device, words * T_);
+        SR_HIP(hipMemcpyAsync(dsend.p, mine.data(), words * 8, hipMemcpyHostToDevice, stream_));
+        SR_NCCL(ncclAllGather(dsend.p, drecv.p, words, ncclUint64, comm_->nccl, stream_));
+        std::vector<u64> all(words * T_);
+        SR_HIP(hipMemcpyAsync(all.data(), drecv.p, words * T_ * 8, hipMemcpyDeviceToHost, stream_));
+        SR_HIP(hipStreamSynchronize(stream_));
+        return all;
+    }
+
+    void wait(Part& p) {
+        volatile u32* flag = &p.hc->seq;
+        for (u64 spin = 1;; ++spin) {
+            if (*flag == p.seq) break;
+            if ((spin & 4095) == 0) {
+                hipError_t e = hipStreamQuery(stream_);
+                if (e != hipSuccess && e != hipErrorNotReady) SR_HIP(e);
+                if (e == hipSuccess && *flag != p.seq) {
+                    if (*flag == p.seq) break;
+                    throw Error(SR_ERR_HIP, "launch finished without publishing its counters");
+                }
+            }
+            _mm_pause();
+        }
+        std::atomic_thread_fence(std::memory_order_acquire);
+        std::memcpy(&p.last, (const void*)p.hc, sizeof(HostCounters));
+    }
+
+    void ensure_arena(Part& p, u64 states) {
+        if (p.arena_cap >= states) return;
+        u64 cap = std::max<u64>(states, p.arena_cap * 2);
+        u64 used = p.lstart.back() + p.last.claims;  // conservative: copy through the newest level
+        used = std::min<u64>(used, p.arena_cap);
+        DBuf<u64> na, np;
+        na.alloc(o_.device, cap * W);
+        np.alloc(o_.device, cap);
+        if (used) {
+            SR_HIP(hipMemcpyAsync(na.p, p.arena.p, used * W * 8, hipMemcpyDeviceToDevice, stream_));
+            SR_HIP(hipMemcpyAsync(np.p, p.apar.p, used * 8, hipMemcpyDeviceToDevice, stream_));
+        }
+        p.arena.swap(na);
+        p.apar.swap(np);
+        p.arena_cap = cap;
+        SR_HIP(hipStreamSynchronize(stream_));
+    }
+
+    void grow_table(Part& p) {
+        DBuf<u64> ok;
+        ok.swap(p.keys);
+        const u64 old_cap = p.cap;
+        p.cap *= 2;
+        p.keys.alloc(o_.device, p.cap);
+        SR_HIP(hipMemsetAsync(p.keys.p, 0, p.cap * 8, stream_));
+        rehash<<<blocks_for(old_cap, 256), 256, 0, stream_>>>(TableView{ok.p, nullptr, old_cap - 1}, old_cap, p.view(), p.lc);
+        SR_HIP(hipGetLastError());
+        SR_HIP(hipStreamSynchronize(stream_));
+        stats.rehashes++;
+    }
+
+    void init_counters(Part& p) {
+        LevelCounters z;
+        std::memset(&z, 0, sizeof(z));
+        for (auto& d : z.disc) d = ~0u;
+        SR_HIP(hipMemcpyAsync(p.lc, &z, sizeof(z), hipMemcpyHostToDevice, stream_));
+    }
+
+    void run_once() {
+        auto t_start = Clock::now();
+        state_count = 0;
+        unique = 0;
+        max_depth = 0;
+        for (auto& d : disc) d = DiscoveryRec{};
+        disc_at_.assign(M::NPROPS, DiscAt{});
+        stats = sr_stats{};
+        stats.words_per_state = W;
+        stats.order_used = SR_ORDER_FAST;
+        const u64 hint = o_.capacity_hint ? o_.capacity_hint : (u64)1 << 22;
+        gl_lstart_.assign(T_, {});
+        gl_off_.assign(T_, 0);
+        const u64 per_part = hint / T_ + 1;
+
+        // ---- partitions: visited sets, arenas, level 0 ----
+        u64 inits[8 * W];
+        int k = m_.init_states(inits);
+        std::vector<u64> rev(k * W);
+        for (int i = 0; i < k; ++i) std::copy(&inits[i * W], &inits[i * W] + W, &rev[(k - 1 - i) * W]);
+        DBuf<u64> dinit;
+        DBuf<u32> dn;
+        dinit.alloc(o_.device, k * W);
+        dn.alloc(o_.device, 1);
+        SR_HIP(hipMemcpyAsync(dinit.p, rev.data(), rev.size() * 8, hipMemcpyHostToDevice, stream_));
+        u64 roots = 0;
+        for (auto& p : parts_) {
+            u64 cap = (u64)(1u << 16) * grow_factor_;
+            while ((double)cap * 0.5 < (double)per_part * grow_factor_) cap <<= 1;
+            p.uniq = 0;
+            p.cap = cap;
+            p.keys.alloc(o_.device, cap);
+            SR_HIP(hipMemsetAsync(p.keys.p, 0, cap * 8, stream_));
+            p.arena_cap = 0;
+            p.last = HostCounters{};
+            p.lstart.assign(1, 0);
+            ensure_arena(p, (per_part + per_part / 8 + 4096) * grow_factor_);
+            p.sendc.alloc(o_.device, T_);
+            init_counters(p);
+            insert_roots_part<M><<<1, 64, 0, stream_>>>(p.view(), dinit.p, (u32)k, p.id, T_, p.arena.p, p.apar.p, dn.p, p.lc);
+            u32 n0 = 0;
+            SR_HIP(hipMemcpyAsync(&n0, dn.p, 4, hipMemcpyDeviceToHost, stream_));
+            SR_HIP(hipStreamSynchronize(stream_));
+            p.n = n0;
+            if (n0) eval_roots<M><<<blocks_for(n0, 64), 64, 0, stream_>>>(m_, p.arena.p, n0, p.lc, (1u << M::NPROPS) - 1);
+            p.seq++;
+            publish_kernel<<<1, 64, 0, stream_>>>(p.lc, p.hc_dev, p.seq, 1, nullptr);
+            SR_HIP(hipGetLastError());
+            wait(p);
+            roots += p.last.claims;
+            p.uniq = p.last.claims;
+            p.lstart.push_back(p.n);
+        }
+        state_count = (u64)k;
+        // distinct roots: a global sum (each init state is claimed by its owner only)
+        u64 unique_total = roots;
+        glob_prev_n_ = 0;
+        for (auto& p : parts_) glob_prev_n_ += p.n;  // virtual mode: exact; RCCL: own share
+        if (comm_) glob_prev_n_ *= T_;
+        u32 undiscovered = (1u << M::NPROPS) - 1;
+        double ratio = (double)D_;  // non-self-loop successors per parent, last level
+        auto t_loop = Clock::now();
+
+        for (u32 level = 0;; ++level) {
+            // ---- 1. expand + route ----
+            const u64 d_eff = pessimistic_ ? D_ : std::min<u64>(D_, (u64)std::ceil(1.5 * ratio + 1.0));
+            for (auto& p : parts_) {
+                // keep each visited-set partition under 75% load for this level's share of new states
+                const u64 expect_new = (u64)((double)glob_prev_n_ * (double)d_eff / (double)T_ * 1.5) + 1024;
+                while ((double)(p.uniq + expect_new) > 0.75 * (double)p.cap) grow_table(p);
+                const u64 base = p.lstart[p.lstart.size() - 2];
+                // per-destination bucket: its share of every successor, with slack
+                u64 bcap = (u64)((double)p.n * (double)d_eff / (double)T_ * 1.5) + 4096;
+                if (pessimistic_) bcap = p.n * D_ + 4096;
+                if (p.bucket_cap < bcap) {
+                    p.bucket_cap = bcap;
+                    p.send.alloc(o_.device, bcap * T_ * REC);
+                }
+                ensure_arena(p, p.lstart.back() + p.n * d_eff + 4096);
+                SR_HIP(hipMemsetAsync(p.sendc.p, 0, T_ * 4, stream_));
+                const u64 nb = p.lstart.back();
+                const u32 ncap = (u32)std::min<u64>(p.arena_cap - nb, 0xffffffffu);
+                p.seq++;
+                expand_route<M><<<std::max<u32>(1, blocks_for(p.n, 256)), 256, 0, stream_>>>(
+                    m_, p.arena.p + base * W, (u32)p.n, p.view(), p.id, T_, p.arena.p + nb * W, p.apar.p + nb, ncap,
+                    ((u64)p.id << GID_SHIFT) + base, p.send.p, (u32)p.bucket_cap, p.sendc.p, p.lc, undiscovered,
+                    p.hc_dev, p.seq);
+                SR_HIP(hipGetLastError());
+                stats.expand_launches++;
+            }
+            // ---- 2. all-gather one row per partition ----
+            const size_t RW = T_ + 6 + M::NPROPS;
+            std::vector<u64> rows;
+            for (auto& p : parts_) {
+                HostCounters before = p.last;  // the insert (or root) publish of the previous level
+                wait(p);
+                std::vector<u64> row(RW, 0);
+                for (u32 q = 0; q < T_; ++q) row[q] = p.last.sendc[q];
+                row[T_ + 0] = p.n;
+                row[T_ + 1] = p.last.successors;
+                row[T_ + 2] = p.last.claims;  // local new states
+                row[T_ + 3] = p.last.err | before.err;
+                for (int pr = 0; pr < M::NPROPS; ++pr) row[T_ + 6 + pr] = before.disc[pr];
+                rows.insert(rows.end(), row.begin(), row.end());
+            }
+            std::vector<u64> all = allgather_rows(rows, RW * parts_.size());
+            u64 glob_n = 0, glob_succ = 0, glob_err = 0;
+            for (u32 q = 0; q < T_; ++q) {
+                const u64* row = &all[q * RW];
+                gl_lstart_[q].push_back(gl_off_[q]);  // arena offset of this level in partition q
+                gl_off_[q] += row[T_ + 0];
+                glob_n += row[T_ + 0];
+                glob_succ += row[T_ + 1];
+                glob_err |= row[T_ + 3];
+            }
+            if (glob_err & ERR_TABLE_FULL) throw Error(SR_ERR_CAPACITY, "visited set probe limit exceeded");
+            if (glob_err & ERR_FRONTIER_OVERFLOW) throw Error(SR_ERR_CAPACITY, "frontier or send bucket overflow");
+            // discoveries among this level's states: the lowest (partition, rank) per property
+            u32 newly = 0;
+            for (int pr = 0; pr < M::NPROPS; ++pr) {
+                if (!(undiscovered >> pr & 1)) continue;
+                for (u32 q = 0; q < T_; ++q) {
+                    u32 rk = (u32)all[q * RW + T_ + 6 + pr];
+                    if (rk != ~0u) {
+                        disc_at_[pr] = DiscAt{true, level, q, rk};
+                        disc[pr].found = true;
+                        disc[pr].level = level;
+                        disc[pr].rank = rk;
+                        newly |= 1u << pr;
+                        break;
+                    }
+                }
+            }
+            undiscovered &= ~newly;
+            if (glob_n == 0) break;  // frontier exhausted everywhere
+            glob_prev_n_ = glob_n;
+            if (level > 0) unique_total += glob_n;  // every state is in exactly one frontier
+            max_depth = level;
+            unique = unique_total;
+            if (M::NPROPS == 0 || (newly && undiscovered == 0)) {
+                // Early exit: every property discovered in this level (order-dependent in FAST);
+                // this level's (speculative) expansion is not counted.
+                reference_done = true;
+                early_exit_ = true;
+                break;
+            }
+            state_count += glob_succ;
+            stats.successors += glob_succ;
+            ratio = glob_n ? (double)glob_succ / (double)glob_n : ratio;
+
+            // ---- 3. all-to-all of the records ----
+            exchange(all, RW);
+
+            // ---- 4. owners insert what they received ----
+            for (auto& p : parts_) {
+                u64 nrec = 0;
+                for (u32 q = 0; q < T_; ++q) nrec += all[q * RW + p.id];
+                const u64 nb = p.lstart.back();
+                const u64 local_new = all[p.id * RW + T_ + 2];
+                ensure_arena(p, nb + local_new + nrec + 1);
+                const u32 ncap = (u32)std::min<u64>(p.arena_cap - nb, 0xffffffffu);
+                p.seq++;
+                insert_recv<M><<<std::max<u32>(1, blocks_for(nrec, 256)), 256, 0, stream_>>>(
+                    m_, p.recv.p, (u32)nrec, p.view(), p.arena.p + nb * W, p.apar.p + nb, ncap, p.lc, undiscovered,
+                    p.hc_dev, p.seq);
+                SR_HIP(hipGetLastError());
+            }
+            glob_prev_n_ = 0;
+            for (auto& p : parts_) {
+                wait(p);
+                p.n = p.last.claims;  // local + received new states = the next frontier
+                p.uniq += p.n;
+                p.lstart.push_back(p.lstart.back() + p.n);
+            }
+            stats.levels++;
+        }
+        unique = unique_total;
+        auto t_end = Clock::now();
+        stats.level_loop_sec = secs(t_loop, t_end);
+        stats.total_sec = secs(t_start, t_end);
+        stats.table_capacity = parts_[0].cap * T_;
+    }
+
+    void exchange(const std::vector<u64>& all, size_t RW) {
+        // receive buffers
+        for (auto& p : parts_) {
+            u64 nrec = 0;
+            for (u32 q = 0; q < T_; ++q) nrec += all[q * RW + p.id];
+            if (p.recv_cap < nrec + 1) {
+                p.recv_cap = std::max<u64>(nrec + 1, p.recv_cap * 2);
+                p.recv.alloc(o_.device, p.recv_cap * REC);
+            }
+        }
+        if (!comm_) {
+            // virtual partitions: device copies, source-major order
+            for (auto& dst : parts_) {
+                u64 off = 0;
+                for (auto& src : parts_) {
+                    u64 c = all[src.id * RW + dst.id];
+                    if (c) SR_HIP(hipMemcpyAsync(dst.recv.p + off * REC, src.send.p + (u64)dst.id * src.bucket_cap * REC,
+                                                 c * REC * 8, hipMemcpyDeviceToDevice, stream_));
+                    off += c;
+                }
+            }
+            return;
+        }
+        Part& p = parts_[0];
+        const int me = comm_->rank;
+        SR_NCCL(ncclGroupStart());
+        u64 off = 0;
+        for (int peer = 0; peer < comm_->world; ++peer) {
+            u64 sc = all[(u64)me * RW + peer];     // I send to peer
+            u64 rc = all[(u64)peer * RW + me];     // peer sends to me
+            if (peer == me) {
+                if (sc) SR_HIP(hipMemcpyAsync(p.recv.p + off * REC, p.send.p + (u64)me * p.bucket_cap * REC, sc * REC * 8,
+                                              hipMemcpyDeviceToDevice, stream_));
+            } else {
+                if (sc) SR_NCCL(ncclSend(p.send.p + (u64)peer * p.bucket_cap * REC, sc * REC, ncclUint64, peer, comm_->nccl, stream_));
+                if (rc) SR_NCCL(ncclRecv(p.recv.p + off * REC, rc * REC, ncclUint64, peer, comm_->nccl, stream_));
+            }
+            off += rc;
+        }
+        SR_NCCL(ncclGroupEnd());
+    }
+
+    bool tree_path(int pr, std::vector<u64>& st) {
+        if (pr < 0 || pr >= M::NPROPS || !disc_at_.size() || !disc_at_[pr].found) return false;
+        SR_HIP(hipSetDevice(o_.device));
+        const DiscAt d = disc_at_[pr];
+        // gid of the discovered state
+        u64 gid = ((u64)d.part << GID_SHIFT) | (part_lstart(d.part, d.level) + d.rank);
+        std::vector<u64> rev;
+        DBuf<u64> buf;
+        buf.alloc(o_.device, REC);
+        for (int guard = 0; guard < (1 << 20); ++guard) {
+            const u32 owner = (u32)(gid >> GID_SHIFT);
+            const u64 idx = gid & (((u64)1 << GID_SHIFT) - 1);
+            u64 rec[REC];
+            if (!comm_) {
+                Part& p = parts_[owner];
+                SR_HIP(hipMemcpy(rec, p.arena.p + idx * W, W * 8, hipMemcpyDeviceToHost));
+                SR_HIP(hipMemcpy(&rec[W], p.apar.p + idx, 8, hipMemcpyDeviceToHost));
+            } else {
+                if (owner == (u32)comm_->rank) {
+                    Part& p = parts_[0];
+                    SR_HIP(hipMemcpyAsync(buf.p, p.arena.p + idx * W, W * 8, hipMemcpyDeviceToDevice, stream_));
+                    SR_HIP(hipMemcpyAsync(buf.p + W, p.apar.p + idx, 8, hipMemcpyDeviceToDevice, stream_));
+                }
+                SR_NCCL(ncclBroadcast(buf.p, buf.p, REC, ncclUint64, (int)owner, comm_->nccl, stream_));
+                SR_HIP(hipMemcpyAsync(rec, buf.p, REC * 8, hipMemcpyDeviceToHost, stream_));
+                SR_HIP(hipStreamSynchronize(stream_));
+            }
+            rev.insert(rev.end(), rec, rec + W);
+            if (rec[W] == NONE) break;
+            gid = rec[W];
+        }
+        const size_t len = rev.size() / W;
+        st.resize(rev.size());
+        for (size_t i = 0; i < len; ++i) std::copy(&rev[(len - 1 - i) * W], &rev[(len - i) * W], &st[i * W]);
+        return true;
+    }
+
+    // arena offset of `level` in partition `part`, as known on every rank (lstart of remote
+    // partitions is rebuilt from the all-gathered frontier sizes)
+    u64 part_lstart(u32 part, u32 level) { return gl_lstart_[part][level]; }
+
+    M m_;
+    sr_opts o_;
+    Comm* comm_;
+    u32 D_;
+    u32 T_ = 1;
+    std::vector<Part> parts_;
+    hipStream_t stream_ = nullptr;
+    bool pessimistic_ = false;
+    u64 grow_factor_ = 1;
+    bool early_exit_ = false;
+    std::vector<DiscAt> disc_at_;
+    std::vector<std::vector<u64>> gl_lstart_;  // per partition: arena offset of each level
+    std::vector<u64> gl_off_;
+    u64 glob_prev_n_ = 0;  // global frontier size of the level being expanded
+};
+
+}  // namespace sr

@@ -629,34 +629,47 @@ class Engine final : public EngineBase {
     std::vector<u64> lvisited_;  // states of each level that the reference would pop
 };
 
-static std::unique_ptr<EngineBase> make_engine(int model, const i64* p, int np, const sr_opts& o) {
+}  // namespace sr
+
+#include "dist.hpp"
+
+namespace sr {
+
+// The registry below instantiates `E<Model>` for every model; the single-GPU engine and the
+// partitioned engine share it.
+template <template <class> class E, class... Args>
+static std::unique_ptr<EngineBase> make_model_engine(int model, const i64* p, int np, const sr_opts& o, Args... args) {
     auto need = [&](int k) {
         if (np < k) throw Error(SR_ERR_ARG, "model " + std::to_string(model) + " needs " + std::to_string(k) + " params");
     };
     switch (model) {
         case SR_MODEL_LINEAR_EQUATION:
             need(3);
-            return std::make_unique<Engine<LinearEquation>>(LinearEquation{(u32)(p[0] & 0xff), (u32)(p[1] & 0xff), (u32)(p[2] & 0xff)}, o);
+            return std::make_unique<E<LinearEquation>>(LinearEquation{(u32)(p[0] & 0xff), (u32)(p[1] & 0xff), (u32)(p[2] & 0xff)}, o, args...);
         case SR_MODEL_BINARY_CLOCK:
-            return std::make_unique<Engine<BinaryClock>>(BinaryClock{}, o);
+            return std::make_unique<E<BinaryClock>>(BinaryClock{}, o, args...);
         case SR_MODEL_2PC:
             need(1);
             if (p[0] < 1 || p[0] > 14) throw Error(SR_ERR_UNSUPPORTED, "2pc: rm_count must be in 1..=14 (4n+4 <= 63 bits)");
-            return std::make_unique<Engine<TwoPhase>>(TwoPhase{(int)p[0]}, o);
+            return std::make_unique<E<TwoPhase>>(TwoPhase{(int)p[0]}, o, args...);
         case SR_MODEL_INCREMENT:
             need(1);
             if (p[0] < 1 || p[0] > 15) throw Error(SR_ERR_UNSUPPORTED, "increment: threads must be in 1..=15");
-            if (p[0] <= 9) return std::make_unique<Engine<Increment<1>>>(Increment<1>{(int)p[0]}, o);
-            return std::make_unique<Engine<Increment<2>>>(Increment<2>{(int)p[0]}, o);
+            if (p[0] <= 9) return std::make_unique<E<Increment<1>>>(Increment<1>{(int)p[0]}, o, args...);
+            return std::make_unique<E<Increment<2>>>(Increment<2>{(int)p[0]}, o, args...);
         case SR_MODEL_INCREMENT_LOCK:
             need(1);
             if (p[0] < 1 || p[0] > 12) throw Error(SR_ERR_UNSUPPORTED, "increment_lock: threads must be in 1..=12");
-            if (p[0] <= 8) return std::make_unique<Engine<IncrementLock<1>>>(IncrementLock<1>{(int)p[0]}, o);
-            return std::make_unique<Engine<IncrementLock<2>>>(IncrementLock<2>{(int)p[0]}, o);
+            if (p[0] <= 8) return std::make_unique<E<IncrementLock<1>>>(IncrementLock<1>{(int)p[0]}, o, args...);
+            return std::make_unique<E<IncrementLock<2>>>(IncrementLock<2>{(int)p[0]}, o, args...);
         case SR_MODEL_DGRAPH:
             throw Error(SR_ERR_UNSUPPORTED, "dgraph: `eventually` properties are not supported by the GPU engine yet");
     }
     throw Error(SR_ERR_ARG, "unknown model id " + std::to_string(model));
+}
+
+static std::unique_ptr<EngineBase> make_engine(int model, const i64* p, int np, const sr_opts& o) {
+    return make_model_engine<Engine>(model, p, np, o);
 }
 
 }  // namespace sr
@@ -805,6 +818,75 @@ int32_t sr_gpu_bfs_replay(const sr_bfs* b, int32_t init, const int64_t* ids, int
     if (states) std::memcpy(states, s.data(), (size_t)std::min<int64_t>(cap_states, (int64_t)s.size()) * sizeof(int64_t));
     for (int i = 0; i < (int)c.size() && i < cap_conds; ++i) conds[i] = c[i];
     return r;
+}
+
+struct sr_dist {
+    Comm c;
+};
+
+int32_t sr_dist_unique_id(uint8_t* out) {
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) {
+        set_error("ncclGetUniqueId failed");
+        return SR_ERR_HIP;
+    }
+    static_assert(sizeof(ncclUniqueId) == SR_DIST_ID_BYTES, "RCCL unique id size");
+    std::memcpy(out, &id, sizeof(id));
+    return SR_OK;
+}
+
+sr_dist* sr_dist_init(int32_t rank, int32_t world, const uint8_t* idb, int32_t device) {
+    try {
+        if (world < 1 || rank < 0 || rank >= world) throw Error(SR_ERR_ARG, "bad rank/world");
+        SR_HIP(hipSetDevice(device));
+        auto d = std::make_unique<sr_dist>();
+        d->c.rank = rank;
+        d->c.world = world;
+        d->c.device = device;
+        ncclUniqueId id;
+        std::memcpy(&id, idb, sizeof(id));
+        SR_NCCL(ncclCommInitRank(&d->c.nccl, world, id, rank));
+        return d.release();
+    } catch (const std::exception& x) {
+        set_error(x.what());
+        return nullptr;
+    }
+}
+
+void sr_dist_free(sr_dist* d) {
+    if (!d) return;
+    if (d->c.nccl) (void)ncclCommDestroy(d->c.nccl);
+    delete d;
+}
+
+sr_bfs* sr_gpu_bfs_spawn_partitioned(sr_dist* comm, int32_t virtual_parts, int32_t model_id, const int64_t* params,
+                                     int32_t nparams, const sr_opts* opts) {
+    try {
+        sr_opts o;
+        sr_opts_init(&o);
+        if (opts) std::memcpy(&o, opts, std::min<size_t>(sizeof(o), opts->struct_size ? opts->struct_size : sizeof(o)));
+        if (comm) o.device = comm->c.device;
+        if (sr_device_count() <= 0) throw Error(SR_ERR_NO_DEVICE, "no HIP device visible");
+        auto b = std::make_unique<sr_bfs>();
+        b->e = make_model_engine<DistEngine>(model_id, params, nparams, o, comm ? &comm->c : nullptr, (int)virtual_parts);
+        EngineBase* e = b->e.get();
+        b->th = std::thread([e] {
+            try {
+                e->run();
+            } catch (const Error& x) {
+                e->status = x.code;
+                e->error = x.what();
+            } catch (const std::exception& x) {
+                e->status = SR_ERR_HIP;
+                e->error = x.what();
+            }
+            e->finished = true;
+        });
+        return b.release();
+    } catch (const std::exception& x) {
+        set_error(x.what());
+        return nullptr;
+    }
 }
 
 void sr_gpu_bfs_free(sr_bfs* b) {

@@ -26,6 +26,7 @@ constexpr int META_SHIFT = 44;
 constexpr u32 CAND_NONE = 0xffffffffu;
 constexpr int MAX_PROBE = 1 << 16;
 constexpr int MAX_PROPS = 32;
+constexpr int MAX_PARTS = 64;  // visited-set partitions (one per GPU, or virtual ones on one GPU)
 
 enum ErrBits { ERR_TABLE_FULL = 1, ERR_FRONTIER_OVERFLOW = 2 };
 
@@ -58,6 +59,7 @@ struct HostCounters {
     u32 err;
     u32 aux;               // launch-specific value (FIFO: number of owners from the scan)
     u32 disc[MAX_PROPS];
+    u32 sendc[MAX_PARTS];  // partitioned search: records routed to each partition
     u32 seq;               // written last: the launch's sequence number
 };
 
@@ -75,7 +77,8 @@ __device__ __forceinline__ void reset_counters(LevelCounters* lc) {
 // and finally stores `seq` (Guideline 16: release before the ticket, acquire after it). NP = the
 // number of properties whose discovery ranks are live.
 template <int NP>
-__device__ __forceinline__ void publish(LevelCounters* lc, HostCounters* h, u32 seq, bool reset, const u32* aux) {
+__device__ __forceinline__ void publish(LevelCounters* lc, HostCounters* h, u32 seq, bool reset, const u32* aux,
+                                        const u32* sendc = nullptr, u32 nparts = 0) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x != 0) return;
@@ -90,6 +93,7 @@ __device__ __forceinline__ void publish(LevelCounters* lc, HostCounters* h, u32 
     h->aux = aux ? __hip_atomic_load(aux, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
 #pragma unroll
     for (int p = 0; p < NP; ++p) h->disc[p] = __hip_atomic_load(&lc->disc[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (u32 q = 0; q < nparts; ++q) h->sendc[q] = __hip_atomic_load(&sendc[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (reset) reset_counters<NP>(lc);
     lc->ticket = 0;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: host memory

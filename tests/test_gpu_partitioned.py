@@ -1,0 +1,86 @@
+"""The partitioned (multi-GPU) search protocol on one MI355X: T virtual partitions exchanging
+successor records by device copies, and a one-rank RCCL communicator (the RCCL code path with a
+self-exchange). Counts must equal the oracle's on every full-exploration config; every discovery
+path must replay on the CPU oracle model."""
+import math
+
+import pytest
+
+from oracle_lib import BINARY_CLOCK, INCREMENT_LOCK, LINEAR_EQUATION, TWO_PHASE, OracleRun, replay
+
+pytestmark = pytest.mark.gpu
+sr = pytest.importorskip("stateright_amd")
+
+MODELS = {
+    LINEAR_EQUATION: lambda p: sr.LinearEquation(*p),
+    BINARY_CLOCK: lambda p: sr.BinaryClock(),
+    TWO_PHASE: lambda p: sr.TwoPhaseSys(*p),
+    INCREMENT_LOCK: lambda p: sr.IncrementLock(*p),
+}
+CASES = [(LINEAR_EQUATION, [2, 4, 7]), (BINARY_CLOCK, [])] + [(TWO_PHASE, [n]) for n in (1, 2, 3, 5, 7)] + [
+    (INCREMENT_LOCK, [n]) for n in (2, 5, 7, 9)]
+
+
+def ids(c):
+    return {LINEAR_EQUATION: "lineq", BINARY_CLOCK: "clock", TWO_PHASE: "2pc", INCREMENT_LOCK: "inclock"}[c[0]] + \
+        "-" + "-".join(map(str, c[1]))
+
+
+_cache = {}
+
+
+def oracle(model, params):
+    k = (model, tuple(params))
+    if k not in _cache:
+        _cache[k] = OracleRun(model, params)
+    return _cache[k]
+
+
+@pytest.mark.parametrize("parts", [1, 2, 3, 4, 8])
+@pytest.mark.parametrize("case", CASES, ids=ids)
+def test_partitioned_counts_match_oracle(case, parts):
+    model, params = case
+    o = oracle(model, params)
+    c = MODELS[model](params).checker().partitions(parts).spawn_bfs().join()
+    assert c.unique_state_count() == o.unique_state_count
+    assert c.state_count() == o.state_count
+    assert c.max_depth() == o.max_depth
+    assert sorted(c.discoveries()) == o.discovery_names()
+
+
+@pytest.mark.parametrize("parts", [2, 5])
+def test_partitioned_paths_replay(parts):
+    c = sr.TwoPhaseSys(5).checker().partitions(parts).spawn_bfs().join()
+    o = oracle(TWO_PHASE, [5])
+    props = [n for n, _ in c.properties()]
+    for name, path in c.discoveries().items():
+        states, holds = replay(TWO_PHASE, [5], path.action_ids, n_props=len(props))
+        assert holds[props.index(name)] == 1
+        assert len(path) == len(o.discovery_actions(name))
+
+
+def test_partitioned_large_closed_form():
+    n = 9
+    c = sr.TwoPhaseSys(n).checker().partitions(8).capacity_hint(6 ** n + 4 ** n + 2 ** n).spawn_bfs().join()
+    assert c.unique_state_count() == 6 ** n + 4 ** n + 2 ** n
+    assert 3 * c.state_count() == 4 * n * 6 ** n + 3 * (n + 1) * 4 ** n + 3 * n * 2 ** n + 6
+    assert c.max_depth() == 3 * n + 1
+
+
+def test_partitioned_restart_on_overflow():
+    # A tiny capacity hint forces the optimistic buffers to overflow; the check restarts and stays exact.
+    c = sr.IncrementLock(8).checker().partitions(4).capacity_hint(10).spawn_bfs().join()
+    n = 8
+    expect = 1 + 4 * sum(math.factorial(n) // math.factorial(n - k) for k in range(1, n + 1))
+    assert c.unique_state_count() == expect
+
+
+def test_rccl_single_rank():
+    from stateright_amd.distributed import Communicator
+    comm = Communicator(0, 1, Communicator.unique_id(), 0)
+    c = sr.TwoPhaseSys(6).checker().comm(comm).spawn_bfs().join()
+    o = oracle(TWO_PHASE, [6]) if False else OracleRun(TWO_PHASE, [6])
+    assert (c.unique_state_count(), c.state_count(), c.max_depth()) == (o.unique_state_count, o.state_count, o.max_depth)
+    assert sorted(c.discoveries()) == o.discovery_names()
+    del c
+    comm.close()
