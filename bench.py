@@ -8,9 +8,11 @@ set is inside the timed region).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
 
-N > 1 runs under torch.distributed.run, one process per GPU. The search itself is not yet
-partitioned across GPUs in this round, so every rank checks its own full replica ("replicas",
-weak scaling); value = total unique states checked by all ranks / max-over-ranks time.
+N > 1 runs under torch.distributed.run, one process per GPU, and partitions ONE check over the
+GPUs: the visited set and frontier are hash-partitioned by fingerprint owner and
+every BFS level does one RCCL all-gather + one all-to-all of successor records over xGMI. The
+workload stays 2pc N=9 at every N ("scaling": "strong"); value = unique states of the check /
+max-over-ranks time. `--mode replicas` instead runs an independent full check per GPU.
 
 Prints ONE JSON line on rank 0 with `roofline` (dominant kernel = the expand kernel, HIP-event
 timed on its own stream inside the engine) and `cpu_baseline` (the CPU restatement of the
@@ -40,6 +42,8 @@ def parse():
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU restatement (rank 0, N=1)")
     ap.add_argument("--cpu-threads", type=int, default=16, help="host threads for the CPU baseline")
     ap.add_argument("--cpu-rm-count", type=int, default=8, help="2pc size of the bounded CPU sample")
+    ap.add_argument("--mode", default="partitioned", choices=["partitioned", "replicas"],
+                    help="N>1: one check partitioned over the GPUs, or one independent check per GPU")
     return ap.parse_args()
 
 
@@ -64,6 +68,20 @@ def cpu_baseline(args):
     }
 
 
+def pmc_traffic(n, world):
+    """Beyond-L2 bytes per expand launch from the committed rocprofv3 PMC passes of this bench
+    (scripts/pmc_traffic.sh -> profiles/pmc_traffic.json), or None if not measured for this config."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        if d.get("rm_count") == n and d.get("n_gpus", 1) == world:
+            return d["bytes_per_launch"]
+    except (OSError, ValueError, KeyError):
+        pass
+    return None
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -82,9 +100,15 @@ def main():
     from stateright_amd import TwoPhaseSys
     n = args.rm_count
     expect_unique = 6 ** n + 4 ** n + 2 ** n
+    partitioned = world > 1 and args.mode == "partitioned"
+    comm = None
+    if partitioned:
+        from stateright_amd.distributed import Communicator
+        comm = Communicator.from_torch(device=dev)
 
     def step(profile=False):
-        b = TwoPhaseSys(n).checker().order(args.order).capacity_hint(expect_unique).device(dev)
+        b = TwoPhaseSys(n).checker().capacity_hint(expect_unique).device(dev)
+        b = b.comm(comm) if partitioned else b.order(args.order)
         if profile:
             b = b.profile()
         c = b.spawn_bfs().join()
@@ -121,20 +145,29 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        u = torch.tensor([unique], dtype=torch.float64, device="cuda")
-        dist.all_reduce(u)
-        unique_total = float(u.item())
+        if partitioned:
+            unique_total = float(unique)  # every rank reports the global count of the shared check
+        else:
+            u = torch.tensor([unique], dtype=torch.float64, device="cuda")
+            dist.all_reduce(u)
+            unique_total = float(u.item())
     else:
         unique_total = float(unique)
 
     if rank != 0:
+        del c
+        if comm is not None:
+            comm.close()
         if dist is not None:
             dist.destroy_process_group()
         return
 
     c, st = last
     avg_launch_ms = kernel_ms / max(1, launches)
+    if partitioned:
+        alg_bytes /= world  # this rank's share of the check's algorithmic bytes
     achieved_gbps = alg_bytes / (kernel_ms * 1e-3) / 1e9 if kernel_ms else 0.0
+    traffic = pmc_traffic(n, world)
     res = {
         "metric": "unique states/sec (whole node) + HBM GB/s, 2pc N=9 at 1/2/4/8 MI355X",
         "value": unique_total / elapsed,
@@ -144,7 +177,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if (world == 1 or partitioned) else "weak",
         "vs_baseline": None,
         "dtype": "u64",
         "data": "synthetic: the 2pc model's own state space (no dataset)",
@@ -152,18 +185,20 @@ def main():
             "workload": f"2pc N={n} spawn_bfs, full check per step ({expect_unique} unique states)",
             "model": "2pc",
             "rm_count": n,
-            "order": args.order,
-            "parallelism": f"replicas{world}" if world > 1 else "1 GPU",
+            "order": "fast",
+            "parallelism": (f"partitioned{world} (RCCL all-to-all per level)" if partitioned else
+                            f"replicas{world}" if world > 1 else "1 GPU"),
         },
         "state_count_per_sec": float(c.state_count()) * world * args.steps / elapsed,
         "roofline": {
             "bound": "hbm",
-            "kernel": "expand_fast (expand + fingerprint + visited-set insert + append + properties)",
+            "kernel": ("expand_route" if partitioned else "expand_fast") +
+                      " (expand + fingerprint + visited-set probe/claim + append + properties)",
             "achieved": achieved_gbps,
             "peak": HBM_PEAK_GBPS,
             "unit": "GB/s",
             "frac": achieved_gbps / HBM_PEAK_GBPS,
-            "traffic": None,
+            "traffic": traffic,
             "avg_launch_ms": avg_launch_ms,
             "launches_per_step": launches / args.steps,
             "algorithmic_bytes_per_step": alg_bytes / args.steps,
@@ -176,6 +211,8 @@ def main():
         except Exception as e:  # the GPU number stands on its own
             res["cpu_baseline"] = {"error": str(e)}
     print(json.dumps(res))
+    if comm is not None:
+        comm.close()
     if dist is not None:
         dist.destroy_process_group()
 

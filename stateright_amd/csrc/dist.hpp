@@ -77,6 +77,7 @@ class DistEngine final : public EngineBase {
             if (p.lc) (void)hipFree(p.lc);
             if (p.hc) (void)hipHostFree(p.hc);
         }
+        for (auto e : events_) (void)hipEventDestroy(e);
         if (stream_) (void)hipStreamDestroy(stream_);
     }
 
@@ -215,6 +216,15 @@ class DistEngine final : public EngineBase {
         SR_HIP(hipStreamSynchronize(stream_));
     }
 
+    hipEvent_t event(size_t i) {
+        while (events_.size() <= i) {
+            hipEvent_t e;
+            SR_HIP(hipEventCreate(&e));
+            events_.push_back(e);
+        }
+        return events_[i];
+    }
+
     void grow_table(Part& p) {
         DBuf<u64> ok;
         ok.swap(p.keys);
@@ -318,11 +328,13 @@ class DistEngine final : public EngineBase {
                 const u64 nb = p.lstart.back();
                 const u32 ncap = (u32)std::min<u64>(p.arena_cap - nb, 0xffffffffu);
                 p.seq++;
+                if (o_.profile) SR_HIP(hipEventRecord(event(2 * stats.expand_launches), stream_));
                 expand_route<M><<<std::max<u32>(1, blocks_for(p.n, 256)), 256, 0, stream_>>>(
                     m_, p.arena.p + base * W, (u32)p.n, p.view(), p.id, T_, p.arena.p + nb * W, p.apar.p + nb, ncap,
                     ((u64)p.id << GID_SHIFT) + base, p.send.p, (u32)p.bucket_cap, p.sendc.p, p.lc, undiscovered,
                     p.hc_dev, p.seq);
                 SR_HIP(hipGetLastError());
+                if (o_.profile) SR_HIP(hipEventRecord(event(2 * stats.expand_launches + 1), stream_));
                 stats.expand_launches++;
             }
             // ---- 2. all-gather one row per partition ----
@@ -413,6 +425,17 @@ class DistEngine final : public EngineBase {
         }
         unique = unique_total;
         auto t_end = Clock::now();
+        if (o_.profile && stats.expand_launches) {
+            SR_HIP(hipEventSynchronize(event(2 * stats.expand_launches - 1)));
+            double ms = 0;
+            for (u64 i = 0; i < stats.expand_launches; ++i) {
+                float t = 0;
+                SR_HIP(hipEventElapsedTime(&t, event(2 * i), event(2 * i + 1)));
+                ms += t;
+            }
+            stats.expand_kernel_ms = ms;
+        }
+        stats.algorithmic_bytes = stats.successors * 8 + (unique_total) * (16 + 8 * W) + unique_total * 8 * W;
         stats.level_loop_sec = secs(t_loop, t_end);
         stats.total_sec = secs(t_start, t_end);
         stats.table_capacity = parts_[0].cap * T_;
@@ -515,6 +538,7 @@ class DistEngine final : public EngineBase {
     std::vector<std::vector<u64>> gl_lstart_;  // per partition: arena offset of each level
     std::vector<u64> gl_off_;
     u64 glob_prev_n_ = 0;  // global frontier size of the level being expanded
+    std::vector<hipEvent_t> events_;
 };
 
 }  // namespace sr

@@ -1,0 +1,42 @@
+"""world_size-2 gloo run of the partitioned level loop (CPU restatement of dist.hpp's protocol):
+global unique / state counts / depth equal the single-process oracle, and the two visited-set
+partitions are disjoint and cover the state space."""
+import os
+import socket
+
+import pytest
+import torch.multiprocessing as mp
+
+from oracle_lib import TWO_PHASE, OracleRun
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, n, out):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from dist_protocol_ref import partitioned_bfs
+    out[rank] = partitioned_bfs(n)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n", [2, 3, 4])
+def test_two_rank_partitioned_protocol(n):
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(world, _free_port(), n, out), nprocs=world, join=True)
+    o = OracleRun(TWO_PHASE, [n])
+    for r in range(world):
+        unique, state_count, depth, _ = out[r]
+        assert (unique, state_count, depth) == (o.unique_state_count, o.state_count, o.max_depth)
+    # the partitions are disjoint and together hold every state
+    assert sum(out[r][3] for r in range(world)) == o.unique_state_count
