@@ -53,7 +53,8 @@ enum sr_model_id {
     SR_MODEL_2PC = 3,             /* (rm_count<=14) examples/2pc.rs:10-121              */
     SR_MODEL_INCREMENT = 4,       /* (threads<=15)  examples/increment.rs:109-197       */
     SR_MODEL_INCREMENT_LOCK = 5,  /* (threads<=12)  examples/increment_lock.rs:3-107    */
-    SR_MODEL_DGRAPH = 6           /* (expectation, len, v.., len, v..) src/test_util.rs:47-116 */
+    SR_MODEL_DGRAPH = 6,          /* (expectation, len, v.., len, v..) src/test_util.rs:47-116 */
+    SR_MODEL_PAXOS = 7            /* (client_count<=3) examples/paxos.rs:93-263 + src/actor/model.rs */
 };
 
 /* Visit order inside a BFS level. */

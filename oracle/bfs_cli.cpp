@@ -5,6 +5,7 @@
 #include <iostream>
 
 #include "models.hpp"
+#include "paxos.hpp"
 
 using namespace oracle;
 
@@ -36,6 +37,7 @@ int main(int argc, char** argv) {
     if (model == "2pc") return run(TwoPhaseSys{n}, threads, target);
     if (model == "increment") return run(Increment{n}, threads, target);
     if (model == "increment_lock") return run(IncrementLock{n}, threads, target);
+    if (model == "paxos") return run(paxos::PaxosModel{n, 3}, threads, target);
     if (model == "linear_equation") return run(LinearEquation{2, 4, 7}, threads, target);
     std::cerr << "unknown model " << model << "\n";
     return 2;

@@ -2,6 +2,7 @@
 #include <cstring>
 
 #include "models.hpp"
+#include "paxos.hpp"
 
 using namespace oracle;
 
@@ -10,7 +11,7 @@ namespace {
 thread_local std::string g_last_error;
 
 // Model ids are shared with include/stateright_gpu.h (SR_MODEL_*).
-enum ModelId { LINEAR_EQUATION = 1, BINARY_CLOCK = 2, TWO_PHASE = 3, INCREMENT = 4, INCREMENT_LOCK = 5, DGRAPH = 6 };
+enum ModelId { LINEAR_EQUATION = 1, BINARY_CLOCK = 2, TWO_PHASE = 3, INCREMENT = 4, INCREMENT_LOCK = 5, DGRAPH = 6, PAXOS = 7 };
 
 struct HandleBase {
     virtual ~HandleBase() = default;
@@ -89,6 +90,7 @@ auto with_model(int model, const i64* p, int np, F&& f) {
         case INCREMENT: return f(Increment{(size_t)p[0]});
         case INCREMENT_LOCK: return f(IncrementLock{(size_t)p[0]});
         case DGRAPH: return f(make_dgraph(p, np));
+        case PAXOS: return f(paxos::PaxosModel{(size_t)p[0], 3});
     }
     throw std::runtime_error("unknown model id " + std::to_string(model));
 }

@@ -16,6 +16,7 @@ SR_MODEL_2PC = 3
 SR_MODEL_INCREMENT = 4
 SR_MODEL_INCREMENT_LOCK = 5
 SR_MODEL_DGRAPH = 6
+SR_MODEL_PAXOS = 7
 
 SR_ORDER_AUTO, SR_ORDER_FIFO, SR_ORDER_FAST = 0, 1, 2
 SR_ALWAYS, SR_EVENTUALLY, SR_SOMETIMES = 0, 1, 2

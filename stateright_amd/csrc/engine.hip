@@ -19,6 +19,7 @@
 #include "../../include/stateright_gpu.h"
 #include "device.hpp"
 #include "kernels.hpp"
+#include "paxos.hpp"
 
 namespace sr {
 
@@ -662,6 +663,10 @@ static std::unique_ptr<EngineBase> make_model_engine(int model, const i64* p, in
             if (p[0] < 1 || p[0] > 12) throw Error(SR_ERR_UNSUPPORTED, "increment_lock: threads must be in 1..=12");
             if (p[0] <= 8) return std::make_unique<E<IncrementLock<1>>>(IncrementLock<1>{(int)p[0]}, o, args...);
             return std::make_unique<E<IncrementLock<2>>>(IncrementLock<2>{(int)p[0]}, o, args...);
+        case SR_MODEL_PAXOS:
+            need(1);
+            if (p[0] < 1 || p[0] > 3) throw Error(SR_ERR_UNSUPPORTED, "paxos: client_count must be in 1..=3");
+            return std::make_unique<E<Paxos>>(Paxos::make((int)p[0], o.device), o, args...);
         case SR_MODEL_DGRAPH:
             throw Error(SR_ERR_UNSUPPORTED, "dgraph: `eventually` properties are not supported by the GPU engine yet");
     }

@@ -64,3 +64,55 @@ class IncrementLock(_Model):
 
     def params(self):
         return [self.thread_count]
+
+
+class Paxos(_Model):
+    """The paxos example: `PaxosModelCfg { client_count, server_count: 3, network }` with an
+    unordered non-duplicating network (examples/paxos.rs:223-263), checked through ActorModel
+    (src/actor/model.rs:176-327) with a linearizability history (src/actor/register.rs:37-87).
+
+    Action ids are canonical envelope codes (oracle/paxos.hpp `envelope_code`), so a path is
+    comparable with the CPU oracle's."""
+    MODEL_ID = N.SR_MODEL_PAXOS
+
+    def __init__(self, client_count=2, server_count=3):
+        if server_count != 3:
+            raise ValueError("the paxos encoding is compiled for server_count = 3 (examples/paxos.rs:275)")
+        self.client_count = client_count
+        self.server_count = server_count
+
+    def params(self):
+        return [self.client_count]
+
+    KINDS = ("Prepare", "Prepared", "Accept", "Accepted", "Decided", "Put", "Get", "PutOk", "GetOk")
+
+    @staticmethod
+    def deliver(src, dst, kind, *fields):
+        """Action id of `Deliver { src, dst, msg }` (src/actor/model.rs:18-24) in the canonical
+        envelope code (oracle/paxos.hpp `envelope_code`). `fields` follow the reference message:
+        Put(req, value), Get(req), PutOk(req), GetOk(req, value), Prepare(ballot),
+        Prepared(ballot, last_accepted), Accept(ballot, proposal), Accepted(ballot),
+        Decided(ballot, proposal); ballot = (round, id), proposal = (req, requester, value),
+        last_accepted = None or (ballot, proposal)."""
+        k = Paxos.KINDS.index(kind)
+
+        def bal(b):
+            return b[0] * 8 + b[1]
+
+        def acc(a):
+            return 0 if a is None else 1 + a[0][0] * 64 + a[0][1] * 8 + a[1][1]
+
+        def ch(v):
+            return ord(v) if isinstance(v, str) else int(v)
+
+        if kind in ("Prepare", "Accepted"):
+            f = bal(fields[0])
+        elif kind == "Prepared":
+            f = bal(fields[0]) * 4096 + acc(fields[1])
+        elif kind in ("Accept", "Decided"):
+            f = bal(fields[0]) * 16 + fields[1][1]
+        elif kind in ("Put", "Get", "PutOk"):
+            f = fields[0]
+        else:
+            f = fields[0] * 256 + ch(fields[1])
+        return (((f * 16) + k) * 16 + dst) * 16 + src

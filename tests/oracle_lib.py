@@ -12,7 +12,7 @@ ORACLE_DIR = os.path.join(ROOT, "oracle")
 LIB_PATH = os.path.join(ORACLE_DIR, "liboracle.so")
 
 # Model ids shared with include/stateright_gpu.h (SR_MODEL_*).
-LINEAR_EQUATION, BINARY_CLOCK, TWO_PHASE, INCREMENT, INCREMENT_LOCK, DGRAPH = 1, 2, 3, 4, 5, 6
+LINEAR_EQUATION, BINARY_CLOCK, TWO_PHASE, INCREMENT, INCREMENT_LOCK, DGRAPH, PAXOS = 1, 2, 3, 4, 5, 6, 7
 
 _lib = None
 

@@ -60,3 +60,22 @@ def test_unsupported_parameters_rejected():
         pytest.skip("a GPU is visible; covered by the gpu tests")
     arr = (ctypes.c_int64 * 1)(99)
     assert not lib.sr_gpu_bfs_spawn(_native.SR_MODEL_2PC, arr, 1, None)
+
+
+def test_paxos_action_codes_match_golden_encoding():
+    # The product's Deliver encoder and the test-side restatement agree on the reference path.
+    from stateright_amd import Paxos
+    from paxos_golden import PAXOS_VALUE_CHOSEN_PATH
+    ours = [
+        Paxos.deliver(4, 1, "Put", 4, "B"),
+        Paxos.deliver(1, 0, "Prepare", (1, 1)),
+        Paxos.deliver(0, 1, "Prepared", (1, 1), None),
+        Paxos.deliver(1, 2, "Accept", (1, 1), (4, 4, "B")),
+        Paxos.deliver(2, 1, "Accepted", (1, 1)),
+        Paxos.deliver(1, 4, "PutOk", 4),
+        Paxos.deliver(1, 2, "Decided", (1, 1), (4, 4, "B")),
+        Paxos.deliver(4, 2, "Get", 8),
+    ]
+    assert ours == PAXOS_VALUE_CHOSEN_PATH
+    with pytest.raises(ValueError):
+        Paxos(2, server_count=5)

@@ -9,8 +9,9 @@ import math
 
 import pytest
 
-from oracle_lib import (BINARY_CLOCK, INCREMENT, INCREMENT_LOCK, LINEAR_EQUATION, TWO_PHASE, OracleRun,
+from oracle_lib import (BINARY_CLOCK, INCREMENT, INCREMENT_LOCK, LINEAR_EQUATION, PAXOS, TWO_PHASE, OracleRun,
                         replay)
+from paxos_golden import PAXOS_VALUE_CHOSEN_PATH
 
 pytestmark = pytest.mark.gpu
 
@@ -22,6 +23,7 @@ MODELS = {
     TWO_PHASE: lambda p: sr.TwoPhaseSys(*p),
     INCREMENT: lambda p: sr.Increment(*p),
     INCREMENT_LOCK: lambda p: sr.IncrementLock(*p),
+    PAXOS: lambda p: sr.Paxos(*p),
 }
 
 CASES = [
@@ -31,12 +33,12 @@ CASES = [
     (BINARY_CLOCK, []),
 ] + [(TWO_PHASE, [n]) for n in range(1, 8)] + [
     (INCREMENT, [n]) for n in (1, 2, 3, 4, 6, 8, 9, 10, 12)
-] + [(INCREMENT_LOCK, [n]) for n in (1, 2, 3, 5, 7, 8, 9)]
+] + [(INCREMENT_LOCK, [n]) for n in (1, 2, 3, 5, 7, 8, 9)] + [(PAXOS, [1]), (PAXOS, [2])]
 
 
 def ids(c):
     names = {LINEAR_EQUATION: "lineq", BINARY_CLOCK: "clock", TWO_PHASE: "2pc", INCREMENT: "inc",
-             INCREMENT_LOCK: "inclock"}
+             INCREMENT_LOCK: "inclock", PAXOS: "paxos"}
     return names[c[0]] + "-" + "-".join(map(str, c[1]))
 
 
@@ -113,7 +115,7 @@ def test_fast_paths_replay_on_cpu_model(case):
 
 @pytest.mark.parametrize("case", [(LINEAR_EQUATION, [2, 10, 14]), (BINARY_CLOCK, []), (TWO_PHASE, [3]),
                                   (INCREMENT, [4]), (INCREMENT, [10]), (INCREMENT_LOCK, [3]),
-                                  (INCREMENT_LOCK, [9])], ids=ids)
+                                  (INCREMENT_LOCK, [9]), (PAXOS, [2])], ids=ids)
 def test_fifo_visit_order_identical(case):
     # Generalises `visits_states_in_bfs_order` (src/checker/bfs.rs:351-364).
     model, params = case
@@ -213,3 +215,27 @@ def test_growth_from_small_table():
     c = sr.TwoPhaseSys(8).checker().order("fast").spawn_bfs().join()
     assert c.unique_state_count() == 6 ** 8 + 4 ** 8 + 2 ** 8
     assert c.stats()["rehashes"] >= 1
+
+
+def test_paxos_golden():
+    # examples/paxos.rs:268-290 (BFS): assert_properties, assert_discovery of the reference's
+    # "value chosen" path, unique_state_count 16_668.
+    for order in ("fifo", "fast", "auto"):
+        c = sr.Paxos(2, 3).checker().order(order).spawn_bfs().join()
+        c.assert_properties()
+        c.assert_discovery("value chosen", PAXOS_VALUE_CHOSEN_PATH)
+        assert c.unique_state_count() == 16_668
+        assert len(c.discovery("value chosen")) == len(PAXOS_VALUE_CHOSEN_PATH)
+        assert c.discovery("value chosen").into_actions()[0].startswith("Deliver { src: Id(")
+
+
+@pytest.mark.parametrize("order", ["fifo", "fast"])
+def test_paxos_3_clients_matches_oracle(order):
+    # BASELINE.json config 5 (`paxos check 3`) at full size.
+    o = oracle(PAXOS, [3])
+    c, _ = gpu(PAXOS, [3], order)
+    assert (c.unique_state_count(), c.state_count(), c.max_depth()) == (o.unique_state_count, o.state_count, o.max_depth)
+    assert (c.unique_state_count(), c.state_count(), c.max_depth()) == (1_194_428, 2_420_477, 27)
+    assert sorted(c.discoveries()) == ["value chosen"]
+    if order == "fifo":
+        assert c.discovery("value chosen").action_ids == o.discovery_actions("value chosen")

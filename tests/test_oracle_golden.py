@@ -4,8 +4,9 @@ Every expected value here is quoted from a test or doc in /root/reference (cited
 """
 import pytest
 
-from oracle_lib import (BINARY_CLOCK, DGRAPH, INCREMENT, INCREMENT_LOCK, LINEAR_EQUATION, TWO_PHASE,
+from oracle_lib import (BINARY_CLOCK, DGRAPH, INCREMENT, INCREMENT_LOCK, LINEAR_EQUATION, PAXOS, TWO_PHASE,
                         OracleRun, dgraph_params, replay)
+from paxos_golden import PAXOS_VALUE_CHOSEN_PATH
 
 INCREASE_X, INCREASE_Y = 0, 1
 
@@ -133,3 +134,36 @@ def test_eventually_fixme_misses_counterexample_when_revisiting():
 def test_2pc_7_counts():
     r = OracleRun(TWO_PHASE, [7], threads=4)
     assert r.unique_state_count == 6 ** 7 + 4 ** 7 + 2 ** 7
+
+
+def test_paxos_2_clients_golden():
+    # examples/paxos.rs:268-290 (BFS half): assert_properties, the "value chosen" example path and
+    # unique_state_count 16_668. The reference's own discovery depends on its HashSet iteration
+    # order; the golden path must be a valid discovery (assert_discovery replays it) and every BFS
+    # discovery is a shortest path of the same length.
+    r = OracleRun(PAXOS, [2])
+    assert r.unique_state_count == 16_668
+    assert r.discovery_names() == ["value chosen"]  # "linearizable" holds everywhere
+    states, holds = replay(PAXOS, [2], PAXOS_VALUE_CHOSEN_PATH, n_props=2)
+    assert holds == [1, 1]
+    assert len(r.discovery_actions("value chosen")) == len(PAXOS_VALUE_CHOSEN_PATH)
+
+
+def test_paxos_golden_path_prefix_is_no_discovery():
+    # The 7-step prefix of the golden path leaves no GetOk in flight: "value chosen" is false there.
+    _, holds = replay(PAXOS, [2], PAXOS_VALUE_CHOSEN_PATH[:-1], n_props=2)
+    assert holds == [1, 0]
+
+
+def test_paxos_multithreaded_counts_match():
+    a = OracleRun(PAXOS, [2], threads=1)
+    b = OracleRun(PAXOS, [2], threads=4)
+    assert (a.unique_state_count, a.state_count, a.max_depth) == (b.unique_state_count, b.state_count, b.max_depth)
+
+
+@pytest.mark.slow
+def test_paxos_3_clients_counts():
+    # BASELINE.json config 5 (`paxos check 3`); counts pinned by the oracle (parity for C = 3 is
+    # anchored on the C = 2 reference golden above).
+    r = OracleRun(PAXOS, [3], threads=8)
+    assert (r.unique_state_count, r.state_count, r.max_depth) == (1_194_428, 2_420_477, 27)
