@@ -37,7 +37,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--model", default="2pc", choices=["2pc", "paxos", "increment_lock"],
+                    help="workload (the BASELINE metric is 2pc; the others are side measurements)")
     ap.add_argument("--rm-count", type=int, default=9)
+    ap.add_argument("--clients", type=int, default=3, help="paxos client_count")
+    ap.add_argument("--threads", type=int, default=10, help="increment_lock thread count")
     ap.add_argument("--order", default="fast", choices=["fast", "fifo"])
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU restatement (rank 0, N=1)")
     ap.add_argument("--cpu-threads", type=int, default=16, help="host threads for the CPU baseline")
@@ -53,7 +57,13 @@ def cpu_baseline(args):
     if not os.path.exists(cli):
         subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
     threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
-    out = subprocess.run([cli, "2pc", str(args.cpu_rm_count), str(threads)], capture_output=True, text=True,
+    if args.model == "paxos":
+        cmd, what = ["paxos", str(args.clients)], f"paxos C={args.clients}"
+    elif args.model == "increment_lock":
+        cmd, what = ["increment_lock", str(min(args.threads, 9))], f"increment_lock N={min(args.threads, 9)}"
+    else:
+        cmd, what = ["2pc", str(args.cpu_rm_count)], f"2pc N={args.cpu_rm_count}"
+    out = subprocess.run([cli] + cmd + [str(threads)], capture_output=True, text=True,
                          timeout=600, check=True).stdout
     m = re.search(r"RESULT state_count=(\d+) unique=(\d+) max_depth=(\d+) threads=(\d+) sec=([\d.e+-]+)", out)
     sc, uq, _, th, sec = int(m[1]), int(m[2]), int(m[3]), int(m[4]), float(m[5])
@@ -62,7 +72,7 @@ def cpu_baseline(args):
         "unit": "unique states/s",
         "cores": th,
         "kind": "port",
-        "sample": f"full 2pc N={args.cpu_rm_count} check ({uq} unique / {sc} generated states) in {sec:.2f} s "
+        "sample": f"full {what} check ({uq} unique / {sc} generated states) in {sec:.2f} s "
                   f"on {th} host threads: C++ restatement of src/checker/bfs.rs (job market, sharded "
                   f"visited map, shared state_count atomic); the Rust reference cannot be built here",
     }
@@ -97,9 +107,23 @@ def main():
         torch.cuda.set_device(0)
     dev = torch.cuda.current_device()
 
-    from stateright_amd import TwoPhaseSys
+    import math
+
+    from stateright_amd import IncrementLock, Paxos, TwoPhaseSys
     n = args.rm_count
-    expect_unique = 6 ** n + 4 ** n + 2 ** n
+    if args.model == "paxos":
+        make = lambda: Paxos(args.clients)  # noqa: E731
+        expect_unique = {1: 265, 2: 16_668, 3: 1_194_428}[args.clients]
+        label = f"paxos C={args.clients}"
+    elif args.model == "increment_lock":
+        t = args.threads
+        make = lambda: IncrementLock(t)  # noqa: E731
+        expect_unique = 1 + 4 * sum(math.factorial(t) // math.factorial(t - k) for k in range(1, t + 1))
+        label = f"increment_lock N={t}"
+    else:
+        make = lambda: TwoPhaseSys(n)  # noqa: E731
+        expect_unique = 6 ** n + 4 ** n + 2 ** n
+        label = f"2pc N={n}"
     partitioned = world > 1 and args.mode == "partitioned"
     comm = None
     if partitioned:
@@ -107,7 +131,7 @@ def main():
         comm = Communicator.from_torch(device=dev)
 
     def step(profile=False):
-        b = TwoPhaseSys(n).checker().capacity_hint(expect_unique).device(dev)
+        b = make().checker().capacity_hint(expect_unique).device(dev)
         b = b.comm(comm) if partitioned else b.order(args.order)
         if profile:
             b = b.profile()
@@ -167,7 +191,7 @@ def main():
     if partitioned:
         alg_bytes /= world  # this rank's share of the check's algorithmic bytes
     achieved_gbps = alg_bytes / (kernel_ms * 1e-3) / 1e9 if kernel_ms else 0.0
-    traffic = pmc_traffic(n, world)
+    traffic = pmc_traffic(n, world) if args.model == "2pc" else None
     res = {
         "metric": "unique states/sec (whole node) + HBM GB/s, 2pc N=9 at 1/2/4/8 MI355X",
         "value": unique_total / elapsed,
@@ -180,12 +204,12 @@ def main():
         "scaling": "strong" if (world == 1 or partitioned) else "weak",
         "vs_baseline": None,
         "dtype": "u64",
-        "data": "synthetic: the 2pc model's own state space (no dataset)",
+        "data": f"synthetic: the {args.model} model's own state space (no dataset)",
         "config": {
-            "workload": f"2pc N={n} spawn_bfs, full check per step ({expect_unique} unique states)",
-            "model": "2pc",
-            "rm_count": n,
-            "order": "fast",
+            "workload": f"{label} spawn_bfs, full check per step ({expect_unique} unique states)",
+            "model": args.model,
+            "rm_count": n if args.model == "2pc" else None,
+            "order": args.order,
             "parallelism": (f"partitioned{world} (RCCL all-to-all per level)" if partitioned else
                             f"replicas{world}" if world > 1 else "1 GPU"),
         },
