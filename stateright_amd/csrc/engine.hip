@@ -384,6 +384,7 @@ class Engine final : public EngineBase {
         u64 cap = (u64)(1u << 20) * grow_factor_;
         if (o_.capacity_hint) while ((double)cap * table_load_ < (double)o_.capacity_hint * grow_factor_) cap <<= 1;
         ratio_ = (double)D_;
+        en_ratio_ = std::max(1.0, (double)D_ / 2.0);
         alloc_table(cap);
 
         // Init states (bfs.rs:43-66): all of them are counted and queued (duplicates too), the
@@ -551,9 +552,7 @@ class Engine final : public EngineBase {
                 const u32 ncap = (u32)std::min<u64>(arena_cap_ - nbase, 0xffffffffu);
                 u64* next = arena_.p + nbase * W;
                 u32* npar = apar_.p + nbase;
-                // Parents per wave: 64 (measured: spreading small levels over more waves with fewer
-                // parents each is slower, SR_PPW_LOG2 sweep in profiles/).
-                u32 ppw_log2 = ppw_env_ >= 0 ? (u32)ppw_env_ : 6;
+                const u32 ppw_log2 = ppw_env_ >= 0 ? (u32)ppw_env_ : ppw_for(c);
                 const u32 grid = blocks_for((c + (1u << ppw_log2) - 1) >> ppw_log2, 4);
                 timed([&] {
                     auto launch = [&](auto kern) {
@@ -575,7 +574,10 @@ class Engine final : public EngineBase {
             lo += c;
         }
         ratio_ = (double)claims / (double)limit;
-        if (!fifo_) return claims;
+        if (!fifo_) {
+            en_ratio_ = std::max(1.0, (double)lc_.enabled / (double)limit);
+            return claims;
+        }
 
         // FIFO passes 2-3: owners per parent, exclusive scan, ordered scatter.
         ensure_arena(nbase + claims, nbase);
@@ -602,6 +604,21 @@ class Engine final : public EngineBase {
         return owners;
     }
 
+    // Parents per wave (log2) of the FAST kernel for a chunk of c parents. A wave walks the
+    // enabled action slots of its parents 64 at a time. Light models (a few ALU ops per successor)
+    // amortise the wave's setup over ~16 such rounds; heavy ones (paxos: ~1.3K VALU ops per
+    // successor) want ~4 rounds per wave and more waves to hide the probe latency. Small levels
+    // use fewer parents per wave until ~1K waves are in flight (minimum 4 parents per wave).
+    // Measured per level with SR_PPW_LOG2 sweeps (profiles/r01_ppw_levels.txt).
+    u32 ppw_for(u64 c) const {
+        const double rounds = W >= 4 ? 4.0 : 16.0;
+        const double ppw = 64.0 * rounds / en_ratio_;
+        u32 l = 2;
+        while (l < 6 && (double)(2u << l) <= ppw) ++l;
+        while (l > 2 && ((c + (1u << l) - 1) >> l) < 1024) --l;
+        return l;
+    }
+
     // The frontier being expanded: the arena's second-to-last level.
     const u64* cur() const { return arena_.p + lstart_[lstart_.size() - 2] * W; }
 
@@ -616,6 +633,7 @@ class Engine final : public EngineBase {
     bool pessimistic_ = false;  // size chunks for max out-degree new states per parent
     u64 grow_factor_ = 1;       // initial-capacity multiplier after a capacity restart
     double ratio_ = 1.0;        // new states per expanded parent in the last level
+    double en_ratio_ = 8.0;     // enabled action slots per expanded parent in the last level
     double table_load_ = 0.5;
     Ctx* ctx_ = nullptr;
     hipStream_t stream_ = nullptr;

@@ -43,7 +43,8 @@ constexpr u32 NO_PARENT = 0xffffffffu;
 // pinned host memory, so the host learns the level's outcome without a copy or a stream sync.
 struct LevelCounters {
     u64 successors;        // successors within boundary (state_count increments, bfs.rs:235)
-    u64 pad0[15];
+    u64 enabled;           // enabled action slots of the expanded parents (launch-shape statistic)
+    u64 pad0[14];
     u32 claims;            // new states inserted into the visited set (= next-frontier cursor)
     u32 pad1[31];
     u32 ticket;            // workgroups finished in this launch
@@ -55,6 +56,7 @@ struct LevelCounters {
 // Host-visible snapshot (hipHostMalloc'd), written by the publishing workgroup.
 struct HostCounters {
     u64 successors;
+    u64 enabled;
     u32 claims;
     u32 err;
     u32 aux;               // launch-specific value (FIFO: number of owners from the scan)
@@ -66,6 +68,7 @@ struct HostCounters {
 template <int NP>
 __device__ __forceinline__ void reset_counters(LevelCounters* lc) {
     lc->successors = 0;
+    lc->enabled = 0;
     lc->claims = 0;
     lc->err = 0;
 #pragma unroll
@@ -88,6 +91,7 @@ __device__ __forceinline__ void publish(LevelCounters* lc, HostCounters* h, u32 
     if (t != gridDim.x - 1) return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     h->successors = __hip_atomic_load(&lc->successors, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    h->enabled = __hip_atomic_load(&lc->enabled, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     h->claims = __hip_atomic_load(&lc->claims, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     h->err = __hip_atomic_load(&lc->err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     h->aux = aux ? __hip_atomic_load(aux, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
@@ -362,22 +366,41 @@ __global__ void __launch_bounds__(256) expand_fast(M m, const u64* __restrict__ 
         }
 #pragma unroll
         for (int j = 0; j < PB; ++j) cur[j] = ok[j] ? probe_load<POL>(&t.keys[idx[j]]) : 0;
+        bool nw[PB];
 #pragma unroll
         for (int j = 0; j < PB; ++j) {
+            nw[j] = false;
             if (!ok[j]) continue;
             ++succ;
             if (cur[j] == key[j]) continue;  // the common case: an already visited state
-            bool is_new;
-            find_or_claim_from<POL>(t, key[j], idx[j], cur[j], &is_new, &lc->err);
-            if (!is_new) continue;
+            find_or_claim_from<POL>(t, key[j], idx[j], cur[j], &nw[j], &lc->err);
+        }
+        // Append the new states of this round, aggregated per wave: one LDS atomic reserves the
+        // wave's span of the stage; what does not fit goes straight to the next frontier with
+        // ONE global atomic for the wave (never one per state).
+#pragma unroll
+        for (int j = 0; j < PB; ++j) {
+            const u64 mask = __ballot(nw[j]);
+            if (!mask) continue;
+            const u32 cnt = __popcll(mask);
+            const u32 below = __popcll(mask & ((1ull << lane) - 1));
+            const int leader = __builtin_ctzll(mask);
+            u32 sb = 0;
+            if (lane == leader) sb = atomicAdd(&stage_n, cnt);
+            sb = __shfl(sb, leader, 64);
+            const u32 in_stage = sb >= (u32)STAGE ? 0u : min(cnt, (u32)STAGE - sb);
+            u32 gb = 0;
+            if (cnt > in_stage && lane == leader) gb = atomicAdd(&lc->claims, cnt - in_stage);
+            gb = __shfl(gb, leader, 64);
+            if (!nw[j]) continue;
             const u32 pr = wave0 + par[j];  // parent rank
-            u32 kk = atomicAdd(&stage_n, 1u);
-            if (kk < (u32)STAGE) {
+            if (below < in_stage) {
+                const u32 kk = sb + below;
 #pragma unroll
                 for (int x = 0; x < W; ++x) stage[kk * W + x] = ns[j][x];
                 stage_par[kk] = pr;
             } else {
-                u32 pos = atomicAdd(&lc->claims, 1u);
+                const u32 pos = gb + (below - in_stage);
                 if (pos < next_cap) {
                     store_state<W>(next, pos, ns[j]);
                     next_par[pos] = pr;
@@ -389,10 +412,12 @@ __global__ void __launch_bounds__(256) expand_fast(M m, const u64* __restrict__ 
         }
     }
     u32 total_succ = block_sum(succ, scratch);
+    u32 total_enabled = block_sum(lane == 0 ? total : 0u, scratch);
     const u32 n = min(stage_n, (u32)STAGE);
     if (threadIdx.x == 0) {
         base = n ? atomicAdd(&lc->claims, n) : 0;
         if (total_succ) atomicAdd(reinterpret_cast<unsigned long long*>(&lc->successors), (unsigned long long)total_succ);
+        if (total_enabled) atomicAdd(reinterpret_cast<unsigned long long*>(&lc->enabled), (unsigned long long)total_enabled);
     }
     __syncthreads();
     for (u32 i = threadIdx.x; i < n; i += blockDim.x) {
