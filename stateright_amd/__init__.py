@@ -9,7 +9,7 @@ property evaluation) runs as hand-written HIP kernels for gfx950 behind the C AB
 include/stateright_gpu.h; this package is the host-side mirror of the reference API.
 """
 from .checker import CheckerBuilder, CheckerError, Expectation, GpuBfsChecker, Path, StateRecorder
-from .models import BinaryClock, Increment, IncrementLock, LinearEquation, Paxos, TwoPhaseSys
+from .models import BinaryClock, DGraph, Increment, IncrementLock, LinearEquation, Paxos, TwoPhaseSys
 
 __all__ = ["CheckerBuilder", "CheckerError", "Expectation", "GpuBfsChecker", "Path", "StateRecorder",
            "BinaryClock", "Increment", "IncrementLock", "LinearEquation", "TwoPhaseSys"]

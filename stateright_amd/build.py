@@ -5,7 +5,7 @@ import subprocess
 HERE = os.path.dirname(os.path.abspath(__file__))
 SRC = os.path.join(HERE, "csrc", "engine.hip")
 DEPS = [os.path.join(HERE, "csrc", f) for f in ("engine.hip", "kernels.hpp", "kernels_dist.hpp", "dist.hpp",
-                                                "models.hpp", "device.hpp", "paxos.hpp")] + [
+                                                "models.hpp", "device.hpp", "paxos.hpp", "dgraph.hpp")] + [
     os.path.join(os.path.dirname(HERE), "include", "stateright_gpu.h")]
 OUT = os.path.join(HERE, "libstateright_gpu.so")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")

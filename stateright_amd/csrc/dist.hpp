@@ -66,6 +66,8 @@ class DistEngine final : public EngineBase {
     DistEngine(M m, const sr_opts& o, Comm* comm, int virtual_parts)
         : m_(m), o_(o), comm_(comm), D_((u32)m.max_out_degree()) {
         disc.resize(M::NPROPS);
+        if (model_emask(m))
+            throw Error(SR_ERR_UNSUPPORTED, "partitioned search: `eventually` properties need the FIFO order of one GPU");
         T_ = comm_ ? (u32)comm_->world : (u32)std::max(1, virtual_parts);
         if (T_ > (u32)MAX_PARTS) throw Error(SR_ERR_ARG, "at most 64 partitions");
         const u32 L = comm_ ? 1 : T_;

@@ -19,6 +19,7 @@
 #include "../../include/stateright_gpu.h"
 #include "device.hpp"
 #include "kernels.hpp"
+#include "dgraph.hpp"
 #include "paxos.hpp"
 
 namespace sr {
@@ -78,7 +79,8 @@ class Engine final : public EngineBase {
     static constexpr int W = M::W;
 
   public:
-    Engine(M m, const sr_opts& o) : m_(m), o_(o), A_((u32)m.max_actions()), D_((u32)m.max_out_degree()) {
+    Engine(M m, const sr_opts& o)
+        : m_(m), o_(o), A_((u32)m.max_actions()), D_((u32)m.max_out_degree()), emask_(model_emask(m)) {
         disc.resize(M::NPROPS);
         // Internal tuning knobs (not part of the ABI): successors per lane per probe round and
         // the visited-set load factor the capacity hint is sized for.
@@ -86,6 +88,7 @@ class Engine final : public EngineBase {
         if (const char* e = std::getenv("SR_TABLE_LOAD")) table_load_ = std::atof(e);
         if (const char* e = std::getenv("SR_PROBE_LOAD")) probe_load_ = std::atoi(e);
         if (const char* e = std::getenv("SR_PPW_LOG2")) ppw_env_ = std::atoi(e);
+        if (const char* e = std::getenv("SR_FILTER_LOG2")) filt_log2_ = (u32)std::atoi(e);
     }
     ~Engine() override = default;
 
@@ -101,6 +104,9 @@ class Engine final : public EngineBase {
         bind(lease.c);
         int order = o_.order;
         if (order == SR_ORDER_AUTO) order = o_.target_state_count ? SR_ORDER_FIFO : SR_ORDER_FAST;
+        // `eventually` discoveries depend on the visit order (terminal-state overwrites), so such
+        // models always run in the reference's FIFO order.
+        if (emask_) order = SR_ORDER_FIFO;
         bool order_dependent = run_with_restart(order);
         if (order_dependent && o_.order == SR_ORDER_AUTO && order == SR_ORDER_FAST) {
             // An early exit inside a level makes counts depend on the visit order: redo the
@@ -292,15 +298,18 @@ class Engine final : public EngineBase {
         if (arena_cap_ >= states) return;
         u64 cap = std::max<u64>(states, arena_cap_ * 2);
         DBuf<u64> na;
-        DBuf<u32> np;
+        DBuf<u32> np, ne;
         na.alloc(o_.device, cap * W);
         np.alloc(o_.device, cap);
+        if (emask_) ne.alloc(o_.device, cap);
         if (used) {
             SR_HIP(hipMemcpyAsync(na.p, arena_.p, used * W * sizeof(u64), hipMemcpyDeviceToDevice, stream_));
             SR_HIP(hipMemcpyAsync(np.p, apar_.p, used * sizeof(u32), hipMemcpyDeviceToDevice, stream_));
+            if (emask_) SR_HIP(hipMemcpyAsync(ne.p, aeb_.p, used * sizeof(u32), hipMemcpyDeviceToDevice, stream_));
         }
         arena_.swap(na);
         apar_.swap(np);
+        if (emask_) aeb_.swap(ne);
         arena_cap_ = cap;
         SR_HIP(hipStreamSynchronize(stream_));
     }
@@ -390,9 +399,9 @@ class Engine final : public EngineBase {
         // Init states (bfs.rs:43-66): all of them are counted and queued (duplicates too), the
         // visited set keeps distinct ones; `pending` pops from the back, so level 0 is visited in
         // REVERSE init order.
-        u64 inits[8 * W];
-        int k = m_.init_states(inits);
-        std::vector<u64> f0(inits, inits + k * W);
+        std::vector<u64> inits(256 * W);
+        int k = m_.init_states(inits.data());
+        std::vector<u64> f0(inits.begin(), inits.begin() + k * W);
         std::vector<u64> rev(k * W);
         for (int i = 0; i < k; ++i) std::copy(&f0[i * W], &f0[i * W] + W, &rev[(k - 1 - i) * W]);
         arena_cap_ = 0;
@@ -403,7 +412,8 @@ class Engine final : public EngineBase {
         SR_HIP(hipMemsetAsync(apar_.p, 0xff, (size_t)k * sizeof(u32), stream_));
         init_counters();
         insert_roots<M><<<blocks_for(k, 64), 64, 0, stream_>>>(view(), arena_.p, (u32)k, lc_d_);
-        eval_roots<M><<<blocks_for(k, 64), 64, 0, stream_>>>(m_, arena_.p, (u32)k, lc_d_, (1u << M::NPROPS) - 1);
+        eval_roots<M><<<blocks_for(k, 64), 64, 0, stream_>>>(m_, arena_.p, (u32)k, lc_d_, ((1u << M::NPROPS) - 1) & ~emask_);
+        if (emask_) fill_u32<<<blocks_for(k, 64), 64, 0, stream_>>>(aeb_.p, (u32)k, emask_);  // bfs.rs:52-60
         u32 sq = next_seq();
         publish_kernel<<<1, 64, 0, stream_>>>(lc_d_, ctx_->hc_dev, sq, 1, nullptr);
         SR_HIP(hipGetLastError());
@@ -430,19 +440,53 @@ class Engine final : public EngineBase {
                     SR_HIP(hipMemcpy(s, arena_.p + (lstart_[level] + lc_.disc[p]) * W, W * sizeof(u64), hipMemcpyDeviceToHost));
                     disc[p].fp = fingerprint<W>(s);
                 }
+            // `eventually` properties: the first terminal candidate of each undiscovered one.
+            const u32 eund = undiscovered & emask_;
+            std::vector<u32> evf(M::NPROPS, ~0u);
+            DBuf<u32> tsat, evd;
+            if (emask_ && n) {
+                tsat.alloc(o_.device, n);
+                evd.alloc(o_.device, 2 * M::NPROPS);  // [first terminal candidate | last terminal + 1]
+                SR_HIP(hipMemsetAsync(evd.p, 0xff, M::NPROPS * sizeof(u32), stream_));
+                SR_HIP(hipMemsetAsync(evd.p + M::NPROPS, 0, M::NPROPS * sizeof(u32), stream_));
+                ev_scan<M><<<blocks_for(n, 256), 256, 0, stream_>>>(m_, cur(), aeb_.p + lstart_[level], (u32)n, eund,
+                                                                    emask_, tsat.p, evd.p);
+                SR_HIP(hipGetLastError());
+                SR_HIP(hipMemcpyAsync(evf.data(), evd.p, M::NPROPS * sizeof(u32), hipMemcpyDeviceToHost, stream_));
+                SR_HIP(hipStreamSynchronize(stream_));
+            }
             u64 limit = n, visited = n;
             bool stop = false;
             if (M::NPROPS == 0) {
                 limit = 0;
                 visited = std::min<u64>(1, n);
                 stop = true;
-            } else if (newly && newly == undiscovered) {
-                // The pop of rank max_rank completes the discoveries: check_block returns without
-                // expanding it (bfs.rs:226) and the worker shuts down (bfs.rs:121-128).
-                limit = max_rank;
-                visited = (u64)max_rank + 1;
+            } else if (undiscovered == 0) {
+                // Every property was discovered at a terminal state of the previous level: the next
+                // pop finds nothing to await and returns (bfs.rs:226).
+                limit = 0;
+                visited = std::min<u64>(1, n);
                 stop = true;
                 order_dependent = true;
+            } else {
+                // The first pop at which every property is discovered: always/sometimes ones at the
+                // pop of their discovering state, eventually ones right after their terminal state.
+                const u32 pop_und = undiscovered & ~emask_;
+                bool all = (newly & pop_und) == pop_und;
+                u64 at = newly ? (u64)max_rank : 0;
+                for (u32 e = eund; e; e &= e - 1) {
+                    const int p = __builtin_ctz(e);
+                    if (evf[p] == ~0u) all = false;
+                    else at = std::max<u64>(at, (u64)evf[p] + 1);
+                }
+                if (all && at < n) {
+                    // The pop of rank `at` finds every property discovered: check_block returns
+                    // without expanding it (bfs.rs:226) and the worker shuts down (bfs.rs:121-128).
+                    limit = at;
+                    visited = at + 1;
+                    stop = true;
+                    order_dependent = true;
+                }
             }
             undiscovered &= ~newly;
 
@@ -461,12 +505,32 @@ class Engine final : public EngineBase {
 
             lvisited_.push_back(visited);
 
-            // 3. Expand ranks [0, limit).
+            // 3. Expand ranks [0, limit) (eventually: the bits passed on, terminal discoveries).
             u64 produced = 0;
+            DBuf<u32> peb;
+            std::vector<u32> evl(M::NPROPS, 0);
+            if (emask_ && limit) {
+                peb.alloc(o_.device, limit);
+                ev_resolve<<<blocks_for(limit, 256), 256, 0, stream_>>>(tsat.p, aeb_.p + lstart_[level], (u32)limit, eund,
+                                                                       evd.p, peb.p, evd.p + M::NPROPS);
+                SR_HIP(hipGetLastError());
+                SR_HIP(hipMemcpyAsync(evl.data(), evd.p + M::NPROPS, M::NPROPS * sizeof(u32), hipMemcpyDeviceToHost, stream_));
+                SR_HIP(hipStreamSynchronize(stream_));
+            }
             if (limit) {
-                produced = expand_level(level, n, limit, undiscovered);
+                produced = expand_level(level, n, limit, undiscovered & ~emask_, peb.p);
             } else {
                 std::memset(&lc_, 0, sizeof(lc_));
+            }
+            for (int p = 0; p < M::NPROPS; ++p) {
+                if (!evl[p]) continue;  // discoveries.insert at a terminal state (bfs.rs:265-272)
+                disc[p].found = true;
+                disc[p].level = level;
+                disc[p].rank = evl[p] - 1;
+                u64 s[W];
+                SR_HIP(hipMemcpy(s, arena_.p + (lstart_[level] + evl[p] - 1) * W, W * sizeof(u64), hipMemcpyDeviceToHost));
+                disc[p].fp = fingerprint<W>(s);
+                undiscovered &= ~(1u << p);
             }
             state_count += lc_.successors;
             unique += lc_.claims;
@@ -519,7 +583,7 @@ class Engine final : public EngineBase {
     }
 
     // Expands frontier ranks [0, limit) of `level` into next_; returns the next frontier size.
-    u64 expand_level(u32 level, u64 n, u64 limit, u32 undiscovered) {
+    u64 expand_level(u32 level, u64 n, u64 limit, u32 undiscovered, const u32* peb = nullptr) {
         const u32 A = A_;  // action slots (FIFO candidate layout)
         u64 claims = 0;
         DBuf<u32> cand;
@@ -556,8 +620,9 @@ class Engine final : public EngineBase {
                 const u32 grid = blocks_for((c + (1u << ppw_log2) - 1) >> ppw_log2, 4);
                 timed([&] {
                     auto launch = [&](auto kern) {
-                        kern<<<grid, 256, 0, stream_>>>(m_, cur(), ulo, uhi, view(), next, npar, ncap, lc_d_,
-                                                        undiscovered, ctx_->hc_dev, sq, last ? 1u : 0u, ppw_log2);
+                        kern<<<grid, 256, filt_log2_ ? (8u << filt_log2_) : 0u, stream_>>>(
+                            m_, cur(), ulo, uhi, view(), next, npar, ncap, lc_d_, undiscovered, ctx_->hc_dev, sq,
+                            last ? 1u : 0u, ppw_log2, filt_log2_);
                     };
                     switch (probe_batch_ * 10 + probe_load_) {
                         case 11: launch(expand_fast<M, 1, 1>); break;
@@ -596,7 +661,8 @@ class Engine final : public EngineBase {
         timed([&] {
             scatter_fifo<M><<<blocks_for(limit, 256), 256, 0, stream_>>>(m_, cur(), cand.p, offs.p, (u32)limit, A, level,
                                                                          view(), arena_.p + nbase * W, apar_.p + nbase, lc_d_,
-                                                                         undiscovered, ctx_->hc_dev, sq, total.p);
+                                                                         undiscovered, ctx_->hc_dev, sq, total.p, peb,
+                                                                         emask_ ? aeb_.p + nbase : nullptr);
         });
         wait_publish(sq);
         const u32 owners = lc_.aux;
@@ -626,10 +692,12 @@ class Engine final : public EngineBase {
     sr_opts o_;
     u32 A_;  // action slots
     u32 D_;  // max successors of one state (bounds the new states a chunk can create)
+    u32 emask_;  // the model's `eventually` properties
     bool fifo_ = false;
     int probe_batch_ = 1;
     int probe_load_ = 0;
     int ppw_env_ = -1;
+    u32 filt_log2_ = W >= 4 ? 10 : 9;  // block-local duplicate filter (SR_FILTER_LOG2 sweep in profiles/)
     bool pessimistic_ = false;  // size chunks for max out-degree new states per parent
     u64 grow_factor_ = 1;       // initial-capacity multiplier after a capacity restart
     double ratio_ = 1.0;        // new states per expanded parent in the last level
@@ -643,6 +711,7 @@ class Engine final : public EngineBase {
     DBuf<u64> keys_, meta_;      // visited set
     DBuf<u64> arena_;            // BFS tree: every level's states in visit order
     DBuf<u32> apar_;             // parent rank (in the previous level) of each arena state
+    DBuf<u32> aeb_;              // EventuallyBits of each arena state (models with eventually properties)
     u64 arena_cap_ = 0;          // states
     std::vector<u64> lstart_;    // arena offset of each level (+ one past the newest)
     std::vector<u64> lvisited_;  // states of each level that the reference would pop
@@ -686,7 +755,7 @@ static std::unique_ptr<EngineBase> make_model_engine(int model, const i64* p, in
             if (p[0] < 1 || p[0] > 3) throw Error(SR_ERR_UNSUPPORTED, "paxos: client_count must be in 1..=3");
             return std::make_unique<E<Paxos>>(Paxos::make((int)p[0], o.device), o, args...);
         case SR_MODEL_DGRAPH:
-            throw Error(SR_ERR_UNSUPPORTED, "dgraph: `eventually` properties are not supported by the GPU engine yet");
+            return std::make_unique<E<DGraph>>(DGraph::make(p, np, o.device), o, args...);
     }
     throw Error(SR_ERR_ARG, "unknown model id " + std::to_string(model));
 }

@@ -281,9 +281,11 @@ template <class M, int PB, int POL>
 __global__ void __launch_bounds__(256) expand_fast(M m, const u64* __restrict__ frontier, u32 lo, u32 hi,
                                                    TableView t, u64* __restrict__ next, u32* __restrict__ next_par,
                                                    u32 next_cap, LevelCounters* lc, u32 undiscovered,
-                                                   HostCounters* hc, u32 seq, u32 reset, u32 ppw_log2) {
+                                                   HostCounters* hc, u32 seq, u32 reset, u32 ppw_log2,
+                                                   u32 filt_log2) {
     constexpr int W = M::W, MW = M::MW;
     constexpr int STAGE = 1024 / W;
+    extern __shared__ u64 filt[];       // 2^filt_log2 fingerprints (dynamic LDS; 0 = no filter)
     __shared__ u64 stage[STAGE * W];
     __shared__ u32 stage_par[STAGE];
     __shared__ u64 pst[4][64 * W];      // parent states of each wave
@@ -320,6 +322,8 @@ __global__ void __launch_bounds__(256) expand_fast(M m, const u64* __restrict__ 
     }
     pexcl[wid][lane] = incl - cnt;
     const u32 total = __shfl(incl, 63, 64);
+    const u32 fmask = filt_log2 ? (1u << filt_log2) - 1 : 0;
+    for (u32 i = threadIdx.x; i < (fmask ? fmask + 1 : 0u); i += blockDim.x) filt[i] = 0;
     __syncthreads();
 
     u32 succ = 0;
@@ -363,6 +367,19 @@ __global__ void __launch_bounds__(256) expand_fast(M m, const u64* __restrict__ 
             }
             key[j] = ok[j] ? fingerprint<W>(ns[j]) : 0;
             idx[j] = key[j] & t.mask;
+            // Block-local duplicate filter: a direct-mapped LDS cache of the fingerprints this
+            // workgroup already sent to the visited set. Siblings' successors coincide often
+            // (commuting actions), and a hit is a duplicate of a state whose probe another lane
+            // of this block owns — counted, never probed again. A miss (or an eviction) only
+            // costs the ordinary probe, so the filter never changes which states are new.
+            if (fmask && ok[j]) {
+                const u64 old = atomicExch(reinterpret_cast<unsigned long long*>(&filt[(u32)(key[j] >> 40) & fmask]),
+                                           (unsigned long long)key[j]);
+                if (old == key[j]) {
+                    ++succ;
+                    ok[j] = false;
+                }
+            }
         }
 #pragma unroll
         for (int j = 0; j < PB; ++j) cur[j] = ok[j] ? probe_load<POL>(&t.keys[idx[j]]) : 0;
@@ -496,10 +513,12 @@ template <class M>
 __device__ __forceinline__ void scatter_fifo_body(M m, const u64* __restrict__ frontier, const u32* __restrict__ cand,
                                                   const u32* __restrict__ offs, u32 n, u32 A, u32 level,
                                                   TableView t, u64* __restrict__ next, u32* __restrict__ next_par,
-                                                  LevelCounters* lc, u32 undiscovered) {
+                                                  LevelCounters* lc, u32 undiscovered,
+                                                  const u32* __restrict__ peb = nullptr, u32* __restrict__ next_eb = nullptr) {
     u32 r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= n) return;
     const u64 lvl = (u64)(level + 1) << META_SHIFT;
+    const u32 eb = peb ? peb[r] : 0u;  // the parent's EventuallyBits after its pop (bfs.rs:263)
     u64 s[M::W];
     bool loaded = false;
     u32 j = offs[r];
@@ -514,6 +533,7 @@ __device__ __forceinline__ void scatter_fifo_body(M m, const u64* __restrict__ f
         m.apply(s, (int)a, ns);
         store_state<M::W>(next, j, ns);
         next_par[j] = r;
+        if (next_eb) next_eb[j] = eb;
         eval_props(m, ns, j, undiscovered, lc);
         ++j;
     }
@@ -524,9 +544,59 @@ __global__ void __launch_bounds__(256) scatter_fifo(M m, const u64* __restrict__
                                                     const u32* __restrict__ offs, u32 n, u32 A, u32 level,
                                                     TableView t, u64* __restrict__ next, u32* __restrict__ next_par,
                                                     LevelCounters* lc, u32 undiscovered, HostCounters* hc, u32 seq,
-                                                    const u32* owners) {
-    scatter_fifo_body(m, frontier, cand, offs, n, A, level, t, next, next_par, lc, undiscovered);
+                                                    const u32* owners, const u32* peb, u32* next_eb) {
+    scatter_fifo_body(m, frontier, cand, offs, n, A, level, t, next, next_par, lc, undiscovered, peb, next_eb);
     publish<M::NPROPS>(lc, hc, seq, true, owners);
+}
+
+// ---- `eventually` properties (src/checker/bfs.rs:52-60,212-222,265-272), FIFO order only ----
+// Each frontier state carries EventuallyBits (one bit per eventually property still unmet on its
+// BFS-tree path). At its pop a state clears the bits of undiscovered properties whose condition
+// holds; a TERMINAL state (no successor within boundary) with a bit still set is a discovery, and
+// `discoveries.insert` OVERWRITES, so the reported discovery is the last such terminal state in
+// visit order. Pass 1 finds, per undiscovered property, the first terminal candidate of the level
+// (which is where the property becomes discovered; from then on its bit is no longer cleared).
+template <class M>
+__global__ void __launch_bounds__(256) ev_scan(M m, const u64* __restrict__ frontier, const u32* __restrict__ eb_in,
+                                               u32 n, u32 eund, u32 emask, u32* __restrict__ tsat, u32* evf) {
+    const u32 r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    u64 s[M::W];
+    load_state<M::W>(frontier, r, s);
+    bool any = false;
+    for_each_successor(m, s, [&](int, const u64*) { any = true; });
+    u32 sat = 0;
+    for (u32 e = emask; e; e &= e - 1) {
+        const int p = __builtin_ctz(e);
+        if (m.discovers(p, s)) sat |= 1u << p;
+    }
+    tsat[r] = sat | (any ? 0u : 0x80000000u);
+    if (!any)
+        for (u32 c = eb_in[r] & ~sat & eund; c; c &= c - 1) atomicMin(&evf[__builtin_ctz(c)], r);
+}
+
+// Pass 2 over the expanded ranks [0, limit): the bits each state passes to its children, and per
+// property the LAST terminal state (rank + 1) whose bits still hold it.
+__global__ void __launch_bounds__(256) ev_resolve(const u32* __restrict__ tsat, const u32* __restrict__ eb_in, u32 limit,
+                                                  u32 eund, const u32* __restrict__ evf, u32* __restrict__ peb,
+                                                  u32* evl) {
+    const u32 r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= limit) return;
+    const u32 ts = tsat[r], sat = ts & 0x7fffffffu;
+    u32 clear = 0;
+    for (u32 c = sat & eund; c; c &= c - 1) {
+        const int p = __builtin_ctz(c);
+        if (r <= evf[p]) clear |= 1u << p;  // still undiscovered at this pop
+    }
+    const u32 eff = eb_in[r] & ~clear;
+    peb[r] = eff;
+    if (ts >> 31)
+        for (u32 c = eff; c; c &= c - 1) atomicMax(&evl[__builtin_ctz(c)], r + 1);
+}
+
+__global__ void fill_u32(u32* p, u32 n, u32 v) {
+    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = v;
 }
 
 

@@ -12,6 +12,8 @@
 
 #include <cstdint>
 #include <string>
+#include <type_traits>
+#include <utility>
 #include <vector>
 
 namespace sr {
@@ -25,6 +27,17 @@ using i64 = int64_t;
 #define SR_HD __host__ __device__ __forceinline__
 
 enum Expect { ALWAYS = 0, EVENTUALLY = 1, SOMETIMES = 2 };
+
+// Mask of a model's `eventually` properties (0 for models without an `emask()` member).
+template <class M, class = void>
+struct has_emask : std::false_type {};
+template <class M>
+struct has_emask<M, std::void_t<decltype(std::declval<const M&>().emask())>> : std::true_type {};
+template <class M>
+inline u32 model_emask(const M& m) {
+    if constexpr (has_emask<M>::value) return m.emask();
+    else return 0;
+}
 
 // murmur3 fmix64: a bijection on u64 with fmix64(0) == 0.
 SR_HD u64 fmix64(u64 k) {

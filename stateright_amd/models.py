@@ -116,3 +116,29 @@ class Paxos(_Model):
         else:
             f = fields[0] * 256 + ch(fields[1])
         return (((f * 16) + k) * 16 + dst) * 16 + src
+
+
+class DGraph(_Model):
+    """The reference's `DGraph` test fixture (src/test_util.rs:47-116): a directed graph over u8
+    states built from paths, with one property "odd" (s % 2 == 1) of the given expectation — the
+    model the reference checks `eventually` properties with (src/checker.rs:349-414)."""
+    MODEL_ID = N.SR_MODEL_DGRAPH
+
+    def __init__(self, expectation=N.SR_EVENTUALLY, paths=()):
+        self.expectation = int(expectation)
+        self.paths = [list(p) for p in paths]
+
+    @classmethod
+    def with_property(cls, expectation):
+        return cls(expectation)
+
+    def with_path(self, path):
+        """`DGraph::with_path`: adds path[0] to the init states and the path's edges."""
+        return DGraph(self.expectation, self.paths + [list(path)])
+
+    def params(self):
+        p = [self.expectation]
+        for path in self.paths:
+            p.append(len(path))
+            p.extend(path)
+        return p

@@ -1,0 +1,82 @@
+"""`eventually` properties on the MI355X engine (src/checker/bfs.rs:52-60,212-222,265-272) against
+the reference's own tests (src/checker.rs:349-414) and the CPU oracle on random graphs.
+
+The GPU keeps one EventuallyBits word per frontier state, finds each level's terminal states, and
+reproduces the reference's overwrite-at-terminal semantics in its FIFO order (eventually models
+always run in FIFO order).
+"""
+import random
+
+import pytest
+
+from oracle_lib import DGRAPH, OracleRun, dgraph_params
+
+pytestmark = pytest.mark.gpu
+
+sr = pytest.importorskip("stateright_amd")
+
+ALWAYS, EVENTUALLY, SOMETIMES = 0, 1, 2
+
+
+def odd(*paths, expectation=EVENTUALLY):
+    g = sr.DGraph.with_property(expectation)
+    for p in paths:
+        g = g.with_path(p)
+    return g.checker().spawn_bfs().join()
+
+
+def test_can_validate():
+    # src/checker.rs:358-376
+    odd([1], [2, 3], [2, 6, 7], [4, 9, 10]).assert_properties()
+    for p in ([1], [2, 3], [2, 6, 7], [4, 9, 10]):
+        odd(p).assert_properties()
+
+
+def test_can_discover_counterexample():
+    # src/checker.rs:378-398
+    assert odd([0, 1], [0, 2]).discovery("odd").into_states() == [(0,), (2,)]
+    assert odd([0, 1], [2, 4]).discovery("odd").into_states() == [(2,), (4,)]
+    assert odd([0, 1, 4, 6], [2, 4, 8]).discovery("odd").into_states() == [(2,), (4,), (6,)]
+
+
+def test_fixme_can_miss_counterexample_when_revisiting_a_state():
+    # src/checker.rs:400-413: known false negatives are part of the reference semantics
+    assert odd([0, 2, 4, 2]).discovery("odd") is None
+    assert odd([0, 2, 4], [1, 4, 6]).discovery("odd") is None
+
+
+def test_report_says_counterexample():
+    import io
+    w = io.StringIO()
+    g = sr.DGraph.with_property(EVENTUALLY).with_path([0, 1]).with_path([0, 2])
+    g.checker().spawn_bfs().report(w)
+    assert 'Discovered "odd" counterexample Path[1]:\n- 2\n' in w.getvalue()
+
+
+def _random_graph(rng):
+    paths = []
+    for _ in range(rng.randint(1, 6)):
+        n = rng.randint(1, 7)
+        paths.append([rng.randrange(0, 24) for _ in range(n)])
+    return paths
+
+
+@pytest.mark.parametrize("expectation", [ALWAYS, EVENTUALLY, SOMETIMES])
+def test_random_graphs_match_oracle(expectation):
+    rng = random.Random(1234 + expectation)
+    for _ in range(60):
+        paths = _random_graph(rng)
+        o = OracleRun(DGRAPH, dgraph_params(expectation, paths))
+        c = odd(*paths, expectation=expectation)
+        assert (c.unique_state_count(), c.state_count(), c.max_depth()) == (
+            o.unique_state_count, o.state_count, o.max_depth), paths
+        assert sorted(c.discoveries()) == o.discovery_names(), paths
+        assert c.is_done() == o.is_done, paths
+        if o.discovery_names():
+            assert c.discovery("odd").into_states() == o.discovery_states("odd"), paths
+
+
+def test_partitioned_rejects_eventually():
+    g = sr.DGraph.with_property(EVENTUALLY).with_path([0, 1])
+    with pytest.raises(sr.CheckerError):
+        g.checker().partitions(2).spawn_bfs().join()
