@@ -5,14 +5,18 @@
 // the protocol is tested on a single device). FAST order only (the reference's single-threaded
 // FIFO order is a single-GPU mode).
 //
-// One level, per partition p:
-//   1. expand_route: local successors are inserted directly; the others become records for their
-//      owner's send bucket.
-//   2. one all-gather of a row per partition: records per destination, frontier size, successors,
-//      local claims, error bits, discovery ranks (every rank then knows the level's global totals
-//      and the full T x T record matrix).
-//   3. all-to-all of the records (ncclSend/ncclRecv in one group; a device copy to itself).
-//   4. insert_recv: owners insert what they received; the next frontier = local + received new.
+// One level, per partition p (ONE host synchronisation per level):
+//   1. expand_route: reads its frontier size from the device control block (DistCtl); local
+//      successors are inserted directly, the others become records for their owner's send bucket
+//      (staged in LDS per chunk, one global reservation per chunk and owner). Its last workgroup
+//      writes the partition's row: records per destination, frontier size, successors, local
+//      claims, error bits, discovery ranks.
+//   2. one all-gather of the rows + a copy to pinned host memory; the host waits for it (every
+//      rank then knows the level's global totals and the full T x T record matrix).
+//   3. all-to-all of the records (ncclSend/ncclRecv in one group).
+//   4. insert_recv: owners insert what they received; its last workgroup closes the level on the
+//      device (next frontier size, discoveries among it) so that the NEXT expand_route, enqueued
+//      right behind it, needs nothing from the host.
 // Capacity planning is optimistic; an overflow on any partition is seen by every rank in the
 // next all-gather and all of them restart the check together with larger buffers.
 #pragma once
@@ -53,11 +57,14 @@ class DistEngine final : public EngineBase {
         DBuf<u64> recv;
         u64 recv_cap = 0;
         LevelCounters* lc = nullptr;
-        HostCounters* hc = nullptr;      // pinned host
+        DistCtl* ctl = nullptr;          // device: frontier size + its discoveries (next level's input)
+        HostCounters* hc = nullptr;      // pinned host (root level only)
         HostCounters* hc_dev = nullptr;
         u32 seq = 0;
         HostCounters last{};             // last published snapshot
-        u64 n = 0;                       // current frontier size
+        u64 n = 0;                       // current frontier size (exact once its row is gathered)
+        u64 n_hi = 0, n_est = 0;         // upper bound / estimate of the next frontier size
+        u64 local_prev = 0, nrec_prev = 0;
         u64 uniq = 0;                    // states claimed in this partition's visited set
         TableView view() const { return TableView{keys.p, nullptr, cap - 1}; }
     };
@@ -77,8 +84,10 @@ class DistEngine final : public EngineBase {
     ~DistEngine() override {
         for (auto& p : parts_) {
             if (p.lc) (void)hipFree(p.lc);
+            if (p.ctl) (void)hipFree(p.ctl);
             if (p.hc) (void)hipHostFree(p.hc);
         }
+        if (hrows_) (void)hipHostFree(hrows_);
         for (auto e : events_) (void)hipEventDestroy(e);
         if (stream_) (void)hipStreamDestroy(stream_);
     }
@@ -104,6 +113,7 @@ class DistEngine final : public EngineBase {
         for (auto& p : parts_) {
             if (!p.lc) {
                 SR_HIP(hipMalloc(&p.lc, sizeof(LevelCounters)));
+                SR_HIP(hipMalloc(&p.ctl, sizeof(DistCtl)));
                 SR_HIP(hipHostMalloc(&p.hc, sizeof(HostCounters), hipHostMallocCoherent | hipHostMallocMapped));
                 SR_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&p.hc_dev), p.hc, 0));
                 std::memset(p.hc, 0, sizeof(HostCounters));
@@ -168,18 +178,24 @@ class DistEngine final : public EngineBase {
     };
 
     // ---- exchange ---------------------------------------------------------------------------
-    // All-gather of one row of `words` u64 per partition; returns rows of every partition.
-    std::vector<u64> allgather_rows(const std::vector<u64>& mine, size_t words) {
-        if (!comm_) return mine;  // virtual partitions: all rows are local already
-        DBuf<u64> dsend, drecv;
-        dsend.alloc(o_.device, words);
-        drecv.alloc(o_.device, words * T_);
-        SR_HIP(hipMemcpyAsync(dsend.p, mine.data(), words * 8, hipMemcpyHostToDevice, stream_));
-        SR_NCCL(ncclAllGather(dsend.p, drecv.p, words, ncclUint64, comm_->nccl, stream_));
-        std::vector<u64> all(words * T_);
-        SR_HIP(hipMemcpyAsync(all.data(), drecv.p, words * T_ * 8, hipMemcpyDeviceToHost, stream_));
-        SR_HIP(hipStreamSynchronize(stream_));
-        return all;
+    // Waits for rows_publish and copies the gathered rows out of pinned memory.
+    void wait_rows(u32 seq, size_t words) {
+        volatile u32* flag = reinterpret_cast<volatile u32*>(hrows_ + words);
+        for (u64 spin = 1;; ++spin) {
+            if (*flag == seq) break;
+            if ((spin & 4095) == 0) {
+                hipError_t e = hipStreamQuery(stream_);
+                if (e != hipSuccess && e != hipErrorNotReady) SR_HIP(e);
+                if (e == hipSuccess && *flag != seq) {
+                    if (*flag == seq) break;
+                    throw Error(SR_ERR_HIP, "level finished without publishing its rows");
+                }
+            }
+            _mm_pause();
+        }
+        std::atomic_thread_fence(std::memory_order_acquire);
+        rows_.assign(words, 0);
+        std::memcpy(rows_.data(), (const void*)hrows_, words * 8);
     }
 
     void wait(Part& p) {
@@ -200,10 +216,10 @@ class DistEngine final : public EngineBase {
         std::memcpy(&p.last, (const void*)p.hc, sizeof(HostCounters));
     }
 
-    void ensure_arena(Part& p, u64 states) {
+    // Grows partition p's arena to hold `states`, preserving its first `used` states.
+    void ensure_arena(Part& p, u64 states, u64 used) {
         if (p.arena_cap >= states) return;
         u64 cap = std::max<u64>(states, p.arena_cap * 2);
-        u64 used = p.lstart.back() + p.last.claims;  // conservative: copy through the newest level
         used = std::min<u64>(used, p.arena_cap);
         DBuf<u64> na, np;
         na.alloc(o_.device, cap * W);
@@ -215,6 +231,7 @@ class DistEngine final : public EngineBase {
         p.arena.swap(na);
         p.apar.swap(np);
         p.arena_cap = cap;
+        arena_grows_++;
         SR_HIP(hipStreamSynchronize(stream_));
     }
 
@@ -272,7 +289,14 @@ class DistEngine final : public EngineBase {
         dinit.alloc(o_.device, k * W);
         dn.alloc(o_.device, 1);
         SR_HIP(hipMemcpyAsync(dinit.p, rev.data(), rev.size() * 8, hipMemcpyHostToDevice, stream_));
-        u64 roots = 0;
+        const size_t RW = T_ + 6 + M::NPROPS;
+        rows_all_.alloc(o_.device, RW * T_);
+        if (comm_) rows_mine_.alloc(o_.device, RW);
+        if (!hrows_) {
+            SR_HIP(hipHostMalloc(&hrows_, RW * T_ * 8 + 64, hipHostMallocCoherent | hipHostMallocMapped));
+            SR_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&hrows_dev_), hrows_, 0));
+            std::memset(hrows_, 0, RW * T_ * 8 + 64);
+        }
         for (auto& p : parts_) {
             u64 cap = (u64)(1u << 16) * grow_factor_;
             while ((double)cap * 0.5 < (double)per_part * grow_factor_) cap <<= 1;
@@ -283,8 +307,9 @@ class DistEngine final : public EngineBase {
             p.arena_cap = 0;
             p.last = HostCounters{};
             p.lstart.assign(1, 0);
-            ensure_arena(p, (per_part + per_part / 8 + 4096) * grow_factor_);
+            ensure_arena(p, (per_part + per_part / 8 + 4096) * grow_factor_, 0);
             p.sendc.alloc(o_.device, T_);
+            SR_HIP(hipMemsetAsync(p.sendc.p, 0, T_ * 4, stream_));
             init_counters(p);
             insert_roots_part<M><<<1, 64, 0, stream_>>>(p.view(), dinit.p, (u32)k, p.id, T_, p.arena.p, p.apar.p, dn.p, p.lc);
             u32 n0 = 0;
@@ -296,76 +321,99 @@ class DistEngine final : public EngineBase {
             publish_kernel<<<1, 64, 0, stream_>>>(p.lc, p.hc_dev, p.seq, 1, nullptr);
             SR_HIP(hipGetLastError());
             wait(p);
-            roots += p.last.claims;
+            // the level-0 control block: frontier = the queued roots, discoveries among them
+            DistCtl c0;
+            std::memset(&c0, 0, sizeof(c0));
+            c0.n = n0;
+            c0.roots = p.last.claims;
+            for (int pr = 0; pr < MAX_PROPS; ++pr) c0.disc_prev[pr] = pr < M::NPROPS ? p.last.disc[pr] : ~0u;
+            SR_HIP(hipMemcpyAsync(p.ctl, &c0, sizeof(c0), hipMemcpyHostToDevice, stream_));
+            SR_HIP(hipStreamSynchronize(stream_));
             p.uniq = p.last.claims;
-            p.lstart.push_back(p.n);
+            p.n_hi = n0;
+            p.n_est = n0;
         }
+        SR_HIP(hipStreamSynchronize(stream_));
         state_count = (u64)k;
-        // distinct roots: a global sum (each init state is claimed by its owner only)
-        u64 unique_total = roots;
-        glob_prev_n_ = 0;
-        for (auto& p : parts_) glob_prev_n_ += p.n;  // virtual mode: exact; RCCL: own share
-        if (comm_) glob_prev_n_ *= T_;
+        u64 unique_total = 0;
+        u64 glob_est = 0;  // estimated global frontier size of the level being expanded
+        for (auto& p : parts_) glob_est += p.n;  // virtual mode: exact; RCCL: own share
+        if (comm_) glob_est *= T_;
         u32 undiscovered = (1u << M::NPROPS) - 1;
         double ratio = (double)D_;  // non-self-loop successors per parent, last level
+        double new_frac = 1.0;      // received records that were new, last level
+        double growth = 2.0;        // global frontier growth, last level
+        u64 prev_glob_n = 0;
         auto t_loop = Clock::now();
 
+        // One host synchronisation per level: the all-gathered rows of expand_route. The exchange,
+        // insert_recv and the NEXT level's expand_route are enqueued right after it; the next
+        // expand reads its frontier size from the device (DistCtl), so the GPU never waits for
+        // the host between the insert and the next expansion.
         for (u32 level = 0;; ++level) {
-            // ---- 1. expand + route ----
+            // ---- 1. expand + route (grid sized from an upper bound of the frontier) ----
             const u64 d_eff = pessimistic_ ? D_ : std::min<u64>(D_, (u64)std::ceil(1.5 * ratio + 1.0));
             for (auto& p : parts_) {
                 // keep each visited-set partition under 75% load for this level's share of new states
-                const u64 expect_new = (u64)((double)glob_prev_n_ * (double)d_eff / (double)T_ * 1.5) + 1024;
-                while ((double)(p.uniq + expect_new) > 0.75 * (double)p.cap) grow_table(p);
-                const u64 base = p.lstart[p.lstart.size() - 2];
-                // per-destination bucket: its share of every successor, with slack
-                u64 bcap = (u64)((double)p.n * (double)d_eff / (double)T_ * 1.5) + 4096;
-                if (pessimistic_) bcap = p.n * D_ + 4096;
+                // new states of a level ~ the frontier times its growth (not its successor count:
+                // most successors are duplicates)
+                const double g = std::min((double)d_eff, std::max(1.0, growth) * 1.5);
+                const u64 expect_new = (u64)((double)glob_est * g / (double)T_) + 1024;
+                while ((double)(p.uniq + p.n_hi + expect_new) > 0.75 * (double)p.cap) grow_table(p);
+                const u64 nb = p.lstart.back();  // arena offset of the frontier being expanded
+                const u64 n_plan = pessimistic_ ? p.n_hi : std::min(p.n_hi, p.n_est * 2 + 1024);
+                u64 bcap = (u64)((double)n_plan * (double)d_eff / (double)T_ * 1.5) + 4096;
+                if (pessimistic_) bcap = p.n_hi * D_ + 4096;
                 if (p.bucket_cap < bcap) {
                     p.bucket_cap = bcap;
                     p.send.alloc(o_.device, bcap * T_ * REC);
                 }
-                ensure_arena(p, p.lstart.back() + p.n * d_eff + 4096);
-                SR_HIP(hipMemsetAsync(p.sendc.p, 0, T_ * 4, stream_));
-                const u64 nb = p.lstart.back();
-                const u32 ncap = (u32)std::min<u64>(p.arena_cap - nb, 0xffffffffu);
-                p.seq++;
+                ensure_arena(p, nb + p.n_hi + n_plan * d_eff + 4096, nb + p.n_hi);
                 if (o_.profile) SR_HIP(hipEventRecord(event(2 * stats.expand_launches), stream_));
-                expand_route<M><<<std::max<u32>(1, blocks_for(p.n, 256)), 256, 0, stream_>>>(
-                    m_, p.arena.p + base * W, (u32)p.n, p.view(), p.id, T_, p.arena.p + nb * W, p.apar.p + nb, ncap,
-                    ((u64)p.id << GID_SHIFT) + base, p.send.p, (u32)p.bucket_cap, p.sendc.p, p.lc, undiscovered,
-                    p.hc_dev, p.seq);
+                const u32 ppw_log2 = route_ppw_env_ >= 0 ? (u32)route_ppw_env_ : ppw_for(p.n_est);
+                const u32 grid = (u32)std::min<u64>(std::max<u64>(1, blocks_for(p.n_hi, 4u << ppw_log2)), 8192);
+                u64* row = comm_ ? rows_mine_.p : rows_all_.p + (u64)p.id * RW;
+                expand_route<M, 1><<<grid, 256, filt_log2_ ? (8u << filt_log2_) : 0u, stream_>>>(
+                    m_, p.arena.p, p.apar.p, nb, p.arena_cap, p.view(), p.id, T_, p.send.p, (u32)p.bucket_cap,
+                    p.sendc.p, p.lc, p.ctl, undiscovered, row, ppw_log2, filt_log2_);
                 SR_HIP(hipGetLastError());
                 if (o_.profile) SR_HIP(hipEventRecord(event(2 * stats.expand_launches + 1), stream_));
                 stats.expand_launches++;
             }
-            // ---- 2. all-gather one row per partition ----
-            const size_t RW = T_ + 6 + M::NPROPS;
-            std::vector<u64> rows;
-            for (auto& p : parts_) {
-                HostCounters before = p.last;  // the insert (or root) publish of the previous level
-                wait(p);
-                std::vector<u64> row(RW, 0);
-                for (u32 q = 0; q < T_; ++q) row[q] = p.last.sendc[q];
-                row[T_ + 0] = p.n;
-                row[T_ + 1] = p.last.successors;
-                row[T_ + 2] = p.last.claims;  // local new states
-                row[T_ + 3] = p.last.err | before.err;
-                for (int pr = 0; pr < M::NPROPS; ++pr) row[T_ + 6 + pr] = before.disc[pr];
-                rows.insert(rows.end(), row.begin(), row.end());
-            }
-            std::vector<u64> all = allgather_rows(rows, RW * parts_.size());
-            u64 glob_n = 0, glob_succ = 0, glob_err = 0;
+            // ---- 2. all-gather one row per partition; the host waits for it ----
+            if (comm_) SR_NCCL(ncclAllGather(rows_mine_.p, rows_all_.p, RW, ncclUint64, comm_->nccl, stream_));
+            const u32 rseq = ++rows_seq_;
+            u32* hseq = reinterpret_cast<u32*>(hrows_dev_ + RW * T_);
+            rows_publish<<<1, 64, 0, stream_>>>(rows_all_.p, hrows_dev_, (u32)(RW * T_), hseq, rseq);
+            SR_HIP(hipGetLastError());
+            wait_rows(rseq, RW * T_);
+            const std::vector<u64>& all = rows_;
+            u64 glob_n = 0, glob_succ = 0, glob_err = 0, glob_roots = 0;
+            u64 glob_enabled = 0;
             for (u32 q = 0; q < T_; ++q) {
                 const u64* row = &all[q * RW];
+                glob_enabled += row[T_ + 4];
                 gl_lstart_[q].push_back(gl_off_[q]);  // arena offset of this level in partition q
                 gl_off_[q] += row[T_ + 0];
                 glob_n += row[T_ + 0];
                 glob_succ += row[T_ + 1];
                 glob_err |= row[T_ + 3];
+                glob_roots += row[T_ + 5];
             }
             if (glob_err & ERR_TABLE_FULL) throw Error(SR_ERR_CAPACITY, "visited set probe limit exceeded");
             if (glob_err & ERR_FRONTIER_OVERFLOW) throw Error(SR_ERR_CAPACITY, "frontier or send bucket overflow");
+            for (auto& p : parts_) {
+                const u64* row = &all[p.id * RW];
+                if (level > 0) {
+                    // the frontier just expanded is exact now: what the last insert_recv received new
+                    const u64 recv_new = row[T_ + 0] - std::min<u64>(row[T_ + 0], p.local_prev);
+                    if (p.nrec_prev) new_frac = std::min(1.0, (double)recv_new / (double)p.nrec_prev);
+                    p.uniq += row[T_ + 0];
+                }
+                p.n = row[T_ + 0];
+                p.lstart.push_back(p.lstart.back() + p.n);  // where the next frontier starts
+            }
+            if (level == 0) unique_total = glob_roots;
             // discoveries among this level's states: the lowest (partition, rank) per property
             u32 newly = 0;
             for (int pr = 0; pr < M::NPROPS; ++pr) {
@@ -383,8 +431,23 @@ class DistEngine final : public EngineBase {
                 }
             }
             undiscovered &= ~newly;
+            if (trace_) {
+                const double us = std::chrono::duration<double, std::micro>(Clock::now() - t_trace_).count();
+                std::fprintf(stderr, "[sr-dist] level %u n=%llu succ=%llu  %.1f us since last row  grows=%llu arena=%llu\n",
+                             level, (unsigned long long)glob_n, (unsigned long long)glob_succ, us,
+                             (unsigned long long)stats.rehashes, (unsigned long long)arena_grows_);
+                t_trace_ = Clock::now();
+            }
+            if (prev_glob_n) growth = (double)glob_n / (double)prev_glob_n;
+            if (glob_n) en_ratio_ = std::max(1.0, (double)glob_enabled / (double)glob_n);
+            if (glob_n) {
+                u64 recs = 0;
+                for (u32 q = 0; q < T_; ++q)
+                    for (u32 d = 0; d < T_; ++d) recs += all[q * RW + d];
+                rec_ratio_ = (double)recs / (double)glob_n;
+            }
+            prev_glob_n = glob_n;
             if (glob_n == 0) break;  // frontier exhausted everywhere
-            glob_prev_n_ = glob_n;
             if (level > 0) unique_total += glob_n;  // every state is in exactly one frontier
             max_depth = level;
             unique = unique_total;
@@ -402,27 +465,25 @@ class DistEngine final : public EngineBase {
             // ---- 3. all-to-all of the records ----
             exchange(all, RW);
 
-            // ---- 4. owners insert what they received ----
+            // ---- 4. owners insert what they received (closes the level on the device) ----
+            glob_est = 0;
             for (auto& p : parts_) {
                 u64 nrec = 0;
                 for (u32 q = 0; q < T_; ++q) nrec += all[q * RW + p.id];
-                const u64 nb = p.lstart.back();
                 const u64 local_new = all[p.id * RW + T_ + 2];
-                ensure_arena(p, nb + local_new + nrec + 1);
+                const u64 nb = p.lstart.back();  // start of the next frontier
+                ensure_arena(p, nb + local_new + nrec + 1, nb + local_new);
                 const u32 ncap = (u32)std::min<u64>(p.arena_cap - nb, 0xffffffffu);
-                p.seq++;
                 insert_recv<M><<<std::max<u32>(1, blocks_for(nrec, 256)), 256, 0, stream_>>>(
-                    m_, p.recv.p, (u32)nrec, p.view(), p.arena.p + nb * W, p.apar.p + nb, ncap, p.lc, undiscovered,
-                    p.hc_dev, p.seq);
+                    m_, p.recv.p, (u32)nrec, p.view(), p.arena.p + nb * W, p.apar.p + nb, ncap, p.lc, undiscovered, p.ctl);
                 SR_HIP(hipGetLastError());
+                p.local_prev = local_new;
+                p.nrec_prev = nrec;
+                p.n_hi = local_new + nrec;  // exact upper bound of the next frontier
+                p.n_est = std::min<u64>(p.n_hi, local_new + (u64)std::ceil((double)nrec * std::min(1.0, 2.0 * new_frac + 0.02)));
+                glob_est += p.n_est;
             }
-            glob_prev_n_ = 0;
-            for (auto& p : parts_) {
-                wait(p);
-                p.n = p.last.claims;  // local + received new states = the next frontier
-                p.uniq += p.n;
-                p.lstart.push_back(p.lstart.back() + p.n);
-            }
+            if (comm_) glob_est *= T_;
             stats.levels++;
         }
         unique = unique_total;
@@ -539,7 +600,33 @@ class DistEngine final : public EngineBase {
     std::vector<DiscAt> disc_at_;
     std::vector<std::vector<u64>> gl_lstart_;  // per partition: arena offset of each level
     std::vector<u64> gl_off_;
-    u64 glob_prev_n_ = 0;  // global frontier size of the level being expanded
+    DBuf<u64> rows_all_, rows_mine_;  // gathered rows (T x RW) / this rank's row (RCCL mode)
+    u64* hrows_ = nullptr;            // pinned host copy of the rows (+ sequence word)
+    u64* hrows_dev_ = nullptr;
+    u32 rows_seq_ = 0;
+    double en_ratio_ = 8.0;  // enabled action slots per parent, last level
+    u32 filt_log2_ = W >= 4 ? 10 : 9;
+
+    // Parents per wave (log2) for a frontier of ~c states (the single-GPU engine's rule,
+    // Engine::ppw_for): ~16 successor rounds per wave for 1-2 word states, 4 for wider ones, and
+    // fewer parents per wave until ~1K waves are in flight.
+    u32 ppw_for(u64 c) const {
+        const double rounds = W >= 4 ? 4.0 : 16.0;
+        const double ppw = 64.0 * rounds / en_ratio_;
+        u32 l = 2;
+        while (l < 6 && (double)(2u << l) <= ppw) ++l;
+        while (l > 2 && ((c + (1u << l) - 1) >> l) < 1024) --l;
+        // a chunk (4 waves) must fit the LDS record stage: 2048 / REC records
+        const double rstage = (double)(2048 / REC);
+        while (l > 2 && 4.0 * (double)(1u << l) * rec_ratio_ * 1.3 > rstage) --l;
+        return l;
+    }
+    double rec_ratio_ = 4.0;  // remote records per parent, last level
+    int route_ppw_env_ = std::getenv("SR_ROUTE_PPW_LOG2") ? std::atoi(std::getenv("SR_ROUTE_PPW_LOG2")) : -1;
+    bool trace_ = std::getenv("SR_DIST_TRACE") != nullptr;
+    Clock::time_point t_trace_ = Clock::now();
+    u64 arena_grows_ = 0;
+    std::vector<u64> rows_;
     std::vector<hipEvent_t> events_;
 };
 

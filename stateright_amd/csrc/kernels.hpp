@@ -75,6 +75,15 @@ __device__ __forceinline__ void reset_counters(LevelCounters* lc) {
     for (int p = 0; p < NP; ++p) lc->disc[p] = ~0u;
 }
 
+// Every counter the last workgroup reads is updated with device-scope atomics (performed at the
+// coherence point, not in an XCD's L2) and read back with agent-scope atomic loads, so the ticket
+// needs only each wave's drained vmcnt before it — no agent release (an L2 writeback, ≈2-6 µs per
+// workgroup, MI355X_MICROARCH.md) and no acquire. The frontier data the workgroups write with plain
+// stores is read only by later launches (kernel boundary). SR_TICKET_FENCE=1 restores both fences.
+#ifndef SR_TICKET_FENCE
+#define SR_TICKET_FENCE 0
+#endif
+
 // Called by every workgroup after its last counter update (all threads). The workgroup that
 // arrives last copies the counters to host memory, optionally resets them for the next level,
 // and finally stores `seq` (Guideline 16: release before the ticket, acquire after it). NP = the
@@ -85,11 +94,15 @@ __device__ __forceinline__ void publish(LevelCounters* lc, HostCounters* h, u32 
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x != 0) return;
+#if SR_TICKET_FENCE
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+#endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     u32 t = atomicAdd(&lc->ticket, 1u);
     if (t != gridDim.x - 1) return;
+#if SR_TICKET_FENCE
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#endif
     h->successors = __hip_atomic_load(&lc->successors, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     h->enabled = __hip_atomic_load(&lc->enabled, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     h->claims = __hip_atomic_load(&lc->claims, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -20,162 +20,318 @@ constexpr int GID_SHIFT = 40;
 // Owner partition of a fingerprint: the high 32 bits scaled to [0, T) (any T, uniform).
 __device__ __host__ __forceinline__ u32 owner_of(u64 fp, u32 nparts) { return (u32)(((fp >> 32) * (u64)nparts) >> 32); }
 
-template <class M>
-__global__ void __launch_bounds__(256) expand_route(M m, const u64* __restrict__ frontier, u32 n, TableView t,
-                                                    u32 my_part, u32 nparts, u64* __restrict__ next,
-                                                    u64* __restrict__ next_par, u32 next_cap, u64 gid_base,
+// Device-side control block of one partition: the size of the frontier being expanded and the
+// discovery ranks among it. The last workgroup of insert_recv writes it for the next level, so the
+// host can enqueue the next expand_route before it knows the frontier size (one host
+// synchronisation per level: the all-gathered rows).
+struct DistCtl {
+    u32 n;
+    u32 roots;                   // distinct init states claimed here (level 0 only)
+    u32 pad0[30];
+    u32 disc_prev[MAX_PROPS];
+};
+
+// Row published by the last workgroup of expand_route (u64 words; RW = T + 6 + NPROPS):
+//   [0, T)  records routed to each partition      T     frontier size n
+//   T+1     successors within boundary             T+2   local claims (new states inserted here)
+//   T+3     error bits    T+4 enabled slots        T+5   distinct roots (level 0)
+//   T+6+p discovery rank of property p in the frontier
+template <int NP>
+__device__ __forceinline__ bool last_workgroup(LevelCounters* lc) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x != 0) return false;
+#if SR_TICKET_FENCE
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+#endif
+    u32 t = atomicAdd(&lc->ticket, 1u);
+    if (t != gridDim.x - 1) return false;
+#if SR_TICKET_FENCE
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#endif
+    return true;
+}
+
+// Expands the frontier of this partition (its size n is read from ctl). Same structure as
+// expand_fast (kernels.hpp): waves of ppw parents, successors load-balanced over the lanes, PB
+// successors per lane per round with their probes issued back to back, and the block-local LDS
+// duplicate filter. A successor owned by another partition becomes a record {state[W], parent
+// gid} for that owner's send bucket.
+//
+// The launch is grid-strided over chunks of 4 waves x ppw parents (sized on the host from an upper
+// bound of n, and ppw so that a chunk's records fit the LDS stages). New local states and remote
+// records are staged in LDS per chunk, then flushed by the whole block: a block-local counting
+// sort by owner and ONE global atomic per (chunk, owner) reserves each owner's span. The global
+// bucket counters are the only same-address atomics, so they must be rare: per-successor or
+// per-wave reservations serialise at the L2 when every wave of the GPU targets T addresses.
+// A stage that overflows (a chunk larger than planned) falls back to per-wave reservations.
+template <class M, int PB>
+__global__ void __launch_bounds__(256) expand_route(M m, u64* __restrict__ arena, u64* __restrict__ apar, u64 nb,
+                                                    u64 arena_cap, TableView t, u32 my_part, u32 nparts,
                                                     u64* __restrict__ send, u32 bucket_cap, u32* send_counts,
-                                                    LevelCounters* lc, u32 undiscovered, HostCounters* hc, u32 seq) {
+                                                    LevelCounters* lc, DistCtl* ctl, u32 undiscovered, u64* row,
+                                                    u32 ppw_log2, u32 filt_log2) {
     constexpr int W = M::W, MW = M::MW, REC = W + 1;
-    constexpr int STAGE = 512 / W;          // local new states staged per workgroup
-    constexpr int RSTAGE = 1536 / REC;      // remote records staged per workgroup (split per owner)
+    constexpr int STAGE = 512 / W;          // local new states staged per chunk
+    constexpr int RSTAGE = 2048 / REC;      // remote records staged per chunk (all owners)
+    extern __shared__ u64 filt[];           // 2^filt_log2 fingerprints (dynamic LDS; 0 = no filter)
     __shared__ u64 stage[STAGE * W];
     __shared__ u64 stage_par[STAGE];
     __shared__ u64 rstage[RSTAGE * REC];
-    __shared__ u32 rcount[MAX_PARTS], rbase[MAX_PARTS];
+    __shared__ u8 rown[RSTAGE];
+    __shared__ u16 rrank[RSTAGE];
+    __shared__ u32 ocnt[MAX_PARTS], obase[MAX_PARTS];
     __shared__ u64 pst[4][64 * W];
     __shared__ u64 pmask[4][64 * MW];
     __shared__ u32 pexcl[4][64];
-    __shared__ u32 stage_n, base, scratch[4];
+    __shared__ u32 stage_n, rstage_n, base, scratch[4];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const u32 seg = RSTAGE / nparts;        // LDS records per owner
-    if (threadIdx.x == 0) stage_n = 0;
-    for (u32 q = threadIdx.x; q < nparts; q += blockDim.x) rcount[q] = 0;
+    const u64 lanes_below = (1ull << lane) - 1;
+    const u64 n = ctl->n;                   // written by the previous level's insert_recv
+    const u64* frontier = arena + nb * W;
+    u64* next = arena + (nb + n) * W;
+    u64* next_par = apar + nb + n;
+    const u32 next_cap = (u32)min<u64>(arena_cap > nb + n ? arena_cap - nb - n : 0, 0xffffffffull);
+    const u64 gid_base = ((u64)my_part << GID_SHIFT) + nb;
+    const u32 ppw = 1u << ppw_log2;
+    const u32 fmask = filt_log2 ? (1u << filt_log2) - 1 : 0;
+    if (threadIdx.x == 0) stage_n = rstage_n = 0;
+    for (u32 q = threadIdx.x; q < nparts; q += blockDim.x) ocnt[q] = 0;
+    for (u32 i = threadIdx.x; i < (fmask ? fmask + 1 : 0u); i += blockDim.x) filt[i] = 0;
 
-    const u32 wave0 = (blockIdx.x * (blockDim.x >> 6) + wid) * 64;
-    const u32 r = wave0 + lane;
-    u32 cnt = 0;
-    if (r < n) {
-        u64 s[W], mk[MW];
-        load_state<W>(frontier, r, s);
-        m.enabled(s, mk);
+    u32 succ = 0, enabled = 0;
+    const u64 chunk = (u64)(blockDim.x >> 6) * ppw;
+    for (u64 c0 = (u64)blockIdx.x * chunk; c0 < n; c0 += (u64)gridDim.x * chunk) {
+        const u64 wave0 = c0 + (u64)wid * ppw;  // first parent of the wave
+        const u64 r = wave0 + lane;
+        u32 cnt = 0;
+        __syncthreads();  // the previous chunk's parents and stages are no longer read
+        if (lane < (int)ppw && r < n) {
+            u64 s[W], mk[MW];
+            load_state<W>(frontier, r, s);
+            m.enabled(s, mk);
 #pragma unroll
-        for (int i = 0; i < W; ++i) pst[wid][lane * W + i] = s[i];
+            for (int i = 0; i < W; ++i) pst[wid][lane * W + i] = s[i];
 #pragma unroll
-        for (int i = 0; i < MW; ++i) {
-            pmask[wid][lane * MW + i] = mk[i];
-            cnt += __popcll(mk[i]);
-        }
-    }
-    u32 incl = cnt;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        u32 y = __shfl_up(incl, d, 64);
-        if (lane >= d) incl += y;
-    }
-    pexcl[wid][lane] = incl - cnt;
-    const u32 total = __shfl(incl, 63, 64);
-    __syncthreads();
-
-    u32 succ = 0;
-    for (u32 it = 0; it < total; it += 64) {
-        const u32 i = it + lane;
-        if (i >= total) break;
-        u32 p = 0;
-#pragma unroll
-        for (int step = 32; step >= 1; step >>= 1)
-            if (pexcl[wid][p + step] <= i) p += step;
-        u32 k = i - pexcl[wid][p];
-        u32 a = 0;
-#pragma unroll
-        for (int w = 0; w < MW; ++w) {
-            u64 mw = pmask[wid][p * MW + w];
-            u32 c = __popcll(mw);
-            if (k < c) {
-                a = w * 64 + select_bit(mw, k);
-                break;
+            for (int i = 0; i < MW; ++i) {
+                pmask[wid][lane * MW + i] = mk[i];
+                cnt += __popcll(mk[i]);
             }
-            k -= c;
         }
-        u64 ps[W], ns[W];
+        u32 incl = cnt;
 #pragma unroll
-        for (int x = 0; x < W; ++x) ps[x] = pst[wid][p * W + x];
-        if (!m.apply(ps, (int)a, ns)) continue;
-        ++succ;
-        if (same_state<W>(ns, ps)) continue;  // self-loop
-        const u64 key = fingerprint<W>(ns);
-        const u32 owner = owner_of(key, nparts);
-        const u64 pgid = gid_base + wave0 + p;
-        if (owner == my_part) {
-            bool is_new;
-            find_or_claim(t, key, &is_new, &lc->err);
-            if (!is_new) continue;
-            u32 kk = atomicAdd(&stage_n, 1u);
-            if (kk < (u32)STAGE) {
+        for (int d = 1; d < 64; d <<= 1) {
+            u32 y = __shfl_up(incl, d, 64);
+            if (lane >= d) incl += y;
+        }
+        pexcl[wid][lane] = incl - cnt;
+        const u32 total = __shfl(incl, 63, 64);
+        if (lane == 0) enabled += total;
+        __syncthreads();
+
+        for (u32 it = 0; it < total; it += 64 * PB) {
+            u64 ns[PB][W], key[PB], idx[PB], cur[PB];
+            u32 par[PB], own[PB];
+            bool ok[PB], rem[PB];
 #pragma unroll
-                for (int x = 0; x < W; ++x) stage[kk * W + x] = ns[x];
-                stage_par[kk] = pgid;
+            for (int j = 0; j < PB; ++j) {
+                const u32 i = it + j * 64 + lane;
+                ok[j] = i < total;
+                par[j] = 0;
+                if (ok[j]) {
+                    u32 p = 0;
+#pragma unroll
+                    for (int step = 32; step >= 1; step >>= 1)
+                        if (pexcl[wid][p + step] <= i) p += step;
+                    u32 k = i - pexcl[wid][p];
+                    u32 a = 0;
+#pragma unroll
+                    for (int w = 0; w < MW; ++w) {
+                        u64 mw = pmask[wid][p * MW + w];
+                        u32 c = __popcll(mw);
+                        if (k < c) {
+                            a = w * 64 + select_bit(mw, k);
+                            break;
+                        }
+                        k -= c;
+                    }
+                    u64 ps[W];
+#pragma unroll
+                    for (int x = 0; x < W; ++x) ps[x] = pst[wid][p * W + x];
+                    ok[j] = m.apply(ps, (int)a, ns[j]);
+                    par[j] = p;
+                    if (ok[j] && same_state<W>(ns[j], ps)) {  // self-loop: counted, never routed
+                        ++succ;
+                        ok[j] = false;
+                    }
+                }
+                key[j] = ok[j] ? fingerprint<W>(ns[j]) : 0;
+                idx[j] = key[j] & t.mask;
+                if (fmask && ok[j]) {  // block-local duplicate filter (see expand_fast)
+                    const u64 old = atomicExch(reinterpret_cast<unsigned long long*>(&filt[(u32)(key[j] >> 40) & fmask]),
+                                               (unsigned long long)key[j]);
+                    if (old == key[j]) {
+                        ++succ;
+                        ok[j] = false;
+                    }
+                }
+                own[j] = ok[j] ? owner_of(key[j], nparts) : my_part;
+                rem[j] = ok[j] && own[j] != my_part;
+            }
+#pragma unroll
+            for (int j = 0; j < PB; ++j) cur[j] = (ok[j] && !rem[j]) ? probe_load<0>(&t.keys[idx[j]]) : 0;
+            bool nw[PB];
+#pragma unroll
+            for (int j = 0; j < PB; ++j) {
+                nw[j] = false;
+                if (!ok[j]) continue;
+                ++succ;
+                if (rem[j] || cur[j] == key[j]) continue;
+                find_or_claim_from<0>(t, key[j], idx[j], cur[j], &nw[j], &lc->err);
+            }
+#pragma unroll
+            for (int j = 0; j < PB; ++j) {
+                const u64 pg = gid_base + wave0 + par[j];
+                // local new states -> the chunk's stage (one LDS atomic per wave)
+                const u64 mask = __ballot(nw[j]);
+                if (mask) {
+                    const u32 cnt = __popcll(mask);
+                    const u32 below = __popcll(mask & lanes_below);
+                    const int leader = __builtin_ctzll(mask);
+                    u32 sb = 0;
+                    if (lane == leader) sb = atomicAdd(&stage_n, cnt);
+                    sb = __shfl(sb, leader, 64);
+                    const u32 in_stage = sb >= (u32)STAGE ? 0u : min(cnt, (u32)STAGE - sb);
+                    u32 gb = 0;
+                    if (cnt > in_stage && lane == leader) gb = atomicAdd(&lc->claims, cnt - in_stage);
+                    gb = __shfl(gb, leader, 64);
+                    if (nw[j]) {
+                        if (below < in_stage) {
+                            const u32 kk = sb + below;
+#pragma unroll
+                            for (int x = 0; x < W; ++x) stage[kk * W + x] = ns[j][x];
+                            stage_par[kk] = pg;
+                        } else {
+                            const u32 pos = gb + (below - in_stage);
+                            if (pos < next_cap) {
+                                store_state<W>(next, pos, ns[j]);
+                                next_par[pos] = pg;
+                            } else {
+                                atomicOr(&lc->err, (u32)ERR_FRONTIER_OVERFLOW);
+                            }
+                            eval_props(m, ns[j], pos, undiscovered, lc);
+                        }
+                    }
+                }
+                // remote records -> the chunk's record stage (one LDS atomic per wave)
+                const u64 rmask = __ballot(rem[j]);
+                if (!rmask) continue;
+                const u32 rcnt = __popcll(rmask);
+                const u32 rbelow = __popcll(rmask & lanes_below);
+                const int rleader = __builtin_ctzll(rmask);
+                u32 rsb = 0;
+                if (lane == rleader) rsb = atomicAdd(&rstage_n, rcnt);
+                rsb = __shfl(rsb, rleader, 64);
+                const u32 rin = rsb >= (u32)RSTAGE ? 0u : min(rcnt, (u32)RSTAGE - rsb);
+                if (rem[j] && rbelow < rin) {
+                    const u32 kk = rsb + rbelow;
+#pragma unroll
+                    for (int x = 0; x < W; ++x) rstage[kk * REC + x] = ns[j][x];
+                    rstage[kk * REC + W] = pg;
+                    rown[kk] = (u8)own[j];
+                }
+                // overflow (rare): per-wave reservations, owner by owner
+                u64 om = __ballot(rem[j] && rbelow >= rin);
+                while (om) {
+                    const int leader = __builtin_ctzll(om);
+                    const u32 q = __shfl(own[j], leader, 64);
+                    const bool mine = rem[j] && rbelow >= rin && own[j] == q;
+                    const u64 qm = __ballot(mine);
+                    om &= ~qm;
+                    u32 gb = 0;
+                    if (lane == leader) gb = atomicAdd(&send_counts[q], (u32)__popcll(qm));
+                    gb = __shfl(gb, leader, 64);
+                    if (mine) {
+                        const u32 pos = gb + __popcll(qm & lanes_below);
+                        if (pos < bucket_cap) {
+                            u64* rec = &send[((u64)q * bucket_cap + pos) * REC];
+#pragma unroll
+                            for (int x = 0; x < W; ++x) rec[x] = ns[j][x];
+                            rec[W] = pg;
+                        } else {
+                            atomicOr(&lc->err, (u32)ERR_FRONTIER_OVERFLOW);
+                        }
+                    }
+                }
+            }
+        }
+
+        // ---- block flush of the chunk's stages ----
+        __syncthreads();
+        const u32 nl = min(stage_n, (u32)STAGE);
+        const u32 nr = min(rstage_n, (u32)RSTAGE);
+        for (u32 i = threadIdx.x; i < nr; i += blockDim.x) rrank[i] = (u16)atomicAdd(&ocnt[rown[i]], 1u);
+        if (threadIdx.x == 0 && nl) base = atomicAdd(&lc->claims, nl);
+        __syncthreads();
+        if (threadIdx.x == 0) stage_n = rstage_n = 0;
+        for (u32 q = threadIdx.x; q < nparts; q += blockDim.x) {
+            const u32 c = ocnt[q];
+            obase[q] = c ? atomicAdd(&send_counts[q], c) : 0;
+            ocnt[q] = 0;
+        }
+        for (u32 i = threadIdx.x; i < nl; i += blockDim.x) {
+            const u32 pos = base + i;
+            u64 ns[W];
+#pragma unroll
+            for (int x = 0; x < W; ++x) ns[x] = stage[i * W + x];
+            if (pos < next_cap) {
+                store_state<W>(next, pos, ns);
+                next_par[pos] = stage_par[i];
             } else {
-                u32 pos = atomicAdd(&lc->claims, 1u);
-                if (pos < next_cap) {
-                    store_state<W>(next, pos, ns);
-                    next_par[pos] = pgid;
-                } else {
-                    atomicOr(&lc->err, (u32)ERR_FRONTIER_OVERFLOW);
-                }
-                eval_props(m, ns, pos, undiscovered, lc);
+                atomicOr(&lc->err, (u32)ERR_FRONTIER_OVERFLOW);
             }
-        } else {
-            u32 kk = atomicAdd(&rcount[owner], 1u);
-            u64* rec;
-            if (kk < seg) {
-                rec = &rstage[(owner * seg + kk) * REC];
-            } else {  // LDS segment full: append straight to the bucket
-                u32 pos = atomicAdd(&send_counts[owner], 1u);
-                if (pos >= bucket_cap) {
-                    atomicOr(&lc->err, (u32)ERR_FRONTIER_OVERFLOW);
-                    continue;
-                }
-                rec = &send[((u64)owner * bucket_cap + pos) * REC];
-            }
-#pragma unroll
-            for (int x = 0; x < W; ++x) rec[x] = ns[x];
-            rec[W] = pgid;
+            eval_props(m, ns, pos, undiscovered, lc);
         }
-    }
-    u32 total_succ = block_sum(succ, scratch);
-    const u32 nl = min(stage_n, (u32)STAGE);
-    if (threadIdx.x == 0) {
-        base = nl ? atomicAdd(&lc->claims, nl) : 0;
-        if (total_succ) atomicAdd(reinterpret_cast<unsigned long long*>(&lc->successors), (unsigned long long)total_succ);
-    }
-    for (u32 q = threadIdx.x; q < nparts; q += blockDim.x) {
-        u32 c = min(rcount[q], seg);
-        rbase[q] = c ? atomicAdd(&send_counts[q], c) : 0;
-    }
-    __syncthreads();
-    for (u32 i = threadIdx.x; i < nl; i += blockDim.x) {
-        u32 pos = base + i;
-        u64 ns[W];
-#pragma unroll
-        for (int x = 0; x < W; ++x) ns[x] = stage[i * W + x];
-        if (pos < next_cap) {
-            store_state<W>(next, pos, ns);
-            next_par[pos] = stage_par[i];
-        } else {
-            atomicOr(&lc->err, (u32)ERR_FRONTIER_OVERFLOW);
-        }
-        eval_props(m, ns, pos, undiscovered, lc);
-    }
-    // flush staged remote records, owner by owner
-    for (u32 q = 0; q < nparts; ++q) {
-        const u32 c = min(rcount[q], seg);
-        for (u32 i = threadIdx.x; i < c * REC; i += blockDim.x) {
-            const u32 rec = i / REC, x = i % REC;
-            const u32 pos = rbase[q] + rec;
-            if (pos < bucket_cap) send[((u64)q * bucket_cap + pos) * REC + x] = rstage[(q * seg + rec) * REC + x];
+        __syncthreads();
+        for (u32 i = threadIdx.x; i < nr * REC; i += blockDim.x) {
+            const u32 rr = i / REC, x = i - rr * REC;
+            const u32 q = rown[rr];
+            const u32 pos = obase[q] + rrank[rr];
+            if (pos < bucket_cap) send[((u64)q * bucket_cap + pos) * REC + x] = rstage[rr * REC + x];
             else if (x == 0) atomicOr(&lc->err, (u32)ERR_FRONTIER_OVERFLOW);
         }
     }
-    publish<M::NPROPS>(lc, hc, seq, false, nullptr, send_counts, nparts);
+    u32 total_succ = block_sum(succ, scratch);
+    u32 total_enabled = block_sum(enabled, scratch);
+    if (threadIdx.x == 0) {
+        if (total_succ) atomicAdd(reinterpret_cast<unsigned long long*>(&lc->successors), (unsigned long long)total_succ);
+        if (total_enabled) atomicAdd(reinterpret_cast<unsigned long long*>(&lc->enabled), (unsigned long long)total_enabled);
+    }
+    if (!last_workgroup<M::NPROPS>(lc)) return;
+    for (u32 q = 0; q < nparts; ++q) {
+        row[q] = __hip_atomic_load(&send_counts[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        send_counts[q] = 0;  // for the next level
+    }
+    row[nparts + 0] = n;
+    row[nparts + 1] = __hip_atomic_load(&lc->successors, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    row[nparts + 2] = __hip_atomic_load(&lc->claims, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    row[nparts + 3] = __hip_atomic_load(&lc->err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    row[nparts + 4] = __hip_atomic_load(&lc->enabled, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    row[nparts + 5] = ctl->roots;
+#pragma unroll
+    for (int p = 0; p < M::NPROPS; ++p) row[nparts + 6 + p] = ctl->disc_prev[p];
+    lc->successors = 0;
+    lc->enabled = 0;
+    lc->ticket = 0;
 }
 
 // Insert the records this partition received (state + parent gid); new states continue the next
-// frontier after the ones expand_route produced locally.
+// frontier after the ones expand_route produced locally. The last workgroup closes the level:
+// ctl = {next frontier size, discoveries among it}, counters reset for the next level.
 template <class M>
 __global__ void __launch_bounds__(256) insert_recv(M m, const u64* __restrict__ recv, u32 nrec, TableView t,
                                                    u64* __restrict__ next, u64* __restrict__ next_par, u32 next_cap,
-                                                   LevelCounters* lc, u32 undiscovered, HostCounters* hc, u32 seq) {
+                                                   LevelCounters* lc, u32 undiscovered, DistCtl* ctl) {
     constexpr int W = M::W, REC = W + 1;
     constexpr int STAGE = 1024 / W;
     __shared__ u64 stage[STAGE * W];
@@ -226,7 +382,25 @@ __global__ void __launch_bounds__(256) insert_recv(M m, const u64* __restrict__ 
         }
         eval_props(m, ns, pos, undiscovered, lc);
     }
-    publish<M::NPROPS>(lc, hc, seq, true, nullptr);
+    if (!last_workgroup<M::NPROPS>(lc)) return;
+    const u32 claims = __hip_atomic_load(&lc->claims, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    ctl->n = min(claims, next_cap);
+#pragma unroll
+    for (int p = 0; p < M::NPROPS; ++p) {
+        ctl->disc_prev[p] = __hip_atomic_load(&lc->disc[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        lc->disc[p] = ~0u;
+    }
+    ctl->roots = 0;
+    lc->claims = 0;
+    lc->ticket = 0;
+}
+
+// Copies the all-gathered rows to pinned host memory and then stores `seq` (the host spins on it).
+__global__ void rows_publish(const u64* rows, u64* host_rows, u32 words, u32* host_seq, u32 seq) {
+    for (u32 i = threadIdx.x; i < words; i += blockDim.x) host_rows[i] = rows[i];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: host memory
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(host_seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Init states owned by this partition (insert + level-0 properties), in visit order.
