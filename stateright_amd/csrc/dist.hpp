@@ -38,6 +38,48 @@ struct Comm {
     ncclComm_t nccl = nullptr;
 };
 
+// Per-device resources of the partitioned engine, pooled across checks like the single-GPU
+// engine's DeviceContext (hipHostMalloc and stream creation cost milliseconds; a 2pc N=9 check
+// takes ~3 ms): the stream, per-partition device counters / control blocks / pinned mirrors with
+// their sequence numbers, the pinned row buffer and the timing events.
+struct DistContext {
+    struct PartRes {
+        LevelCounters* lc = nullptr;
+        DistCtl* ctl = nullptr;
+        HostCounters* hc = nullptr;
+        HostCounters* hc_dev = nullptr;
+        u32 seq = 0;
+    };
+    static constexpr size_t ROW_WORDS = (size_t)MAX_PARTS * (MAX_PARTS + 6 + MAX_PROPS);
+    int dev = 0;
+    hipStream_t stream = nullptr;
+    std::vector<PartRes> parts;
+    u64* hrows = nullptr;      // [0] = sequence word, rows from word 8
+    u64* hrows_dev = nullptr;
+    u32 rows_seq = 0;
+    std::vector<hipEvent_t> events;
+
+    void init(int d) {
+        dev = d;
+        SR_HIP(hipSetDevice(d));
+        SR_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+        SR_HIP(hipHostMalloc(&hrows, (ROW_WORDS + 8) * 8, hipHostMallocCoherent | hipHostMallocMapped));
+        SR_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&hrows_dev), hrows, 0));
+        std::memset(hrows, 0, (ROW_WORDS + 8) * 8);
+    }
+    void ensure_parts(size_t L) {
+        while (parts.size() < L) {
+            PartRes r;
+            SR_HIP(hipMalloc(&r.lc, sizeof(LevelCounters)));
+            SR_HIP(hipMalloc(&r.ctl, sizeof(DistCtl)));
+            SR_HIP(hipHostMalloc(&r.hc, sizeof(HostCounters), hipHostMallocCoherent | hipHostMallocMapped));
+            SR_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&r.hc_dev), r.hc, 0));
+            std::memset(r.hc, 0, sizeof(HostCounters));
+            parts.push_back(r);
+        }
+    }
+};
+
 template <class M>
 class DistEngine final : public EngineBase {
     static constexpr int W = M::W, REC = W + 1;
@@ -82,14 +124,11 @@ class DistEngine final : public EngineBase {
         for (u32 i = 0; i < L; ++i) parts_[i].id = comm_ ? (u32)comm_->rank : i;
     }
     ~DistEngine() override {
-        for (auto& p : parts_) {
-            if (p.lc) (void)hipFree(p.lc);
-            if (p.ctl) (void)hipFree(p.ctl);
-            if (p.hc) (void)hipHostFree(p.hc);
+        if (ctx_) {
+            (void)hipStreamSynchronize(stream_);
+            for (size_t i = 0; i < parts_.size(); ++i) ctx_->parts[i].seq = parts_[i].seq;
+            ContextPool<DistContext>::get().release(ctx_);
         }
-        if (hrows_) (void)hipHostFree(hrows_);
-        for (auto e : events_) (void)hipEventDestroy(e);
-        if (stream_) (void)hipStreamDestroy(stream_);
     }
 
     int nprops() const override { return M::NPROPS; }
@@ -109,14 +148,17 @@ class DistEngine final : public EngineBase {
 
     void run() override {
         SR_HIP(hipSetDevice(o_.device));
-        if (!stream_) SR_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
-        for (auto& p : parts_) {
-            if (!p.lc) {
-                SR_HIP(hipMalloc(&p.lc, sizeof(LevelCounters)));
-                SR_HIP(hipMalloc(&p.ctl, sizeof(DistCtl)));
-                SR_HIP(hipHostMalloc(&p.hc, sizeof(HostCounters), hipHostMallocCoherent | hipHostMallocMapped));
-                SR_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&p.hc_dev), p.hc, 0));
-                std::memset(p.hc, 0, sizeof(HostCounters));
+        if (!ctx_) {
+            ctx_ = ContextPool<DistContext>::get().acquire(o_.device);
+            ctx_->ensure_parts(parts_.size());
+            stream_ = ctx_->stream;
+            for (size_t i = 0; i < parts_.size(); ++i) {
+                auto& r = ctx_->parts[i];
+                parts_[i].lc = r.lc;
+                parts_[i].ctl = r.ctl;
+                parts_[i].hc = r.hc;
+                parts_[i].hc_dev = r.hc_dev;
+                parts_[i].seq = r.seq;
             }
         }
         for (int attempt = 0;; ++attempt) {
@@ -180,7 +222,7 @@ class DistEngine final : public EngineBase {
     // ---- exchange ---------------------------------------------------------------------------
     // Waits for rows_publish and copies the gathered rows out of pinned memory.
     void wait_rows(u32 seq, size_t words) {
-        volatile u32* flag = reinterpret_cast<volatile u32*>(hrows_ + words);
+        volatile u32* flag = reinterpret_cast<volatile u32*>(ctx_->hrows);
         for (u64 spin = 1;; ++spin) {
             if (*flag == seq) break;
             if ((spin & 4095) == 0) {
@@ -195,7 +237,7 @@ class DistEngine final : public EngineBase {
         }
         std::atomic_thread_fence(std::memory_order_acquire);
         rows_.assign(words, 0);
-        std::memcpy(rows_.data(), (const void*)hrows_, words * 8);
+        std::memcpy(rows_.data(), (const void*)(ctx_->hrows + 8), words * 8);
     }
 
     void wait(Part& p) {
@@ -236,12 +278,13 @@ class DistEngine final : public EngineBase {
     }
 
     hipEvent_t event(size_t i) {
-        while (events_.size() <= i) {
+        auto& ev = ctx_->events;
+        while (ev.size() <= i) {
             hipEvent_t e;
             SR_HIP(hipEventCreate(&e));
-            events_.push_back(e);
+            ev.push_back(e);
         }
-        return events_[i];
+        return ev[i];
     }
 
     void grow_table(Part& p) {
@@ -292,11 +335,6 @@ class DistEngine final : public EngineBase {
         const size_t RW = T_ + 6 + M::NPROPS;
         rows_all_.alloc(o_.device, RW * T_);
         if (comm_) rows_mine_.alloc(o_.device, RW);
-        if (!hrows_) {
-            SR_HIP(hipHostMalloc(&hrows_, RW * T_ * 8 + 64, hipHostMallocCoherent | hipHostMallocMapped));
-            SR_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&hrows_dev_), hrows_, 0));
-            std::memset(hrows_, 0, RW * T_ * 8 + 64);
-        }
         for (auto& p : parts_) {
             u64 cap = (u64)(1u << 16) * grow_factor_;
             while ((double)cap * 0.5 < (double)per_part * grow_factor_) cap <<= 1;
@@ -382,9 +420,9 @@ class DistEngine final : public EngineBase {
             }
             // ---- 2. all-gather one row per partition; the host waits for it ----
             if (comm_) SR_NCCL(ncclAllGather(rows_mine_.p, rows_all_.p, RW, ncclUint64, comm_->nccl, stream_));
-            const u32 rseq = ++rows_seq_;
-            u32* hseq = reinterpret_cast<u32*>(hrows_dev_ + RW * T_);
-            rows_publish<<<1, 64, 0, stream_>>>(rows_all_.p, hrows_dev_, (u32)(RW * T_), hseq, rseq);
+            const u32 rseq = ++ctx_->rows_seq;
+            u32* hseq = reinterpret_cast<u32*>(ctx_->hrows_dev);
+            rows_publish<<<1, 64, 0, stream_>>>(rows_all_.p, ctx_->hrows_dev + 8, (u32)(RW * T_), hseq, rseq);
             SR_HIP(hipGetLastError());
             wait_rows(rseq, RW * T_);
             const std::vector<u64>& all = rows_;
@@ -601,9 +639,7 @@ class DistEngine final : public EngineBase {
     std::vector<std::vector<u64>> gl_lstart_;  // per partition: arena offset of each level
     std::vector<u64> gl_off_;
     DBuf<u64> rows_all_, rows_mine_;  // gathered rows (T x RW) / this rank's row (RCCL mode)
-    u64* hrows_ = nullptr;            // pinned host copy of the rows (+ sequence word)
-    u64* hrows_dev_ = nullptr;
-    u32 rows_seq_ = 0;
+    DistContext* ctx_ = nullptr;      // pooled stream, counters, pinned mirrors, events
     double en_ratio_ = 8.0;  // enabled action slots per parent, last level
     u32 filt_log2_ = W >= 4 ? 10 : 9;
 
@@ -627,7 +663,6 @@ class DistEngine final : public EngineBase {
     Clock::time_point t_trace_ = Clock::now();
     u64 arena_grows_ = 0;
     std::vector<u64> rows_;
-    std::vector<hipEvent_t> events_;
 };
 
 }  // namespace sr
