@@ -46,8 +46,9 @@ def parse():
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU restatement (rank 0, N=1)")
     ap.add_argument("--cpu-threads", type=int, default=16, help="host threads for the CPU baseline")
     ap.add_argument("--cpu-rm-count", type=int, default=8, help="2pc size of the bounded CPU sample")
-    ap.add_argument("--mode", default="partitioned", choices=["partitioned", "replicas"],
-                    help="N>1: one check partitioned over the GPUs, or one independent check per GPU")
+    ap.add_argument("--mode", default="partitioned", choices=["partitioned", "replicas", "rccl1"],
+                    help="N>1: one check partitioned over the GPUs, or one independent check per GPU; "
+                         "rccl1: the partitioned RCCL path on a one-rank communicator (N=1 rehearsal)")
     return ap.parse_args()
 
 
@@ -124,11 +125,11 @@ def main():
         make = lambda: TwoPhaseSys(n)  # noqa: E731
         expect_unique = 6 ** n + 4 ** n + 2 ** n
         label = f"2pc N={n}"
-    partitioned = world > 1 and args.mode == "partitioned"
+    partitioned = (world > 1 and args.mode == "partitioned") or args.mode == "rccl1"
     comm = None
     if partitioned:
         from stateright_amd.distributed import Communicator
-        comm = Communicator.from_torch(device=dev)
+        comm = Communicator.from_torch(device=dev) if world > 1 else Communicator(0, 1, Communicator.unique_id(), dev)
 
     def step(profile=False):
         b = make().checker().capacity_hint(expect_unique).device(dev)

@@ -128,9 +128,11 @@ struct DeviceContext {
         SR_HIP(hipSetDevice(d));
         SR_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
         SR_HIP(hipMalloc(&lc, sizeof(Counters)));
-        SR_HIP(hipHostMalloc(&hc, sizeof(HostMirror), hipHostMallocCoherent | hipHostMallocMapped));
+        // two mirrors: launch `seq` publishes to slot seq & 1, so a launch may run while the host
+        // still reads the previous one's snapshot
+        SR_HIP(hipHostMalloc(&hc, 2 * sizeof(HostMirror), hipHostMallocCoherent | hipHostMallocMapped));
         SR_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&hc_dev), hc, 0));
-        std::memset(hc, 0, sizeof(HostMirror));
+        std::memset(hc, 0, 2 * sizeof(HostMirror));
     }
     hipEvent_t event(size_t i) {
         while (events.size() <= i) {

@@ -400,13 +400,18 @@ class DistEngine final : public EngineBase {
                 while ((double)(p.uniq + p.n_hi + expect_new) > 0.75 * (double)p.cap) grow_table(p);
                 const u64 nb = p.lstart.back();  // arena offset of the frontier being expanded
                 const u64 n_plan = pessimistic_ ? p.n_hi : std::min(p.n_hi, p.n_est * 2 + 1024);
-                u64 bcap = (u64)((double)n_plan * (double)d_eff / (double)T_ * 1.5) + 4096;
+                // records per destination: last level's records per parent (measured), with slack
+                const double rpp = std::min((double)d_eff, 1.5 * rec_ratio_ + 1.0);
+                u64 bcap = (u64)((double)n_plan * rpp / (double)std::max<u32>(1, T_ - 1) * 1.5) + 4096;
                 if (pessimistic_) bcap = p.n_hi * D_ + 4096;
                 if (p.bucket_cap < bcap) {
                     p.bucket_cap = bcap;
                     p.send.alloc(o_.device, bcap * T_ * REC);
                 }
-                ensure_arena(p, nb + p.n_hi + n_plan * d_eff + 4096, nb + p.n_hi);
+                // local new states of this level: ~ the frontier times its growth (an overflow
+                // restarts the check pessimistically)
+                const double npp = pessimistic_ ? (double)d_eff : std::min((double)d_eff, std::max(4.0, 2.0 * growth));
+                ensure_arena(p, nb + p.n_hi + (u64)((double)n_plan * npp) + 4096, nb + p.n_hi);
                 if (o_.profile) SR_HIP(hipEventRecord(event(2 * stats.expand_launches), stream_));
                 const u32 ppw_log2 = route_ppw_env_ >= 0 ? (u32)route_ppw_env_ : ppw_for(p.n_est);
                 const u32 grid = (u32)std::min<u64>(std::max<u64>(1, blocks_for(p.n_hi, 4u << ppw_log2)), 8192);

@@ -89,6 +89,7 @@ class Engine final : public EngineBase {
         if (const char* e = std::getenv("SR_PROBE_LOAD")) probe_load_ = std::atoi(e);
         if (const char* e = std::getenv("SR_PPW_LOG2")) ppw_env_ = std::atoi(e);
         if (const char* e = std::getenv("SR_FILTER_LOG2")) filt_log2_ = (u32)std::atoi(e);
+        if (const char* e = std::getenv("SR_PIPELINE")) pipeline_ = std::atoi(e) != 0;
     }
     ~Engine() override = default;
 
@@ -330,12 +331,13 @@ class Engine final : public EngineBase {
         SR_HIP(hipStreamSynchronize(stream_));
     }
     u32 next_seq() { return ++ctx_->seq; }
+    HostCounters* hcd(u32 seq) const { return ctx_->hc_dev + (seq & 1); }  // device view of seq's mirror
 
     // Waits until the launch tagged `seq` has published its counters to pinned host memory: a
     // spin on one host word (no stream synchronisation, no copy), with a periodic stream query
     // so that a failed launch cannot hang the host.
     void wait_publish(u32 seq) {
-        volatile u32* flag = &ctx_->hc->seq;
+        volatile u32* flag = &ctx_->hc[seq & 1].seq;
         for (u64 spin = 1;; ++spin) {
             if (*flag == seq) break;
             if ((spin & 4095) == 0) {
@@ -349,7 +351,7 @@ class Engine final : public EngineBase {
             _mm_pause();
         }
         std::atomic_thread_fence(std::memory_order_acquire);
-        std::memcpy(&lc_, (const void*)ctx_->hc, sizeof(lc_));
+        std::memcpy(&lc_, (const void*)&ctx_->hc[seq & 1], sizeof(lc_));
         if (lc_.err & ERR_TABLE_FULL) throw Error(SR_ERR_CAPACITY, "visited set probe limit exceeded");
         if (lc_.err & ERR_FRONTIER_OVERFLOW) throw Error(SR_ERR_CAPACITY, "frontier overflow");
     }
@@ -405,7 +407,9 @@ class Engine final : public EngineBase {
         std::vector<u64> rev(k * W);
         for (int i = 0; i < k; ++i) std::copy(&f0[i * W], &f0[i * W] + W, &rev[(k - 1 - i) * W]);
         arena_cap_ = 0;
-        ensure_arena(std::max<u64>(1u << 16, (o_.capacity_hint + o_.capacity_hint / 8 + 1024) * grow_factor_), 0);
+        // hinted: room for every state plus one level's worth of planning slack (a regrowth copies
+        // the whole arena mid-run)
+        ensure_arena(std::max<u64>(1u << 16, (o_.capacity_hint + o_.capacity_hint / 2 + 1024) * grow_factor_), 0);
         lstart_.assign({0, (u64)k});
         lvisited_.clear();
         SR_HIP(hipMemcpyAsync(arena_.p, rev.data(), rev.size() * sizeof(u64), hipMemcpyHostToDevice, stream_));
@@ -415,7 +419,7 @@ class Engine final : public EngineBase {
         eval_roots<M><<<blocks_for(k, 64), 64, 0, stream_>>>(m_, arena_.p, (u32)k, lc_d_, ((1u << M::NPROPS) - 1) & ~emask_);
         if (emask_) fill_u32<<<blocks_for(k, 64), 64, 0, stream_>>>(aeb_.p, (u32)k, emask_);  // bfs.rs:52-60
         u32 sq = next_seq();
-        publish_kernel<<<1, 64, 0, stream_>>>(lc_d_, ctx_->hc_dev, sq, 1, nullptr);
+        publish_kernel<<<1, 64, 0, stream_>>>(lc_d_, hcd(sq), sq, 1, nullptr);
         SR_HIP(hipGetLastError());
         wait_publish(sq);
         state_count = (u64)k;
@@ -426,7 +430,9 @@ class Engine final : public EngineBase {
         u32 level = 0;
         bool order_dependent = false;
         auto t_loop = Clock::now();
-        for (;;) {
+        const bool pipelined = !fifo_ && !emask_ && !o_.target_state_count && M::NPROPS > 0 && pipeline_;
+        if (pipelined) order_dependent = pipeline_levels(n);
+        else for (;;) {
             // 1. Discoveries among this level's states (evaluated when they were produced).
             u32 newly = 0, max_rank = 0;
             for (int p = 0; p < M::NPROPS; ++p)
@@ -563,6 +569,136 @@ class Engine final : public EngineBase {
         return order_dependent && !fifo_;
     }
 
+    // FAST order without `eventually` properties or a target count: the expansion of level L+1 is
+    // enqueued while level L still runs (its frontier size is read on the device: the claims of the
+    // last resetting publish), so the GPU does not idle while the host digests a level. The host
+    // keeps one level in flight beyond the one it waits for. A speculative launch is skipped when
+    // the visited set or the arena might not hold it (that level is then launched after the wait,
+    // sized exactly). A speculative level launched past the end (an exhausted frontier or an early
+    // exit) is ignored. Returns whether the run stopped early inside a level.
+    bool pipeline_levels(u64 n) {
+        u32 undiscovered = (1u << M::NPROPS) - 1;
+        u32 level = 0;
+        bool order_dependent = false;
+        auto discoveries_of = [&](u32 lvl, u32& max_rank) {
+            u32 newly = 0;
+            for (int p = 0; p < M::NPROPS; ++p)
+                if ((undiscovered >> p & 1) && lc_.disc[p] != ~0u) {
+                    newly |= 1u << p;
+                    max_rank = std::max(max_rank, lc_.disc[p]);
+                    disc[p].found = true;
+                    disc[p].level = lvl;
+                    disc[p].rank = lc_.disc[p];
+                }
+            return newly;
+        };
+        u32 max_rank = 0;
+        u32 newly = discoveries_of(0, max_rank);  // among the init states (roots publish)
+        undiscovered &= ~newly;
+        if (newly && undiscovered == 0) {
+            lvisited_.push_back(max_rank + 1);
+            reference_done = true;
+            fill_discovery_fps();
+            return true;
+        }
+        u32 sq = launch_sync(n, undiscovered);
+        for (;;) {
+            // enqueue the next level before waiting for this one
+            const double g = std::max(ratio_, 1.0) * 1.5;
+            const u64 est1 = (u64)((double)n * g) + 1024;     // the next frontier
+            const u64 est2 = (u64)((double)est1 * g) + 1024;  // the states it will claim
+            const u64 nb_next = lstart_.back();
+            const bool spec = !pessimistic_ && (double)(unique + est1 + est2) < 0.8 * (double)cap_ &&
+                              nb_next + est1 + est2 <= arena_cap_;
+            // launch shape: a tight estimate (the grid strides over any excess)
+            const u64 shape = (u64)((double)n * std::max(ratio_, 0.05) * 1.1) + 64;
+            u32 sq_next = spec ? launch_expand(nb_next, 0, true, shape, undiscovered) : 0;
+
+            wait_publish(sq);  // lc_ = this level's counters
+            const u64 produced = lc_.claims;
+            state_count += lc_.successors;
+            unique += produced;
+            stats.successors += lc_.successors;
+            stats.algorithmic_bytes += n * 8 * W + lc_.successors * 8 + produced * (16 + 8 * W);
+            stats.levels++;
+            ratio_ = (double)produced / (double)n;
+            en_ratio_ = std::max(1.0, (double)lc_.enabled / (double)n);
+            lvisited_.push_back(n);
+            if (o_.verbose)
+                std::fprintf(stderr, "[sr] level %u: frontier %llu succ %llu new %llu unique %llu cap %llu%s\n", level,
+                             (unsigned long long)n, (unsigned long long)lc_.successors, (unsigned long long)produced,
+                             (unsigned long long)unique.load(), (unsigned long long)cap_, spec ? " (next enqueued)" : "");
+            if (produced == 0) {  // exhausted (a speculative launch saw an empty frontier)
+                reference_done = true;
+                break;
+            }
+            max_depth = level + 1;
+            lstart_.push_back(lstart_.back() + produced);
+            n = produced;
+            ++level;
+            max_rank = 0;
+            newly = discoveries_of(level, max_rank);
+            undiscovered &= ~newly;
+            if (newly && undiscovered == 0) {
+                // every property discovered inside this level: the reference stops at that pop
+                // (order-dependent in FAST order; AUTO re-runs FIFO). A speculative expansion of
+                // this level is not counted.
+                lvisited_.push_back(max_rank + 1);
+                reference_done = true;
+                order_dependent = true;
+                break;
+            }
+            sq = spec ? sq_next : launch_sync(n, undiscovered);
+        }
+        (void)hipStreamSynchronize(stream_);
+        fill_discovery_fps();
+        return order_dependent;
+    }
+
+    // Launch of the level whose frontier (n states) ends the arena, after the previous one is done:
+    // the visited set and the arena are grown first if the level might not fit.
+    u32 launch_sync(u64 n, u32 undiscovered) {
+        const u64 d_eff = pessimistic_ ? D_ : std::min<u64>(D_, (u64)std::ceil(2.0 * ratio_ + 1.0));
+        while ((double)(unique + n * d_eff) > 0.8 * (double)cap_) grow_table();
+        const u64 fbase = lstart_[lstart_.size() - 2];
+        ensure_arena(fbase + n + n * d_eff, fbase + n);
+        return launch_expand(fbase, (u32)n, false, n, undiscovered);
+    }
+
+    // One expand_fast launch over a whole level whose frontier starts at arena offset `fbase`:
+    // n states (dev_n = 0), or the previous level's claims read on the device (dev_n = 1, `shape`
+    // is then an estimate used only for the launch shape; the grid strides over any excess).
+    u32 launch_expand(u64 fbase, u32 n, bool dev_n, u64 shape, u32 undiscovered) {
+        const u32 sq = next_seq();
+        const u64 nbase = fbase + (dev_n ? 0 : n);  // start of the next level (dev_n: + n on the device)
+        const u32 ncap = (u32)std::min<u64>(arena_cap_ - nbase, 0xffffffffu);
+        const u32 ppw_log2 = ppw_env_ >= 0 ? (u32)ppw_env_ : ppw_for(shape);
+        const u32 grid = std::max<u32>(1, blocks_for((shape + (1u << ppw_log2) - 1) >> ppw_log2, 4));
+        timed([&] {
+            auto launch = [&](auto kern) {
+                kern<<<grid, 256, filt_log2_ ? (8u << filt_log2_) : 0u, stream_>>>(
+                    m_, arena_.p + fbase * W, 0u, n, view(), arena_.p + nbase * W, apar_.p + nbase, ncap, lc_d_,
+                    undiscovered, hcd(sq), sq, 1u, ppw_log2, filt_log2_, dev_n ? 1u : 0u);
+            };
+            switch (probe_batch_ * 10 + probe_load_) {
+                case 20: launch(expand_fast<M, 2, 0>); break;
+                default: launch(expand_fast<M, 1, 0>); break;
+            }
+        });
+        return sq;
+    }
+
+    // disc[p].fp from the discovering state in the arena (after the level loop).
+    void fill_discovery_fps() {
+        for (int p = 0; p < M::NPROPS; ++p) {
+            if (!disc[p].found) continue;
+            u64 s[W];
+            SR_HIP(hipMemcpy(s, arena_.p + (lstart_[disc[p].level] + disc[p].rank) * W, W * sizeof(u64),
+                             hipMemcpyDeviceToHost));
+            disc[p].fp = fingerprint<W>(s);
+        }
+    }
+
     // Smallest 1500-pop block boundary inside this level at which state_count >= target.
     u64 target_limit(u64 n, u64 popped_before, u64 limit) {
         DBuf<u32> counts;
@@ -610,7 +746,7 @@ class Engine final : public EngineBase {
             if (fifo_) {
                 timed([&] {
                     expand_fifo<M><<<blocks_for(c, 256), 256, 0, stream_>>>(m_, cur(), ulo, uhi, (u32)limit, view(), cand.p,
-                                                                            A, level, lc_d_, ctx_->hc_dev, sq);
+                                                                            A, level, lc_d_, hcd(sq), sq);
                 });
             } else {
                 const u32 ncap = (u32)std::min<u64>(arena_cap_ - nbase, 0xffffffffu);
@@ -621,8 +757,8 @@ class Engine final : public EngineBase {
                 timed([&] {
                     auto launch = [&](auto kern) {
                         kern<<<grid, 256, filt_log2_ ? (8u << filt_log2_) : 0u, stream_>>>(
-                            m_, cur(), ulo, uhi, view(), next, npar, ncap, lc_d_, undiscovered, ctx_->hc_dev, sq,
-                            last ? 1u : 0u, ppw_log2, filt_log2_);
+                            m_, cur(), ulo, uhi, view(), next, npar, ncap, lc_d_, undiscovered, hcd(sq), sq,
+                            last ? 1u : 0u, ppw_log2, filt_log2_, 0u);
                     };
                     switch (probe_batch_ * 10 + probe_load_) {
                         case 11: launch(expand_fast<M, 1, 1>); break;
@@ -661,7 +797,7 @@ class Engine final : public EngineBase {
         timed([&] {
             scatter_fifo<M><<<blocks_for(limit, 256), 256, 0, stream_>>>(m_, cur(), cand.p, offs.p, (u32)limit, A, level,
                                                                          view(), arena_.p + nbase * W, apar_.p + nbase, lc_d_,
-                                                                         undiscovered, ctx_->hc_dev, sq, total.p, peb,
+                                                                         undiscovered, hcd(sq), sq, total.p, peb,
                                                                          emask_ ? aeb_.p + nbase : nullptr);
         });
         wait_publish(sq);
@@ -697,6 +833,7 @@ class Engine final : public EngineBase {
     int probe_batch_ = 1;
     int probe_load_ = 0;
     int ppw_env_ = -1;
+    bool pipeline_ = true;  // FAST-order level pipelining (SR_PIPELINE=0 disables, for A/B runs)
     u32 filt_log2_ = W >= 4 ? 10 : 9;  // block-local duplicate filter (SR_FILTER_LOG2 sweep in profiles/)
     bool pessimistic_ = false;  // size chunks for max out-degree new states per parent
     u64 grow_factor_ = 1;       // initial-capacity multiplier after a capacity restart

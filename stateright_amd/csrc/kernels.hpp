@@ -51,6 +51,9 @@ struct LevelCounters {
     u32 pad2[31];
     u32 err;               // ErrBits
     u32 disc[MAX_PROPS];   // min rank of a discovering state in the frontier being produced
+    u32 pad3[32];
+    u32 prev_claims;       // claims of the last level (set by a resetting publish): the size of the
+                           // frontier a pipelined launch expands, read on the device
 };
 
 // Host-visible snapshot (hipHostMalloc'd), written by the publishing workgroup.
@@ -105,13 +108,17 @@ __device__ __forceinline__ void publish(LevelCounters* lc, HostCounters* h, u32 
 #endif
     h->successors = __hip_atomic_load(&lc->successors, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     h->enabled = __hip_atomic_load(&lc->enabled, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    h->claims = __hip_atomic_load(&lc->claims, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const u32 claims = __hip_atomic_load(&lc->claims, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    h->claims = claims;
     h->err = __hip_atomic_load(&lc->err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     h->aux = aux ? __hip_atomic_load(aux, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
 #pragma unroll
     for (int p = 0; p < NP; ++p) h->disc[p] = __hip_atomic_load(&lc->disc[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     for (u32 q = 0; q < nparts; ++q) h->sendc[q] = __hip_atomic_load(&sendc[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (reset) reset_counters<NP>(lc);
+    if (reset) {
+        lc->prev_claims = claims;
+        reset_counters<NP>(lc);
+    }
     lc->ticket = 0;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: host memory
     __hip_atomic_store(&h->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -295,7 +302,7 @@ __global__ void __launch_bounds__(256) expand_fast(M m, const u64* __restrict__ 
                                                    TableView t, u64* __restrict__ next, u32* __restrict__ next_par,
                                                    u32 next_cap, LevelCounters* lc, u32 undiscovered,
                                                    HostCounters* hc, u32 seq, u32 reset, u32 ppw_log2,
-                                                   u32 filt_log2) {
+                                                   u32 filt_log2, u32 dev_n) {
     constexpr int W = M::W, MW = M::MW;
     constexpr int STAGE = 1024 / W;
     extern __shared__ u64 filt[];       // 2^filt_log2 fingerprints (dynamic LDS; 0 = no filter)
@@ -307,142 +314,157 @@ __global__ void __launch_bounds__(256) expand_fast(M m, const u64* __restrict__ 
     __shared__ u32 stage_n, base, scratch[4];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     if (threadIdx.x == 0) stage_n = 0;
-
+    if (dev_n) {
+        // Pipelined launch (enqueued before the host saw the previous level finish): the frontier
+        // is the previous level's claims, and the next level starts right after it.
+        const u32 nn = lc->prev_claims;
+        hi = lo + nn;
+        next += (u64)nn * W;
+        next_par += nn;
+        next_cap = next_cap > nn ? next_cap - nn : 0u;
+    }
     // Each wave takes ppw = 2^ppw_log2 <= 64 parents (small levels use fewer parents per wave so
-    // that their successors spread over more waves: shorter per-lane probe chains).
+    // that their successors spread over more waves: shorter per-lane probe chains). The grid
+    // strides over chunks of 4 waves (a pipelined launch is sized from an estimate of the frontier).
     const u32 ppw = 1u << ppw_log2;
-    const u32 wave0 = lo + ((blockIdx.x * (blockDim.x >> 6) + wid) << ppw_log2);  // first parent of the wave
-    const u32 r = wave0 + lane;
-    u32 cnt = 0;
-    if (lane < ppw && r < hi) {
-        u64 s[W], mk[MW];
-        load_state<W>(frontier, r, s);
-        m.enabled(s, mk);
-#pragma unroll
-        for (int i = 0; i < W; ++i) pst[wid][lane * W + i] = s[i];
-#pragma unroll
-        for (int i = 0; i < MW; ++i) {
-            pmask[wid][lane * MW + i] = mk[i];
-            cnt += __popcll(mk[i]);
-        }
-    }
-    // wave-inclusive scan of the counts
-    u32 incl = cnt;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        u32 y = __shfl_up(incl, d, 64);
-        if (lane >= d) incl += y;
-    }
-    pexcl[wid][lane] = incl - cnt;
-    const u32 total = __shfl(incl, 63, 64);
+    const u64 chunk = (u64)(blockDim.x >> 6) << ppw_log2;
     const u32 fmask = filt_log2 ? (1u << filt_log2) - 1 : 0;
-    for (u32 i = threadIdx.x; i < (fmask ? fmask + 1 : 0u); i += blockDim.x) filt[i] = 0;
-    __syncthreads();
+    if (lo + (u64)blockIdx.x * chunk < hi)  // blocks past the frontier only take their ticket
+        for (u32 i = threadIdx.x; i < (fmask ? fmask + 1 : 0u); i += blockDim.x) filt[i] = 0;
+    u32 succ = 0, enabled = 0;
+    for (u64 c0 = lo + (u64)blockIdx.x * chunk; c0 < hi; c0 += (u64)gridDim.x * chunk) {
+        const u32 wave0 = (u32)(c0 + ((u64)wid << ppw_log2));  // first parent of the wave
+        const u32 r = wave0 + lane;
+        u32 cnt = 0;
+        __syncthreads();  // the previous chunk's parents are no longer read
+        if (lane < ppw && r < hi) {
+            u64 s[W], mk[MW];
+            load_state<W>(frontier, r, s);
+            m.enabled(s, mk);
+#pragma unroll
+            for (int i = 0; i < W; ++i) pst[wid][lane * W + i] = s[i];
+#pragma unroll
+            for (int i = 0; i < MW; ++i) {
+                pmask[wid][lane * MW + i] = mk[i];
+                cnt += __popcll(mk[i]);
+            }
+        }
+        // wave-inclusive scan of the counts
+        u32 incl = cnt;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            u32 y = __shfl_up(incl, d, 64);
+            if (lane >= d) incl += y;
+        }
+        pexcl[wid][lane] = incl - cnt;
+        const u32 total = __shfl(incl, 63, 64);
+        if (lane == 0) enabled += total;
+        __syncthreads();
 
-    u32 succ = 0;
-    for (u32 it = 0; it < total; it += 64 * PB) {
-        u64 ns[PB][W], key[PB], idx[PB], cur[PB];
-        u32 par[PB];
-        bool ok[PB];
+        for (u32 it = 0; it < total; it += 64 * PB) {
+            u64 ns[PB][W], key[PB], idx[PB], cur[PB];
+            u32 par[PB];
+            bool ok[PB];
 #pragma unroll
-        for (int j = 0; j < PB; ++j) {
-            const u32 i = it + j * 64 + lane;
-            ok[j] = i < total;
-            par[j] = 0;
-            if (ok[j]) {
-                // parent p: last lane with pexcl[p] <= i (zero-count lanes share their successor's
-                // prefix; the last of them has a non-zero count because i < its inclusive prefix)
-                u32 p = 0;
+            for (int j = 0; j < PB; ++j) {
+                const u32 i = it + j * 64 + lane;
+                ok[j] = i < total;
+                par[j] = 0;
+                if (ok[j]) {
+                    // parent p: last lane with pexcl[p] <= i (zero-count lanes share their successor's
+                    // prefix; the last of them has a non-zero count because i < its inclusive prefix)
+                    u32 p = 0;
 #pragma unroll
-                for (int step = 32; step >= 1; step >>= 1)
-                    if (pexcl[wid][p + step] <= i) p += step;
-                u32 k = i - pexcl[wid][p];
-                u32 a = 0;
+                    for (int step = 32; step >= 1; step >>= 1)
+                        if (pexcl[wid][p + step] <= i) p += step;
+                    u32 k = i - pexcl[wid][p];
+                    u32 a = 0;
 #pragma unroll
-                for (int w = 0; w < MW; ++w) {
-                    u64 mw = pmask[wid][p * MW + w];
-                    u32 c = __popcll(mw);
-                    if (k < c) {
-                        a = w * 64 + select_bit(mw, k);
-                        break;
+                    for (int w = 0; w < MW; ++w) {
+                        u64 mw = pmask[wid][p * MW + w];
+                        u32 c = __popcll(mw);
+                        if (k < c) {
+                            a = w * 64 + select_bit(mw, k);
+                            break;
+                        }
+                        k -= c;
                     }
-                    k -= c;
-                }
-                u64 ps[W];
+                    u64 ps[W];
 #pragma unroll
-                for (int x = 0; x < W; ++x) ps[x] = pst[wid][p * W + x];
-                ok[j] = m.apply(ps, (int)a, ns[j]);
-                par[j] = p;
-                if (ok[j] && same_state<W>(ns[j], ps)) {  // self-loop: counted, never probed
-                    ++succ;
-                    ok[j] = false;
+                    for (int x = 0; x < W; ++x) ps[x] = pst[wid][p * W + x];
+                    ok[j] = m.apply(ps, (int)a, ns[j]);
+                    par[j] = p;
+                    if (ok[j] && same_state<W>(ns[j], ps)) {  // self-loop: counted, never probed
+                        ++succ;
+                        ok[j] = false;
+                    }
+                }
+                key[j] = ok[j] ? fingerprint<W>(ns[j]) : 0;
+                idx[j] = key[j] & t.mask;
+                // Block-local duplicate filter: a direct-mapped LDS cache of the fingerprints this
+                // workgroup already sent to the visited set. Siblings' successors coincide often
+                // (commuting actions), and a hit is a duplicate of a state whose probe another lane
+                // of this block owns — counted, never probed again. A miss (or an eviction) only
+                // costs the ordinary probe, so the filter never changes which states are new.
+                if (fmask && ok[j]) {
+                    const u64 old = atomicExch(reinterpret_cast<unsigned long long*>(&filt[(u32)(key[j] >> 40) & fmask]),
+                                               (unsigned long long)key[j]);
+                    if (old == key[j]) {
+                        ++succ;
+                        ok[j] = false;
+                    }
                 }
             }
-            key[j] = ok[j] ? fingerprint<W>(ns[j]) : 0;
-            idx[j] = key[j] & t.mask;
-            // Block-local duplicate filter: a direct-mapped LDS cache of the fingerprints this
-            // workgroup already sent to the visited set. Siblings' successors coincide often
-            // (commuting actions), and a hit is a duplicate of a state whose probe another lane
-            // of this block owns — counted, never probed again. A miss (or an eviction) only
-            // costs the ordinary probe, so the filter never changes which states are new.
-            if (fmask && ok[j]) {
-                const u64 old = atomicExch(reinterpret_cast<unsigned long long*>(&filt[(u32)(key[j] >> 40) & fmask]),
-                                           (unsigned long long)key[j]);
-                if (old == key[j]) {
-                    ++succ;
-                    ok[j] = false;
-                }
+#pragma unroll
+            for (int j = 0; j < PB; ++j) cur[j] = ok[j] ? probe_load<POL>(&t.keys[idx[j]]) : 0;
+            bool nw[PB];
+#pragma unroll
+            for (int j = 0; j < PB; ++j) {
+                nw[j] = false;
+                if (!ok[j]) continue;
+                ++succ;
+                if (cur[j] == key[j]) continue;  // the common case: an already visited state
+                find_or_claim_from<POL>(t, key[j], idx[j], cur[j], &nw[j], &lc->err);
             }
-        }
+            // Append the new states of this round, aggregated per wave: one LDS atomic reserves the
+            // wave's span of the stage; what does not fit goes straight to the next frontier with
+            // ONE global atomic for the wave (never one per state).
 #pragma unroll
-        for (int j = 0; j < PB; ++j) cur[j] = ok[j] ? probe_load<POL>(&t.keys[idx[j]]) : 0;
-        bool nw[PB];
+            for (int j = 0; j < PB; ++j) {
+                const u64 mask = __ballot(nw[j]);
+                if (!mask) continue;
+                const u32 cnt = __popcll(mask);
+                const u32 below = __popcll(mask & ((1ull << lane) - 1));
+                const int leader = __builtin_ctzll(mask);
+                u32 sb = 0;
+                if (lane == leader) sb = atomicAdd(&stage_n, cnt);
+                sb = __shfl(sb, leader, 64);
+                const u32 in_stage = sb >= (u32)STAGE ? 0u : min(cnt, (u32)STAGE - sb);
+                u32 gb = 0;
+                if (cnt > in_stage && lane == leader) gb = atomicAdd(&lc->claims, cnt - in_stage);
+                gb = __shfl(gb, leader, 64);
+                if (!nw[j]) continue;
+                const u32 pr = wave0 + par[j];  // parent rank
+                if (below < in_stage) {
+                    const u32 kk = sb + below;
 #pragma unroll
-        for (int j = 0; j < PB; ++j) {
-            nw[j] = false;
-            if (!ok[j]) continue;
-            ++succ;
-            if (cur[j] == key[j]) continue;  // the common case: an already visited state
-            find_or_claim_from<POL>(t, key[j], idx[j], cur[j], &nw[j], &lc->err);
-        }
-        // Append the new states of this round, aggregated per wave: one LDS atomic reserves the
-        // wave's span of the stage; what does not fit goes straight to the next frontier with
-        // ONE global atomic for the wave (never one per state).
-#pragma unroll
-        for (int j = 0; j < PB; ++j) {
-            const u64 mask = __ballot(nw[j]);
-            if (!mask) continue;
-            const u32 cnt = __popcll(mask);
-            const u32 below = __popcll(mask & ((1ull << lane) - 1));
-            const int leader = __builtin_ctzll(mask);
-            u32 sb = 0;
-            if (lane == leader) sb = atomicAdd(&stage_n, cnt);
-            sb = __shfl(sb, leader, 64);
-            const u32 in_stage = sb >= (u32)STAGE ? 0u : min(cnt, (u32)STAGE - sb);
-            u32 gb = 0;
-            if (cnt > in_stage && lane == leader) gb = atomicAdd(&lc->claims, cnt - in_stage);
-            gb = __shfl(gb, leader, 64);
-            if (!nw[j]) continue;
-            const u32 pr = wave0 + par[j];  // parent rank
-            if (below < in_stage) {
-                const u32 kk = sb + below;
-#pragma unroll
-                for (int x = 0; x < W; ++x) stage[kk * W + x] = ns[j][x];
-                stage_par[kk] = pr;
-            } else {
-                const u32 pos = gb + (below - in_stage);
-                if (pos < next_cap) {
-                    store_state<W>(next, pos, ns[j]);
-                    next_par[pos] = pr;
+                    for (int x = 0; x < W; ++x) stage[kk * W + x] = ns[j][x];
+                    stage_par[kk] = pr;
                 } else {
-                    atomicOr(&lc->err, (u32)ERR_FRONTIER_OVERFLOW);
+                    const u32 pos = gb + (below - in_stage);
+                    if (pos < next_cap) {
+                        store_state<W>(next, pos, ns[j]);
+                        next_par[pos] = pr;
+                    } else {
+                        atomicOr(&lc->err, (u32)ERR_FRONTIER_OVERFLOW);
+                    }
+                    eval_props(m, ns[j], pos, undiscovered, lc);
                 }
-                eval_props(m, ns[j], pos, undiscovered, lc);
             }
         }
     }
     u32 total_succ = block_sum(succ, scratch);
-    u32 total_enabled = block_sum(lane == 0 ? total : 0u, scratch);
+    u32 total_enabled = block_sum(enabled, scratch);
     const u32 n = min(stage_n, (u32)STAGE);
     if (threadIdx.x == 0) {
         base = n ? atomicAdd(&lc->claims, n) : 0;
