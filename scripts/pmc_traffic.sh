@@ -32,5 +32,6 @@ res = {"rm_count": 9, "n_gpus": 1, "kernel": "expand_fast<TwoPhase>", "launches"
        "note": "beyond-L2 (Infinity Cache + HBM) bytes from TCC_EA0_RDREQ_{128B,64B,32B} and WRITE_SIZE, "
                "averaged over every expand_fast dispatch of `bench.py --steps 2 --warmup 1` (3 full checks)"}
 json.dump(res, open("profiles/pmc_traffic.json", "w"), indent=1)
+json.dump(res, open("gpurun_out/pmc_traffic/pmc_traffic.json", "w"), indent=1)  # gpurun merges this one back
 print(json.dumps(res))
 PY
