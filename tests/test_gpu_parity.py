@@ -184,8 +184,10 @@ def test_target_state_count_matches_oracle(case, target):
     assert c.is_done() == o.is_done
 
 
-@pytest.mark.parametrize("n", [8, 9, 10])
+@pytest.mark.parametrize("n", [8, 9, 10, 11, 12])
 def test_2pc_large_closed_form(n):
+    # n = 11 is BASELINE.json configs[3] (367 M states); n = 12 (2.2 G states, a 64 GB visited set
+    # and a 26 GB arena) is the largest size one MI355X holds with this layout.
     # Full sizes: BASELINE.md §3 (closed forms anchored at the reference goldens 288 / 8 832).
     c = sr.TwoPhaseSys(n).checker().capacity_hint(6 ** n + 4 ** n + 2 ** n).spawn_bfs().join()
     assert c.unique_state_count() == 6 ** n + 4 ** n + 2 ** n
@@ -195,13 +197,22 @@ def test_2pc_large_closed_form(n):
     c.assert_properties()
 
 
-@pytest.mark.parametrize("n", [9, 10])
+@pytest.mark.parametrize("n", [9, 10, 11])
 def test_increment_lock_large_closed_form(n):
     c = sr.IncrementLock(n).checker().spawn_bfs().join()
     expect = 1 + 4 * sum(math.factorial(n) // math.factorial(n - k) for k in range(1, n + 1))
     assert c.unique_state_count() == c.state_count() == expect
     assert c.max_depth() == 4 * n
     assert c.discoveries() == {}
+
+
+def test_2pc_10_fifo_matches_fast():
+    # The exact-order pipeline at a BASELINE size: same counts as FAST, same closed forms.
+    n = 10
+    a = sr.TwoPhaseSys(n).checker().order("fifo").capacity_hint(6 ** n + 4 ** n + 2 ** n).spawn_bfs().join()
+    assert a.unique_state_count() == 6 ** n + 4 ** n + 2 ** n
+    assert 3 * a.state_count() == 4 * n * 6 ** n + 3 * (n + 1) * 4 ** n + 3 * n * 2 ** n + 6
+    assert a.max_depth() == 3 * n + 1
 
 
 def test_2pc_8_fifo_matches_fast():
