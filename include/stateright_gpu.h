@@ -20,6 +20,8 @@
  *   sr_gpu_bfs_replay             <- Path::from_actions (assert_discovery) src/checker/path.rs:90-112,
  *                                                                     src/checker.rs:292-337
  *   sr_gpu_bfs_visits             <- StateRecorder visitor            src/checker/visitor.rs:70-99
+ *   sr_gpu_bfs_visit_tree         <- PathRecorder / Fn(Path) visitors src/checker/visitor.rs:19-66,
+ *                                                                     src/checker/bfs.rs:187-189
  *   sr_gpu_bfs_free               <- Drop of the checker (join(self) consumes it in Rust)
  *   sr_last_error                 <- the reference panics; see "Errors" below
  *   sr_dist_* / sr_gpu_bfs_spawn_partitioned <- new: the visited set partitioned over GPUs
@@ -147,6 +149,12 @@ int32_t sr_gpu_bfs_replay(const sr_bfs* bfs, int32_t init_index, const int64_t* 
                           int64_t* states, int64_t cap_states, int32_t* conditions, int32_t cap_conditions);
 /* Visited states in visit order (record_visits=1), describe_width int64s each; returns count*width. */
 int64_t sr_gpu_bfs_visits(const sr_bfs* bfs, int64_t* out, int64_t cap);
+/* The visitor's paths (`CheckerVisitor::visit` gets `Path::from_fingerprints` of every popped
+ * state, src/checker/bfs.rs:187-189, src/checker/visitor.rs:19-66): per visit, in the order of
+ * sr_gpu_bfs_visits, the visit index of its BFS-tree parent and the canonical id of the first
+ * action leading from that parent to it (-1 and -1 for init states). Returns the visit count,
+ * or SR_ERR_UNSUPPORTED for the partitioned search. */
+int64_t sr_gpu_bfs_visit_tree(const sr_bfs* bfs, int64_t* parent, int64_t* action, int64_t cap);
 void sr_gpu_bfs_free(sr_bfs* bfs);
 
 /* ---- Partitioned search over several GPUs (no counterpart in the reference,

@@ -3,6 +3,7 @@
 
 #include "models.hpp"
 #include "paxos.hpp"
+#include "dfs.hpp"
 
 using namespace oracle;
 
@@ -11,7 +12,7 @@ namespace {
 thread_local std::string g_last_error;
 
 // Model ids are shared with include/stateright_gpu.h (SR_MODEL_*).
-enum ModelId { LINEAR_EQUATION = 1, BINARY_CLOCK = 2, TWO_PHASE = 3, INCREMENT = 4, INCREMENT_LOCK = 5, DGRAPH = 6, PAXOS = 7 };
+enum ModelId { LINEAR_EQUATION = 1, BINARY_CLOCK = 2, TWO_PHASE = 3, INCREMENT = 4, INCREMENT_LOCK = 5, DGRAPH = 6, PAXOS = 7, SYM_TOY = 8 };
 
 struct HandleBase {
     virtual ~HandleBase() = default;
@@ -25,6 +26,8 @@ struct HandleBase {
     virtual std::optional<std::vector<i64>> discovery_actions(const std::string& n) const = 0;
     virtual std::optional<std::vector<i64>> discovery_states(const std::string& n) const = 0;
     virtual std::vector<i64> visits() const = 0;
+    // The path a visitor receives for visit i (`Path::from_fingerprints(reconstruct_path(fp))`).
+    virtual std::optional<std::vector<i64>> visit_path(i64 i) const = 0;
     virtual int width() const = 0;
     virtual std::string report() const = 0;
 };
@@ -40,6 +43,11 @@ struct Handle : HandleBase {
     bool is_done() const override { return c.is_done(); }
     double elapsed() const override { return c.elapsed_sec(); }
     std::vector<std::string> discovery_names() const override { return c.discovery_names(); }
+    std::optional<std::vector<i64>> visit_path(i64 i) const override {
+        const auto& f = c.visit_fps();
+        if (i < 0 || i >= (i64)f.size()) return std::nullopt;
+        return c.reconstruct_path(f[(size_t)i]).action_ids(c.model());
+    }
     std::optional<std::vector<i64>> discovery_actions(const std::string& n) const override {
         auto fp = c.discovery_fp(n);
         if (!fp) return std::nullopt;
@@ -67,6 +75,55 @@ struct Handle : HandleBase {
     std::string report() const override { return c.report_done(); }
 };
 
+template <class M, class = void>
+struct has_representative : std::false_type {};
+template <class M>
+struct has_representative<M, std::void_t<decltype(std::declval<const M&>().representative(
+                                 std::declval<const typename M::State&>()))>> : std::true_type {};
+
+// `spawn_dfs` (src/checker/dfs.rs), optionally with `symmetry()`.
+template <class M>
+struct DfsHandle : HandleBase {
+    DfsChecker<M> c;
+    DfsHandle(M m, CheckerOptions o, typename DfsChecker<M>::Representative rep) : c(std::move(m), o, std::move(rep)) {}
+    void join() override { c.join(); }
+    u64 state_count() const override { return c.state_count(); }
+    u64 unique_state_count() const override { return c.unique_state_count(); }
+    u32 max_depth() const override { return 0; }
+    bool is_done() const override { return c.is_done(); }
+    double elapsed() const override { return c.elapsed_sec(); }
+    std::vector<std::string> discovery_names() const override { return c.discovery_names(); }
+    std::optional<std::vector<i64>> visit_path(i64 i) const override {
+        if (i < 0 || i >= (i64)c.visit_count()) return std::nullopt;
+        return c.visit_path((size_t)i).action_ids(c.model());
+    }
+    std::optional<std::vector<i64>> discovery_actions(const std::string& n) const override {
+        auto p = c.discovery(n);
+        if (!p) return std::nullopt;
+        return p->action_ids(c.model());
+    }
+    std::optional<std::vector<i64>> discovery_states(const std::string& n) const override {
+        auto p = c.discovery(n);
+        if (!p) return std::nullopt;
+        std::vector<i64> out;
+        for (auto& [s, a] : p->steps) {
+            auto d = c.model().describe(s);
+            out.insert(out.end(), d.begin(), d.end());
+        }
+        return out;
+    }
+    std::vector<i64> visits() const override {
+        std::vector<i64> out;
+        for (auto& s : c.visits()) {
+            auto d = c.model().describe(s);
+            out.insert(out.end(), d.begin(), d.end());
+        }
+        return out;
+    }
+    int width() const override { return (int)c.model().describe(c.model().init_states().front()).size(); }
+    std::string report() const override { return ""; }
+};
+
 DGraph make_dgraph(const i64* p, int np) {
     // params: [expectation(0 always,1 eventually,2 sometimes), len0, v..., len1, v..., ...]
     DGraph g;
@@ -91,6 +148,7 @@ auto with_model(int model, const i64* p, int np, F&& f) {
         case INCREMENT_LOCK: return f(IncrementLock{(size_t)p[0]});
         case DGRAPH: return f(make_dgraph(p, np));
         case PAXOS: return f(paxos::PaxosModel{(size_t)p[0], 3});
+        case SYM_TOY: return f(SymToy{});
     }
     throw std::runtime_error("unknown model id " + std::to_string(model));
 }
@@ -114,6 +172,32 @@ void* oracle_spawn_bfs(int model, const i64* params, int nparams, int threads, u
         o.record_visits = record_visits != 0;
         return with_model(model, params, nparams, [&](auto m) -> HandleBase* {
             return new Handle<decltype(m)>(std::move(m), o);
+        });
+    } catch (const std::exception& e) {
+        g_last_error = e.what();
+        return nullptr;
+    }
+}
+
+void* oracle_spawn_dfs(int model, const i64* params, int nparams, int threads, u64 target, int record_visits,
+                       int symmetry) {
+    try {
+        CheckerOptions o;
+        o.thread_count = threads > 0 ? (size_t)threads : 1;
+        o.target_state_count = target;
+        o.record_visits = record_visits != 0;
+        return with_model(model, params, nparams, [&](auto m) -> HandleBase* {
+            using Mt = decltype(m);
+            typename DfsChecker<Mt>::Representative rep = nullptr;
+            if (symmetry) {
+                if constexpr (has_representative<Mt>::value) {
+                    Mt copy = m;
+                    rep = [copy](const typename Mt::State& s) { return copy.representative(s); };
+                } else {
+                    throw std::runtime_error("model has no Representative implementation");
+                }
+            }
+            return new DfsHandle<Mt>(std::move(m), o, std::move(rep));
         });
     } catch (const std::exception& e) {
         g_last_error = e.what();
@@ -170,6 +254,17 @@ i64 oracle_visits(void* h, i64* out, i64 cap) {
     auto v = static_cast<HandleBase*>(h)->visits();
     if (out) std::memcpy(out, v.data(), sizeof(i64) * (size_t)std::min<i64>(cap, (i64)v.size()));
     return (i64)v.size();
+}
+// Action ids of the path the visitor receives for visit i; -1 if out of range.
+int oracle_visit_path(void* h, i64 i, i64* out, i64 cap) {
+    try {
+        auto v = static_cast<HandleBase*>(h)->visit_path(i);
+        if (!v) return -1;
+        return copy_out(*v, out, cap);
+    } catch (const std::exception& e) {
+        g_last_error = e.what();
+        return -2;
+    }
 }
 int oracle_report(void* h, char* buf, int cap) {
     auto s = static_cast<HandleBase*>(h)->report();

@@ -201,6 +201,25 @@ struct TwoPhaseSys {
             if (m.kind == 0) h.write_usize(m.rm);
         }
     }
+    // `impl Representative for TwoPhaseState` (examples/2pc.rs:164-182): RewritePlan sorts the
+    // (rm_state, index) pairs (src/checker/rewrite_plan.rs:36-49), so RMs with EQUAL rm_state keep
+    // their index order — not a canonical form of the RM permutation group.
+    State representative(const State& s) const {
+        std::vector<std::pair<RmState, size_t>> combined;
+        for (size_t i = 0; i < s.rm_state.size(); ++i) combined.emplace_back(s.rm_state[i], i);
+        std::sort(combined.begin(), combined.end());
+        std::vector<size_t> reindex, rewrite(s.rm_state.size());
+        for (auto& c : combined) reindex.push_back(c.second);
+        for (size_t dst = 0; dst < reindex.size(); ++dst) rewrite[reindex[dst]] = dst;
+        State r;
+        r.tm_state = s.tm_state;
+        for (size_t i : reindex) {
+            r.rm_state.push_back(s.rm_state[i]);
+            r.tm_prepared.push_back(s.tm_prepared[i]);
+        }
+        for (auto& m : s.msgs) r.insert(m.kind == 0 ? Message{0, rewrite[m.rm]} : m);
+        return r;
+    }
     // [rm_state x N, tm_state, tm_prepared x N, msg Prepared(rm) x N, msg Commit, msg Abort]
     std::vector<i64> describe(const State& s) const {
         std::vector<i64> d;
@@ -354,6 +373,49 @@ struct IncrementLock {
         const char* names[] = {"Lock", "Read", "Write", "Release"};
         return std::string(names[(int)a.kind]) + "(" + std::to_string(a.thread) + ")";
     }
+};
+
+// ---------------------------------------------------------------------------------------------
+// The symmetry fixture of src/checker/dfs.rs:393-476 (`Sys`): two processes, each
+// Loading -> Running <-> Paused; either process can step. Its representative sorts the process
+// states (derived Ord: Paused < Loading < Running).
+// ---------------------------------------------------------------------------------------------
+struct SymToy {
+    enum class Proc : u8 { Paused, Loading, Running };
+    using State = std::vector<Proc>;
+    using Action = size_t;  // `Id`
+    std::vector<State> init_states() const { return {State{Proc::Loading, Proc::Loading}}; }
+    void actions(const State&, std::vector<Action>& out) const {
+        out.push_back(0);
+        out.push_back(1);
+    }
+    std::optional<State> next_state(const State& last, Action i) const {
+        State s = last;
+        s[i] = s[i] == Proc::Loading ? Proc::Running : s[i] == Proc::Running ? Proc::Paused : Proc::Running;
+        return s;
+    }
+    bool within_boundary(const State&) const { return true; }
+    std::vector<Property<SymToy>> properties() const {
+        using P = Property<SymToy>;
+        return {
+            P::always("visit all states", [](const SymToy&, const State&) { return true; }),
+            P::sometimes("a process pauses", [](const SymToy&, const State& s) {
+                return s[0] == Proc::Paused || s[1] == Proc::Paused;
+            }),
+        };
+    }
+    State representative(const State& s) const {
+        State r = s;
+        std::stable_sort(r.begin(), r.end());
+        return r;
+    }
+    void hash_state(const State& s, Hasher& h) const {
+        h.write_usize(s.size());
+        for (auto p : s) h.write_u64((u64)p);
+    }
+    std::vector<i64> describe(const State& s) const { return {(i64)s[0], (i64)s[1]}; }
+    i64 action_id(Action a) const { return (i64)a; }
+    std::string format_action(Action a) const { return "Id(" + std::to_string(a) + ")"; }
 };
 
 }  // namespace oracle

@@ -395,6 +395,7 @@ class BfsChecker {
     }
     const M& model() const { return model_; }
     const std::vector<State>& visits() const { return visits_; }
+    const std::vector<u64>& visit_fps() const { return visit_fps_; }
 
     // `reconstruct_path` (src/checker/bfs.rs:314-342).
     Path<M> reconstruct_path(u64 fp) const {
@@ -506,6 +507,7 @@ class BfsChecker {
             if (opt_.record_visits) {
                 std::lock_guard<std::mutex> g(visit_mu_);
                 visits_.push_back(job.state);
+                visit_fps_.push_back(job.fp);  // the visitor gets reconstruct_path(fp), bfs.rs:187-189
             }
             bool is_awaiting_discoveries = false;
             for (size_t i = 0; i < properties_.size(); ++i) {
@@ -566,6 +568,7 @@ class BfsChecker {
     std::exception_ptr worker_error_;
     std::mutex visit_mu_;
     std::vector<State> visits_;
+    std::vector<u64> visit_fps_;
     std::chrono::steady_clock::time_point start_;
     double elapsed_ = 0;
     bool elapsed_set_ = false;

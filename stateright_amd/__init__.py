@@ -8,8 +8,8 @@ The hot path (frontier expansion, fingerprinting, the HBM visited set, stream co
 property evaluation) runs as hand-written HIP kernels for gfx950 behind the C ABI in
 include/stateright_gpu.h; this package is the host-side mirror of the reference API.
 """
-from .checker import CheckerBuilder, CheckerError, Expectation, GpuBfsChecker, Path, StateRecorder
+from .checker import CheckerBuilder, CheckerError, Expectation, GpuBfsChecker, Path, PathRecorder, StateRecorder
 from .models import BinaryClock, DGraph, Increment, IncrementLock, LinearEquation, Paxos, TwoPhaseSys
 
-__all__ = ["CheckerBuilder", "CheckerError", "Expectation", "GpuBfsChecker", "Path", "StateRecorder",
+__all__ = ["CheckerBuilder", "CheckerError", "Expectation", "GpuBfsChecker", "Path", "PathRecorder", "StateRecorder",
            "BinaryClock", "Increment", "IncrementLock", "LinearEquation", "TwoPhaseSys"]

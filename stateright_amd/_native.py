@@ -81,6 +81,7 @@ SIGNATURES = [
     ("sr_gpu_bfs_replay", ctypes.c_int32, [_P, ctypes.c_int32, _I64P, ctypes.c_int32, _I64P, ctypes.c_int64,
                                            ctypes.POINTER(ctypes.c_int32), ctypes.c_int32]),
     ("sr_gpu_bfs_visits", ctypes.c_int64, [_P, _I64P, ctypes.c_int64]),
+    ("sr_gpu_bfs_visit_tree", ctypes.c_int64, [_P, _I64P, _I64P, ctypes.c_int64]),
     ("sr_gpu_bfs_free", None, [_P]),
     ("sr_dist_unique_id", ctypes.c_int32, [ctypes.c_char_p]),
     ("sr_dist_init", _P, [ctypes.c_int32, ctypes.c_int32, ctypes.c_char_p, ctypes.c_int32]),

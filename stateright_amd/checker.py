@@ -62,6 +62,12 @@ class Path:
     def __repr__(self):
         return f"Path({self.action_names!r})"
 
+    def __eq__(self, other):
+        return isinstance(other, Path) and (self.states, self.action_ids) == (other.states, other.action_ids)
+
+    def __hash__(self):
+        return hash((tuple(self.states), tuple(self.action_ids)))
+
 
 class StateRecorder:
     """`StateRecorder` visitor (src/checker/visitor.rs:70-99): records every visited state."""
@@ -75,6 +81,22 @@ class StateRecorder:
         return r, (lambda: list(r.states))
 
 
+class PathRecorder:
+    """`PathRecorder` visitor (src/checker/visitor.rs:32-66): records the path to every visited
+    state (as a set, like the reference's `HashSet<Path>`)."""
+
+    def __init__(self):
+        self.paths = set()
+
+    @classmethod
+    def new_with_accessor(cls):
+        r = cls()
+        return r, (lambda: set(r.paths))
+
+    def visit(self, path):
+        self.paths.add(path)
+
+
 class CheckerBuilder:
     """`CheckerBuilder` (src/checker.rs:35-178) for a registered GpuModel."""
 
@@ -86,6 +108,7 @@ class CheckerBuilder:
         self._visitor = None
         self._partitions = 1
         self._comm = None
+        self._symmetry = False
 
     # --- options mirrored from the reference ---------------------------------------------------
     def threads(self, thread_count):
@@ -101,15 +124,21 @@ class CheckerBuilder:
         return self
 
     def visitor(self, visitor):
-        """`visitor` (src/checker.rs:175-177); only `StateRecorder` is supported (batched export)."""
-        if not isinstance(visitor, StateRecorder):
-            raise TypeError("the GPU engine exports visits in bulk: pass a StateRecorder")
+        """`visitor` (src/checker.rs:175-177): a `StateRecorder`, a `PathRecorder`, or any callable
+        taking a `Path` (`impl Fn(Path)`, src/checker/visitor.rs:23-30). The GPU explores a whole
+        level per launch, so the visits are exported in bulk after the run and handed to the
+        visitor in visit order (the reference's order in FIFO mode); a visitor cannot steer the
+        search in the reference either."""
+        if not (isinstance(visitor, (StateRecorder, PathRecorder)) or callable(visitor)):
+            raise TypeError("visitor must be a StateRecorder, a PathRecorder or a callable taking a Path")
         self._visitor = visitor
         self._opts.record_visits = 1
         return self
 
     def symmetry(self):
-        # BfsChecker ignores symmetry (src/checker/bfs.rs:36-74 never reads options.symmetry).
+        """`symmetry` (src/checker.rs:145-160). The BFS checker ignores it, as the reference's does
+        (src/checker/bfs.rs:36-74 never reads options.symmetry); `spawn_dfs` rejects it (see there)."""
+        self._symmetry = True
         return self
 
     # --- engine-specific options ---------------------------------------------------------------
@@ -156,6 +185,25 @@ class CheckerBuilder:
         return GpuBfsChecker(self._model, self._opts, self._visitor)
 
     spawn_gpu_bfs = spawn_bfs
+
+    def spawn_dfs(self):
+        """`spawn_dfs` (src/checker.rs:131-136, src/checker/dfs.rs) on the GPU engine.
+
+        A check that runs to completion (no early exit) visits the same reachable set whatever the
+        traversal, so `unique_state_count`, `state_count`, `is_done` and the set of discovered
+        properties equal the reference DFS's; the engine explores level by level (FAST order) and
+        its discovery paths are BFS-tree paths (valid, and shortest). When every property gets
+        discovered, the reference stops at an order-dependent point of its depth-first order, and
+        the counts then differ. `symmetry()` is refused: the reference's representatives
+        (e.g. examples/2pc.rs:164-182) are not canonical forms, so the reduced count depends on the
+        DFS visit order itself (2pc N=5: 665 in DFS order, tests/test_oracle_dfs.py), which a
+        level-synchronous search cannot reproduce."""
+        if self._symmetry:
+            raise NotImplementedError(
+                "symmetry().spawn_dfs(): the symmetry-reduced count depends on the reference's "
+                "depth-first visit order (non-canonical representatives); not reproducible on the GPU")
+        self._opts.order = N.SR_ORDER_FAST
+        return self.spawn_bfs()
 
     def serve(self, *_):
         raise NotImplementedError("Explorer is out of scope for the GPU engine (SURVEY.md §2)")
@@ -208,8 +256,12 @@ class GpuBfsChecker:
             self._joined = True
             if st != 0:
                 raise CheckerError("sr_gpu_bfs_join", st)
-            if self._visitor is not None:
+            if isinstance(self._visitor, StateRecorder):
                 self._visitor.states.extend(self.visits())
+            elif self._visitor is not None:
+                visit = self._visitor.visit if isinstance(self._visitor, PathRecorder) else self._visitor
+                for path in self.visit_paths():
+                    visit(path)
         return self
 
     def is_done(self):
@@ -288,6 +340,28 @@ class GpuBfsChecker:
         self._lib.sr_gpu_bfs_visits(self._h, buf, n)
         flat = list(buf[:n])
         return [tuple(flat[k:k + width]) for k in range(0, n, width)]
+
+    def visit_paths(self):
+        """The path to every visited state, in visit order (what the reference hands to its
+        visitor at each pop, src/checker/bfs.rs:187-189)."""
+        n = self._lib.sr_gpu_bfs_visit_tree(self._h, None, None, 0)
+        if n < 0:
+            raise CheckerError("sr_gpu_bfs_visit_tree", n)
+        parent = (ctypes.c_int64 * max(1, n))()
+        action = (ctypes.c_int64 * max(1, n))()
+        self._lib.sr_gpu_bfs_visit_tree(self._h, parent, action, n)
+        states = self.visits()
+        out = []
+        for i in range(n):
+            chain = []
+            j = i
+            while j >= 0:
+                chain.append(j)
+                j = parent[j]
+            chain.reverse()
+            ids = [action[k] for k in chain[1:]]
+            out.append(Path([states[k] for k in chain], ids, [self.action_name(a) for a in ids]))
+        return out
 
     def stats(self):
         s = N.sr_stats()

@@ -60,6 +60,10 @@ class EngineBase {
     virtual int chain(int p, std::vector<u64>& out) = 0;
     virtual int path(int p, std::vector<i64>& actions, std::vector<i64>& states) = 0;
     virtual std::vector<i64> visits() const = 0;
+    // Per visit (visit order): the visit index of its BFS-tree parent (-1 for an init state) and
+    // the canonical id of the first action leading there (-1 for an init state). Returns false if
+    // the engine keeps no visit record.
+    virtual bool visit_tree(std::vector<i64>&, std::vector<i64>&) const { return false; }
     virtual i64 action_id_bound() const = 0;
     virtual int init_count() const = 0;
     virtual int replay(int init, const i64* ids, int n, std::vector<i64>& states, std::vector<int>& conds) const = 0;
@@ -245,6 +249,52 @@ class Engine final : public EngineBase {
             conds[p] = m_.expectation(p) == SOMETIMES ? d : !d;
         }
         return n;
+    }
+
+    // The visitor's paths (src/checker/bfs.rs:187-189 builds `Path::from_fingerprints` of every
+    // popped state): each visited state's BFS-tree parent and the FIRST action, in `actions()`
+    // order, that leads from the parent to it (src/checker/path.rs:55-79).
+    bool visit_tree(std::vector<i64>& parent, std::vector<i64>& action) const override {
+        parent.clear();
+        action.clear();
+        std::vector<u64> prev_states;
+        i64 prev_base = 0;  // visit index of the previous level's first state
+        for (size_t d = 0; d < lvisited_.size(); ++d) {
+            const u64 nv = lvisited_[d];
+            std::vector<u64> st(nv * W);
+            std::vector<u32> par(nv);
+            if (nv) {
+                SR_HIP(hipMemcpy(st.data(), arena_.p + lstart_[d] * W, nv * W * sizeof(u64), hipMemcpyDeviceToHost));
+                SR_HIP(hipMemcpy(par.data(), apar_.p + lstart_[d], nv * sizeof(u32), hipMemcpyDeviceToHost));
+            }
+            const i64 base = (i64)parent.size();
+            for (u64 i = 0; i < nv; ++i) {
+                if (d == 0) {
+                    parent.push_back(-1);
+                    action.push_back(-1);
+                    continue;
+                }
+                const u64 pr = par[i];
+                if (pr >= prev_states.size() / W) throw Error(SR_ERR_NONDETERMINISM, "visit parent outside the visited prefix");
+                const u64* ps = &prev_states[pr * W];
+                const u64 want = fingerprint<W>(&st[i * W]);
+                u64 mask[M::MW];
+                m_.enabled(ps, mask);
+                i64 id = -1;
+                for (int w = 0; w < M::MW && id < 0; ++w)
+                    for (u64 bits = mask[w]; bits && id < 0; bits &= bits - 1) {
+                        const int a = w * 64 + __builtin_ctzll(bits);
+                        u64 ns[W];
+                        if (m_.apply(ps, a, ns) && fingerprint<W>(ns) == want) id = m_.action_id(ps, a);
+                    }
+                if (id < 0) throw Error(SR_ERR_NONDETERMINISM, "Unable to reconstruct a `Path` for a visited state");
+                parent.push_back(prev_base + (i64)pr);
+                action.push_back(id);
+            }
+            prev_states.swap(st);
+            prev_base = base;
+        }
+        return true;
     }
 
     std::vector<i64> visits() const override {
@@ -1032,6 +1082,24 @@ int64_t sr_gpu_bfs_visits(const sr_bfs* b, int64_t* out, int64_t cap) {
     auto v = b->e->visits();
     if (out) std::memcpy(out, v.data(), (size_t)std::min<int64_t>(cap, (int64_t)v.size()) * sizeof(int64_t));
     return (int64_t)v.size();
+}
+
+int64_t sr_gpu_bfs_visit_tree(const sr_bfs* b, int64_t* parent, int64_t* action, int64_t cap) {
+    try {
+        if (!b) return SR_ERR_ARG;
+        std::vector<i64> p, a;
+        if (!b->e->visit_tree(p, a)) {
+            set_error("this engine keeps no visit record (partitioned search)");
+            return SR_ERR_UNSUPPORTED;
+        }
+        const size_t n = std::min<size_t>((size_t)std::max<int64_t>(cap, 0), p.size());
+        if (parent) std::memcpy(parent, p.data(), n * sizeof(i64));
+        if (action) std::memcpy(action, a.data(), n * sizeof(i64));
+        return (int64_t)p.size();
+    } catch (const Error& x) {
+        set_error(x.what());
+        return x.code;
+    }
 }
 
 int64_t sr_gpu_bfs_action_id_bound(const sr_bfs* b) { return b ? b->e->action_id_bound() : 0; }

@@ -13,6 +13,7 @@ LIB_PATH = os.path.join(ORACLE_DIR, "liboracle.so")
 
 # Model ids shared with include/stateright_gpu.h (SR_MODEL_*).
 LINEAR_EQUATION, BINARY_CLOCK, TWO_PHASE, INCREMENT, INCREMENT_LOCK, DGRAPH, PAXOS = 1, 2, 3, 4, 5, 6, 7
+SYM_TOY = 8  # oracle only: the symmetry fixture of src/checker/dfs.rs:393-476
 
 _lib = None
 
@@ -26,6 +27,9 @@ def lib():
         i64p = ctypes.POINTER(ctypes.c_int64)
         L.oracle_spawn_bfs.restype = ctypes.c_void_p
         L.oracle_spawn_bfs.argtypes = [ctypes.c_int, i64p, ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_int]
+        L.oracle_spawn_dfs.restype = ctypes.c_void_p
+        L.oracle_spawn_dfs.argtypes = [ctypes.c_int, i64p, ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_int,
+                                       ctypes.c_int]
         L.oracle_join.argtypes = [ctypes.c_void_p]
         for f in ("oracle_state_count", "oracle_unique_state_count"):
             getattr(L, f).restype = ctypes.c_uint64
@@ -43,6 +47,7 @@ def lib():
         L.oracle_visits.restype = ctypes.c_int64
         L.oracle_visits.argtypes = [ctypes.c_void_p, i64p, ctypes.c_int64]
         L.oracle_report.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int]
+        L.oracle_visit_path.argtypes = [ctypes.c_void_p, ctypes.c_int64, i64p, ctypes.c_int64]
         L.oracle_free.argtypes = [ctypes.c_void_p]
         L.oracle_last_error.restype = ctypes.c_char_p
         L.oracle_replay.argtypes = [ctypes.c_int, i64p, ctypes.c_int, i64p, ctypes.c_int, i64p, ctypes.c_int64,
@@ -61,11 +66,15 @@ def _arr(vals):
 class OracleRun:
     """Runs the restated `spawn_bfs().join()` and exposes the `Checker` surface."""
 
-    def __init__(self, model, params=(), threads=1, target=0, record_visits=False):
+    def __init__(self, model, params=(), threads=1, target=0, record_visits=False, dfs=False, symmetry=False):
+        """`spawn_bfs` (default) or `spawn_dfs` (dfs=True, optionally with `symmetry()`)."""
         L = lib()
         self.model, self.params = model, list(params)
         p = _arr(self.params)
-        self.h = L.oracle_spawn_bfs(model, p, len(self.params), threads, target, int(record_visits))
+        if dfs:
+            self.h = L.oracle_spawn_dfs(model, p, len(self.params), threads, target, int(record_visits), int(symmetry))
+        else:
+            self.h = L.oracle_spawn_bfs(model, p, len(self.params), threads, target, int(record_visits))
         if not self.h:
             raise RuntimeError(L.oracle_last_error().decode())
         if L.oracle_join(self.h) != 0:
@@ -117,6 +126,21 @@ class OracleRun:
         L.oracle_visits(self.h, buf, n)
         flat = list(buf[:n])
         return [tuple(flat[i:i + self.width]) for i in range(0, n, self.width)]
+
+    def visit_paths(self):
+        """Action ids of the path the reference's visitor receives at each pop, in visit order."""
+        L = lib()
+        buf = (ctypes.c_int64 * 65536)()
+        out = []
+        i = 0
+        while True:
+            n = L.oracle_visit_path(self.h, i, buf, 65536)
+            if n == -1:
+                return out
+            if n < 0:
+                raise RuntimeError(L.oracle_last_error().decode())
+            out.append(list(buf[:n]))
+            i += 1
 
     def report(self):
         buf = ctypes.create_string_buffer(1 << 16)

@@ -1,0 +1,70 @@
+"""Visitors on the MI355X engine (src/checker/visitor.rs): StateRecorder, PathRecorder and plain
+callables. The reference hands `Path::from_fingerprints(reconstruct_path(fp))` of every popped
+state to the visitor (src/checker/bfs.rs:187-189); the engine exports the BFS tree after the run
+(sr_gpu_bfs_visit_tree) and replays the same paths in visit order. In FIFO order the paths must be
+exactly the oracle's; in FAST order every path must replay on the CPU model to its state with the
+BFS depth of that state."""
+import pytest
+
+from oracle_lib import BINARY_CLOCK, INCREMENT, LINEAR_EQUATION, PAXOS, TWO_PHASE, OracleRun, replay
+
+pytestmark = pytest.mark.gpu
+sr = pytest.importorskip("stateright_amd")
+
+MODELS = {
+    LINEAR_EQUATION: lambda p: sr.LinearEquation(*p),
+    BINARY_CLOCK: lambda p: sr.BinaryClock(),
+    TWO_PHASE: lambda p: sr.TwoPhaseSys(*p),
+    INCREMENT: lambda p: sr.Increment(*p),
+    PAXOS: lambda p: sr.Paxos(*p),
+}
+CASES = [(LINEAR_EQUATION, [2, 10, 14]), (BINARY_CLOCK, []), (TWO_PHASE, [2]), (TWO_PHASE, [3]),
+         (INCREMENT, [3]), (PAXOS, [1])]
+
+
+def ids(c):
+    return {LINEAR_EQUATION: "lineq", BINARY_CLOCK: "clock", TWO_PHASE: "2pc", INCREMENT: "inc", PAXOS: "paxos"}[c[0]] + \
+        "-" + "-".join(map(str, c[1]))
+
+
+@pytest.mark.parametrize("case", CASES, ids=ids)
+def test_fifo_visitor_paths_equal_oracle(case):
+    model, params = case
+    o = OracleRun(model, params, record_visits=True)
+    seen = []
+    MODELS[model](params).checker().order("fifo").visitor(seen.append).spawn_bfs().join()
+    assert [p.action_ids for p in seen] == o.visit_paths()
+    assert [p.last_state() for p in seen] == o.visits()
+
+
+@pytest.mark.parametrize("case", CASES, ids=ids)
+def test_path_recorder_matches_oracle(case):
+    model, params = case
+    o = OracleRun(model, params, record_visits=True)
+    recorder, accessor = sr.PathRecorder.new_with_accessor()
+    MODELS[model](params).checker().order("fifo").visitor(recorder).spawn_bfs().join()
+    got = {(tuple(p.action_ids), p.last_state()) for p in accessor()}
+    want = {(tuple(a), s) for a, s in zip(o.visit_paths(), o.visits())}
+    assert got == want
+
+
+def test_fast_visitor_paths_replay():
+    n = 4
+    seen = []
+    c = sr.TwoPhaseSys(n).checker().order("fast").visitor(seen.append).spawn_bfs().join()
+    assert len(seen) == c.unique_state_count()
+    assert len({p.last_state() for p in seen}) == len(seen)
+    for p in seen:
+        states, _ = replay(TWO_PHASE, [n], p.action_ids, n_props=3)
+        width = len(p.last_state())
+        assert tuple(states[-width:]) == p.last_state()
+        assert [tuple(states[k:k + width]) for k in range(0, len(states), width)] == p.into_states()
+    # BFS-tree paths are shortest paths: each state's path length is its BFS level
+    o = OracleRun(TWO_PHASE, [n], record_visits=True)
+    depth = {s: len(a) for s, a in zip(o.visits(), o.visit_paths())}
+    assert all(len(p) == depth[p.last_state()] for p in seen)
+
+
+def test_visitor_rejected_by_partitioned_search():
+    with pytest.raises(NotImplementedError):
+        sr.TwoPhaseSys(3).checker().partitions(2).visitor(lambda p: None).spawn_bfs()
