@@ -103,6 +103,8 @@ typedef struct sr_stats {
     uint64_t successors;         /* == state_count - init states                                 */
     uint32_t words_per_state;
     uint32_t order_used;         /* enum sr_order actually used for the reported counts          */
+    uint32_t restarts;           /* capacity restarts of this check (larger buffers / synchronous) */
+    uint32_t pipelined;          /* partitioned search: 1 = levels pipelined, no host wait inside */
 } sr_stats;
 
 typedef struct sr_bfs sr_bfs;

@@ -1,4 +1,5 @@
 """Times the partitioned search on one GPU: T virtual partitions and a one-rank RCCL communicator."""
+import os
 import sys
 import time
 
@@ -21,13 +22,24 @@ def timed(make, reps=5):
     return best, c
 
 
-for parts in (1, 2, 4, 8):
-    dt, c = timed(lambda: TwoPhaseSys(n).checker().partitions(parts).capacity_hint(want))
-    print(f"virtual parts={parts}: {dt * 1e3:.2f} ms  levels={c.stats()['levels']}  {want / dt / 1e9:.3f} G unique/s", flush=True)
-comm = Communicator(0, 1, Communicator.unique_id(), 0)
-dt, c = timed(lambda: TwoPhaseSys(n).checker().comm(comm).capacity_hint(want))
-print(f"rccl world=1: {dt * 1e3:.2f} ms  {want / dt / 1e9:.3f} G unique/s", flush=True)
-del c
-comm.close()
+def st(c):
+    s = c.stats()
+    return f"pipelined={s['pipelined']} restarts={s['restarts']}"
+
+
+for mode in ("pipelined", "sync"):
+    if mode == "sync":
+        os.environ["SR_DIST_SYNC"] = "1"
+    else:
+        os.environ.pop("SR_DIST_SYNC", None)
+    print(f"== {mode}", flush=True)
+    for parts in (1, 2, 4, 8):
+        dt, c = timed(lambda: TwoPhaseSys(n).checker().partitions(parts).capacity_hint(want))
+        print(f"virtual parts={parts}: {dt * 1e3:.2f} ms  levels={c.stats()['levels']}  {want / dt / 1e9:.3f} G unique/s  {st(c)}", flush=True)
+    comm = Communicator(0, 1, Communicator.unique_id(), 0)
+    dt, c = timed(lambda: TwoPhaseSys(n).checker().comm(comm).capacity_hint(want))
+    print(f"rccl world=1: {dt * 1e3:.2f} ms  {want / dt / 1e9:.3f} G unique/s  {st(c)}", flush=True)
+    del c
+    comm.close()
 dt, c = timed(lambda: TwoPhaseSys(n).checker().capacity_hint(want))
 print(f"single-GPU engine: {dt * 1e3:.2f} ms  {want / dt / 1e9:.3f} G unique/s", flush=True)

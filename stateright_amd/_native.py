@@ -48,6 +48,8 @@ class sr_stats(ctypes.Structure):
         ("successors", ctypes.c_uint64),
         ("words_per_state", ctypes.c_uint32),
         ("order_used", ctypes.c_uint32),
+        ("restarts", ctypes.c_uint32),
+        ("pipelined", ctypes.c_uint32),
     ]
 
     def as_dict(self):

@@ -49,6 +49,9 @@ struct DistContext {
         HostCounters* hc = nullptr;
         HostCounters* hc_dev = nullptr;
         u32 seq = 0;
+        LagPub* pub[2] = {nullptr, nullptr};      // pipelined mode: pinned, slot = seq & 1
+        LagPub* pub_dev[2] = {nullptr, nullptr};
+        size_t pub_words = 0;
     };
     static constexpr size_t ROW_WORDS = (size_t)MAX_PARTS * (MAX_PARTS + 6 + MAX_PROPS);
     int dev = 0;
@@ -78,6 +81,20 @@ struct DistContext {
             parts.push_back(r);
         }
     }
+    // pinned publish slots of partition i holding `words` row words
+    void ensure_pub(size_t i, size_t words) {
+        PartRes& r = parts[i];
+        if (r.pub_words >= words) return;
+        for (int k = 0; k < 2; ++k) {
+            if (r.pub[k]) SR_HIP(hipHostFree(r.pub[k]));
+            const size_t bytes = sizeof(LagPub) + words * 8;
+            SR_HIP(hipHostMalloc(&r.pub[k], bytes, hipHostMallocCoherent | hipHostMallocMapped));
+            SR_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&r.pub_dev[k]), r.pub[k], 0));
+            std::memset(r.pub[k], 0, bytes);
+            r.pub[k]->seq = ~0u;
+        }
+        r.pub_words = words;
+    }
 };
 
 template <class M>
@@ -103,6 +120,8 @@ class DistEngine final : public EngineBase {
         HostCounters* hc = nullptr;      // pinned host (root level only)
         HostCounters* hc_dev = nullptr;
         u32 seq = 0;
+        u32 res = 0;                     // index of this partition's pooled resources
+        u64 send_words = 0, recv_words = 0;  // pipelined mode: allocated bucket words
         HostCounters last{};             // last published snapshot
         u64 n = 0;                       // current frontier size (exact once its row is gathered)
         u64 n_hi = 0, n_est = 0;         // upper bound / estimate of the next frontier size
@@ -159,6 +178,7 @@ class DistEngine final : public EngineBase {
                 parts_[i].hc = r.hc;
                 parts_[i].hc_dev = r.hc_dev;
                 parts_[i].seq = r.seq;
+                parts_[i].res = (u32)i;
             }
         }
         for (int attempt = 0;; ++attempt) {
@@ -167,10 +187,19 @@ class DistEngine final : public EngineBase {
                 return;
             } catch (const Error& e) {
                 if (e.code != SR_ERR_CAPACITY || attempt >= 3) throw;
+                SR_HIP(hipStreamSynchronize(stream_));
+                stats.restarts++;
+                restarts_++;
+                if (lag_) {
+                    // the pipelined plan under-estimated a level: rerun with one host
+                    // synchronisation per level (exact bucket sizes)
+                    if (o_.verbose) std::fprintf(stderr, "[sr] %s; restarting in synchronous mode\n", e.what());
+                    lag_ = false;
+                    continue;
+                }
                 if (o_.verbose) std::fprintf(stderr, "[sr] %s; restarting with larger buffers\n", e.what());
                 pessimistic_ = true;
                 grow_factor_ *= 4;
-                SR_HIP(hipStreamSynchronize(stream_));
             }
         }
     }
@@ -317,6 +346,8 @@ class DistEngine final : public EngineBase {
         stats = sr_stats{};
         stats.words_per_state = W;
         stats.order_used = SR_ORDER_FAST;
+        stats.restarts = restarts_;
+        stats.pipelined = lag_ ? 1u : 0u;
         const u64 hint = o_.capacity_hint ? o_.capacity_hint : (u64)1 << 22;
         gl_lstart_.assign(T_, {});
         gl_off_.assign(T_, 0);
@@ -388,7 +419,8 @@ class DistEngine final : public EngineBase {
         // insert_recv and the NEXT level's expand_route are enqueued right after it; the next
         // expand reads its frontier size from the device (DistCtl), so the GPU never waits for
         // the host between the insert and the next expansion.
-        for (u32 level = 0;; ++level) {
+        if (lag_) lag_loop(unique_total, undiscovered);
+        else for (u32 level = 0;; ++level) {
             // ---- 1. expand + route (grid sized from an upper bound of the frontier) ----
             const u64 d_eff = pessimistic_ ? D_ : std::min<u64>(D_, (u64)std::ceil(1.5 * ratio + 1.0));
             for (auto& p : parts_) {
@@ -418,7 +450,7 @@ class DistEngine final : public EngineBase {
                 u64* row = comm_ ? rows_mine_.p : rows_all_.p + (u64)p.id * RW;
                 expand_route<M, 1><<<grid, 256, filt_log2_ ? (8u << filt_log2_) : 0u, stream_>>>(
                     m_, p.arena.p, p.apar.p, nb, p.arena_cap, p.view(), p.id, T_, p.send.p, (u32)p.bucket_cap,
-                    p.sendc.p, p.lc, p.ctl, undiscovered, row, ppw_log2, filt_log2_);
+                    p.sendc.p, p.lc, p.ctl, undiscovered, row, ppw_log2, filt_log2_, p.bucket_cap * REC, 0u);
                 SR_HIP(hipGetLastError());
                 if (o_.profile) SR_HIP(hipEventRecord(event(2 * stats.expand_launches + 1), stream_));
                 stats.expand_launches++;
@@ -547,6 +579,231 @@ class DistEngine final : public EngineBase {
         stats.table_capacity = parts_[0].cap * T_;
     }
 
+    // ---- pipelined level loop ------------------------------------------------------------------
+    // No host wait inside a level. Level L is enqueued as expand_route -> ONE all-to-all of
+    // fixed-capacity buckets (C records each, the sender's row in a header) -> insert_recv_lag,
+    // whose last workgroup closes the level on the device and publishes every row to pinned host
+    // memory. The host enqueues level L+1 BEFORE it reads level L's rows, planning L+1 from the
+    // rows of level L-1 (identical on every rank, so every rank makes the same collective-size
+    // decision). An under-estimated bucket, arena or table shows up as an error bit in the rows of
+    // that level or the next one on every rank, and all ranks restart together in the synchronous
+    // mode (`run`).
+    u64 lag_S(u64 C) const { return DIST_HDR + C * REC; }
+
+    void lag_enqueue(u32 level, u64 C, u32 undiscovered, const std::vector<u64>& n_plan) {
+        const u64 S = lag_S(C);
+        const size_t RW = T_ + 6 + M::NPROPS;
+        bool sync = false;
+        for (auto& p : parts_) {
+            if (p.send_words < S * T_ || p.recv_words < S * T_) {
+                if (!sync) SR_HIP(hipStreamSynchronize(stream_));  // in-flight levels use the old buffers
+                sync = true;
+                const u64 words = std::max<u64>(S * T_, p.send_words * 2);
+                p.send.alloc(o_.device, words);
+                p.recv.alloc(o_.device, words);
+                p.send_words = p.recv_words = words;
+            }
+        }
+        for (auto& p : parts_) {
+            if (o_.profile) SR_HIP(hipEventRecord(event(2 * stats.expand_launches), stream_));
+            const u32 ppw_log2 = route_ppw_env_ >= 0 ? (u32)route_ppw_env_ : ppw_for(n_plan[p.id]);
+            const u32 grid = (u32)std::min<u64>(std::max<u64>(1, blocks_for(n_plan[p.id], 4u << ppw_log2)), 8192);
+            u64* row = comm_ ? rows_mine_.p : rows_all_.p + (u64)p.id * RW;
+            expand_route<M, 1><<<grid, 256, filt_log2_ ? (8u << filt_log2_) : 0u, stream_>>>(
+                m_, p.arena.p, p.apar.p, 0, p.arena_cap, p.view(), p.id, T_, p.send.p + DIST_HDR, (u32)C, p.sendc.p,
+                p.lc, p.ctl, undiscovered, row, ppw_log2, filt_log2_, S, 1u);
+            SR_HIP(hipGetLastError());
+            if (o_.profile) SR_HIP(hipEventRecord(event(2 * stats.expand_launches + 1), stream_));
+            stats.expand_launches++;
+        }
+        if (comm_) {
+            SR_NCCL(ncclAllToAll(parts_[0].send.p, parts_[0].recv.p, S, ncclUint64, comm_->nccl, stream_));
+        } else {
+            for (auto& dst : parts_)
+                for (auto& src : parts_)
+                    SR_HIP(hipMemcpyAsync(dst.recv.p + (u64)src.id * S, src.send.p + (u64)dst.id * S, S * 8,
+                                          hipMemcpyDeviceToDevice, stream_));
+        }
+        const u32 ig = (u32)std::min<u64>(std::max<u64>(1, blocks_for((u64)T_ * C, 256)), 2048);
+        for (auto& p : parts_) {
+            p.seq++;
+            auto& r = ctx_->parts[p.res];
+            insert_recv_lag<M><<<ig, 256, 0, stream_>>>(m_, p.recv.p, S, (u32)C, p.id, T_, p.view(), p.arena.p, p.apar.p,
+                                                        p.arena_cap, p.lc, undiscovered, p.ctl, r.pub_dev[p.seq & 1], p.seq);
+            SR_HIP(hipGetLastError());
+        }
+        (void)level;
+    }
+
+    // Waits for partition p's publish of the level tagged `seq`.
+    const LagPub* lag_wait(Part& p, u32 seq) {
+        auto& r = ctx_->parts[p.res];
+        const LagPub* pub = r.pub[seq & 1];
+        volatile const u32* flag = &pub->seq;
+        for (u64 spin = 1;; ++spin) {
+            if (*flag == seq) break;
+            if ((spin & 4095) == 0) {
+                hipError_t e = hipStreamQuery(stream_);
+                if (e != hipSuccess && e != hipErrorNotReady) SR_HIP(e);
+                if (e == hipSuccess && *flag != seq) {
+                    if (*flag == seq) break;
+                    throw Error(SR_ERR_HIP, "pipelined level finished without publishing its rows");
+                }
+            }
+            _mm_pause();
+        }
+        std::atomic_thread_fence(std::memory_order_acquire);
+        return pub;
+    }
+
+    void lag_loop(u64& unique_total, u32& undiscovered) {
+        const size_t RW = T_ + 6 + M::NPROPS;
+        for (auto& p : parts_) ctx_->ensure_pub(p.res, RW * T_);
+        const u64 cmin = lag_cmin_;
+        glob_prev_ = 0;
+        // What the plan knows (the same on every rank): exact frontier sizes up to the last rows
+        // processed, an upper bound of the next one (local claims + records received), the growth
+        // of the last exact step, and records per (source, destination) pair per frontier state.
+        std::vector<u64> n_last(T_, 0), n_hi(T_, 0), n_plan(T_, 0);
+        u64 glob0 = 0;
+        for (auto& p : parts_) glob0 += p.n;
+        if (comm_) glob0 *= T_;  // level 0 (roots): a rank knows only its own share
+        for (u32 q = 0; q < T_; ++q) n_last[q] = std::max<u64>(1, glob0 / T_);
+        double growth = (double)std::min<u32>(D_, 32);  // first levels: no measurement yet
+        double pair_ratio = 0.0;
+        bool have_rows = false;
+        for (u32 q = 0; q < T_; ++q) n_plan[q] = n_last[q];
+        lag_enqueue(0, cmin, undiscovered, n_plan);
+        std::vector<u32> seq0(parts_.size());
+        for (size_t i = 0; i < parts_.size(); ++i) seq0[i] = parts_[i].seq;  // level L: seq0 + L
+        // Plan and enqueue the next level, `ahead` levels past the last rows read (1 or 2).
+        u32 enq = 1;  // the next level to enqueue
+        u64 C = cmin;
+        auto plan_enqueue = [&](u32 ahead) {
+            // growth of the last exact step with a margin (no floor at 1: shrinking tails shrink the
+            // buckets too); it compounds once per level of look-ahead
+            const double g = growth * 1.1;
+            const double gc = std::max(1.0, growth) * 1.3;  // capacities: cheap, so generous
+            u64 glob_fr = 0;
+            for (auto& p : parts_) {
+                // the frontier after the last rows (<= its upper bound), the target level's
+                // frontier and the states it will claim
+                const u64 hi = have_rows ? n_hi[p.id] : (u64)((double)n_last[p.id] * gc) + 64;
+                const u64 c1 = std::min<u64>(hi, (u64)((double)n_last[p.id] * gc) + 64);
+                const u64 fr = ahead == 2 ? (u64)((double)c1 * gc) + 1024 : c1;
+                const u64 nw = (u64)((double)fr * gc) + 1024;
+                const u64 before = ahead == 2 ? hi : 0;  // a frontier between the rows and the target
+                while ((double)(p.uniq + before + hi + fr + nw) > 0.75 * (double)p.cap) grow_table(p);
+                const u64 need = p.lstart.back() + hi + (ahead == 2 ? fr : 0) + nw + 1024;
+                if (p.arena_cap < need) ensure_arena(p, std::max<u64>(need + need / 4, p.arena_cap * 2), p.arena_cap);
+                n_plan[p.id] = fr;
+            }
+            for (u32 q = 0; q < T_; ++q) {
+                const u64 c1 = have_rows ? std::min<u64>(n_hi[q], (u64)((double)n_last[q] * g) + 64) : n_last[q];
+                glob_fr += ahead == 2 ? (u64)((double)c1 * g) : c1;
+            }
+            C = have_rows ? std::max<u64>(cmin, (u64)(pair_ratio * (double)glob_fr * 1.15) + 256) : cmin;
+            lag_enqueue(enq++, C, undiscovered, n_plan);
+        };
+        for (u32 level = 0;; ++level) {
+            // ---- level+1 is enqueued before the rows of `level` are read, unless it is big: then
+            // its buckets are planned one level closer (one host round trip, tighter buckets) ----
+            u64 glob_last = 0;
+            for (u32 q = 0; q < T_; ++q) glob_last += n_last[q];
+            const bool big = have_rows && (double)glob_last * growth * growth >= (double)lag_big_;
+            if (enq == level + 1 && !big) plan_enqueue(have_rows ? 2 : 1);
+
+            // ---- the rows of `level` ----
+            const LagPub* pub = nullptr;
+            for (size_t i = 0; i < parts_.size(); ++i) {
+                const LagPub* pb = lag_wait(parts_[i], seq0[i] + level);
+                if (i == 0) pub = pb;
+            }
+            rows_.assign(pub->rows, pub->rows + RW * T_);
+            const std::vector<u64>& all = rows_;
+            u64 glob_n = 0, glob_succ = 0, glob_err = 0, glob_roots = 0, glob_enabled = 0, maxpair = 0, recs = 0;
+            for (u32 q = 0; q < T_; ++q) {
+                const u64* row = &all[q * RW];
+                glob_enabled += row[T_ + 4];
+                gl_lstart_[q].push_back(gl_off_[q]);
+                gl_off_[q] += row[T_ + 0];
+                glob_n += row[T_ + 0];
+                glob_succ += row[T_ + 1];
+                glob_err |= row[T_ + 3];
+                glob_roots += row[T_ + 5];
+                for (u32 d = 0; d < T_; ++d) {
+                    maxpair = std::max<u64>(maxpair, row[d]);
+                    recs += row[d];
+                }
+            }
+            // A bucket over its capacity, an arena or a visited set too small: the sender's (or,
+            // one level later, the receiver's) error bit is in these rows on every rank.
+            if (glob_err & ERR_TABLE_FULL) throw Error(SR_ERR_CAPACITY, "visited set probe limit exceeded");
+            if (glob_err & ERR_FRONTIER_OVERFLOW) throw Error(SR_ERR_CAPACITY, "frontier or send bucket overflow");
+            u64 glob_hi = 0;
+            for (u32 q = 0; q < T_; ++q) {
+                u64 r = 0;
+                for (u32 s2 = 0; s2 < T_; ++s2) r += all[s2 * RW + q];
+                const u64 nq = all[q * RW + T_ + 0];
+                n_hi[q] = all[q * RW + T_ + 2] + r;  // upper bound of partition q's next frontier
+                glob_hi += n_hi[q];
+                n_last[q] = nq;
+            }
+            for (auto& p : parts_) {
+                if (level > 0) p.uniq += n_last[p.id];
+                p.n = n_last[p.id];
+                p.lstart.push_back(p.lstart.back() + p.n);
+            }
+            if (level == 0) unique_total = glob_roots;
+            u32 newly = 0;
+            for (int pr = 0; pr < M::NPROPS; ++pr) {
+                if (!(undiscovered >> pr & 1)) continue;
+                for (u32 q = 0; q < T_; ++q) {
+                    u32 rk = (u32)all[q * RW + T_ + 6 + pr];
+                    if (rk != ~0u) {
+                        disc_at_[pr] = DiscAt{true, level, q, rk};
+                        disc[pr].found = true;
+                        disc[pr].level = level;
+                        disc[pr].rank = rk;
+                        newly |= 1u << pr;
+                        break;
+                    }
+                }
+            }
+            undiscovered &= ~newly;
+            if (trace_) {
+                const double us = std::chrono::duration<double, std::micro>(Clock::now() - t_trace_).count();
+                std::fprintf(stderr, "[sr-lag] level %u n=%llu succ=%llu maxpair=%llu C(next)=%llu  %.1f us since last\n",
+                             level, (unsigned long long)glob_n, (unsigned long long)glob_succ,
+                             (unsigned long long)maxpair, (unsigned long long)C, us);
+                t_trace_ = Clock::now();
+            }
+            if (glob_n) {
+                en_ratio_ = std::max(1.0, (double)glob_enabled / (double)glob_n);
+                rec_ratio_ = (double)recs / (double)glob_n;
+                pair_ratio = (double)maxpair / (double)glob_n;
+                if (glob_prev_) growth = (double)glob_n / (double)glob_prev_;
+                have_rows = true;
+            }
+            glob_prev_ = glob_n;
+            if (glob_n == 0) break;  // frontier exhausted everywhere
+            if (level > 0) unique_total += glob_n;
+            max_depth = level;
+            unique = unique_total;
+            if (M::NPROPS == 0 || (newly && undiscovered == 0)) {
+                reference_done = true;
+                early_exit_ = true;
+                break;
+            }
+            state_count += glob_succ;
+            stats.successors += glob_succ;
+            stats.levels++;
+            (void)glob_hi;
+            if (enq == level + 1) plan_enqueue(1);
+        }
+        SR_HIP(hipStreamSynchronize(stream_));  // the speculative level enqueued past the end
+    }
+
     void exchange(const std::vector<u64>& all, size_t RW) {
         // receive buffers
         for (auto& p : parts_) {
@@ -638,6 +895,12 @@ class DistEngine final : public EngineBase {
     std::vector<Part> parts_;
     hipStream_t stream_ = nullptr;
     bool pessimistic_ = false;
+    bool lag_ = std::getenv("SR_DIST_SYNC") == nullptr;  // pipelined levels (synchronous on restart)
+    u64 lag_cmin_ = 8192;      // minimum bucket capacity (records) of the pipelined mode
+    u64 lag_big_ = std::getenv("SR_LAG_BIG") ? std::strtoull(std::getenv("SR_LAG_BIG"), nullptr, 10) : 262144;
+                               // global frontier from which a level is planned after the previous one's rows
+    u32 restarts_ = 0;
+    u64 glob_prev_ = 0;        // pipelined mode: global frontier of the last level read
     u64 grow_factor_ = 1;
     bool early_exit_ = false;
     std::vector<DiscAt> disc_at_;

@@ -27,9 +27,15 @@ __device__ __host__ __forceinline__ u32 owner_of(u64 fp, u32 nparts) { return (u
 struct DistCtl {
     u32 n;
     u32 roots;                   // distinct init states claimed here (level 0 only)
-    u32 pad0[30];
+    u64 nb;                      // arena offset of that frontier (pipelined mode: kept on the device)
+    u32 pad0[28];
     u32 disc_prev[MAX_PROPS];
 };
+
+// Pipelined mode: every send bucket starts with a header of HDR words holding the sender's row, so
+// the all-to-all also delivers every partition's row to every rank (no separate all-gather, no
+// host wait inside a level). Bucket q of a sender = [HDR words: row][C records].
+constexpr u32 DIST_HDR = 128;
 
 // Row published by the last workgroup of expand_route (u64 words; RW = T + 6 + NPROPS):
 //   [0, T)  records routed to each partition      T     frontier size n
@@ -70,7 +76,7 @@ __global__ void __launch_bounds__(256) expand_route(M m, u64* __restrict__ arena
                                                     u64 arena_cap, TableView t, u32 my_part, u32 nparts,
                                                     u64* __restrict__ send, u32 bucket_cap, u32* send_counts,
                                                     LevelCounters* lc, DistCtl* ctl, u32 undiscovered, u64* row,
-                                                    u32 ppw_log2, u32 filt_log2) {
+                                                    u32 ppw_log2, u32 filt_log2, u64 bucket_stride, u32 lag) {
     constexpr int W = M::W, MW = M::MW, REC = W + 1;
     constexpr int STAGE = 512 / W;          // local new states staged per chunk
     constexpr int RSTAGE = 2048 / REC;      // remote records staged per chunk (all owners)
@@ -88,6 +94,7 @@ __global__ void __launch_bounds__(256) expand_route(M m, u64* __restrict__ arena
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const u64 lanes_below = (1ull << lane) - 1;
     const u64 n = ctl->n;                   // written by the previous level's insert_recv
+    if (lag) nb = ctl->nb;                  // pipelined: the arena offset is tracked on the device
     const u64* frontier = arena + nb * W;
     u64* next = arena + (nb + n) * W;
     u64* next_par = apar + nb + n;
@@ -254,7 +261,7 @@ __global__ void __launch_bounds__(256) expand_route(M m, u64* __restrict__ arena
                     if (mine) {
                         const u32 pos = gb + __popcll(qm & lanes_below);
                         if (pos < bucket_cap) {
-                            u64* rec = &send[((u64)q * bucket_cap + pos) * REC];
+                            u64* rec = &send[(u64)q * bucket_stride + (u64)pos * REC];
 #pragma unroll
                             for (int x = 0; x < W; ++x) rec[x] = ns[j][x];
                             rec[W] = pg;
@@ -297,7 +304,7 @@ __global__ void __launch_bounds__(256) expand_route(M m, u64* __restrict__ arena
             const u32 rr = i / REC, x = i - rr * REC;
             const u32 q = rown[rr];
             const u32 pos = obase[q] + rrank[rr];
-            if (pos < bucket_cap) send[((u64)q * bucket_cap + pos) * REC + x] = rstage[rr * REC + x];
+            if (pos < bucket_cap) send[(u64)q * bucket_stride + (u64)pos * REC + x] = rstage[rr * REC + x];
             else if (x == 0) atomicOr(&lc->err, (u32)ERR_FRONTIER_OVERFLOW);
         }
     }
@@ -320,6 +327,11 @@ __global__ void __launch_bounds__(256) expand_route(M m, u64* __restrict__ arena
     row[nparts + 5] = ctl->roots;
 #pragma unroll
     for (int p = 0; p < M::NPROPS; ++p) row[nparts + 6 + p] = ctl->disc_prev[p];
+    if (lag) {  // the row travels in the header of every bucket (and so reaches every rank)
+        const u32 rw = nparts + 6 + M::NPROPS;
+        for (u32 q = 0; q < nparts; ++q)
+            for (u32 w = 0; w < rw; ++w) send[(u64)q * bucket_stride - DIST_HDR + w] = row[w];
+    }
     lc->successors = 0;
     lc->enabled = 0;
     lc->ticket = 0;
@@ -393,6 +405,116 @@ __global__ void __launch_bounds__(256) insert_recv(M m, const u64* __restrict__ 
     ctl->roots = 0;
     lc->claims = 0;
     lc->ticket = 0;
+}
+
+// Pipelined mode: the last workgroup of a launch, told to every thread of that workgroup.
+__device__ __forceinline__ bool last_block(LevelCounters* lc) {
+    __shared__ u32 is_last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) is_last = atomicAdd(&lc->ticket, 1u) == gridDim.x - 1;
+    __syncthreads();
+    return is_last != 0;
+}
+
+// Host-visible outcome of one pipelined level (pinned, two slots per partition): the rows of
+// every partition (from the bucket headers) and this partition's close.
+struct LagPub {
+    u32 seq;           // written last
+    u32 claims;        // next frontier of this partition (local + received new states)
+    u32 err;
+    u32 pad;
+    u64 rows[1];       // nparts x RW words
+};
+
+// Pipelined insert: the records of source q sit in recv[q * S + HDR ...], their count in the
+// header (source q's row, word `me`). Grid-strided over the T x C slots (counts are known only on
+// the device). The last workgroup closes the level on the device (ctl: arena offset, frontier
+// size, discoveries) and publishes every row plus the close to pinned host memory.
+template <class M>
+__global__ void __launch_bounds__(256) insert_recv_lag(M m, const u64* __restrict__ recv, u64 S, u32 C, u32 me,
+                                                       u32 nparts, TableView t, u64* __restrict__ arena,
+                                                       u64* __restrict__ apar, u64 arena_cap, LevelCounters* lc,
+                                                       u32 undiscovered, DistCtl* ctl, LagPub* pub, u32 seq) {
+    constexpr int W = M::W, REC = W + 1;
+    constexpr int STAGE = 256;
+    __shared__ u64 stage[STAGE * W];
+    __shared__ u64 stage_par[STAGE];
+    __shared__ u32 cnt_q[MAX_PARTS];
+    __shared__ u32 stage_n, base;
+    const u64 nb = ctl->nb, n = ctl->n;
+    u64* next = arena + (nb + n) * W;
+    u64* next_par = apar + nb + n;
+    const u32 next_cap = (u32)min<u64>(arena_cap > nb + n ? arena_cap - nb - n : 0, 0xffffffffull);
+    for (u32 q = threadIdx.x; q < nparts; q += blockDim.x) cnt_q[q] = (u32)min<u64>(recv[(u64)q * S + me], C);
+    const u64 slots = (u64)nparts * C;
+    for (u64 g0 = (u64)blockIdx.x * blockDim.x; g0 < slots; g0 += (u64)gridDim.x * blockDim.x) {
+        if (threadIdx.x == 0) stage_n = 0;
+        __syncthreads();
+        const u64 g = g0 + threadIdx.x;
+        if (g < slots) {
+            const u32 q = (u32)(g / C), i = (u32)(g - (u64)q * C);
+            if (i < cnt_q[q]) {
+                const u64* rec = recv + (u64)q * S + DIST_HDR + (u64)i * REC;
+                u64 ns[W];
+#pragma unroll
+                for (int x = 0; x < W; ++x) ns[x] = rec[x];
+                const u64 pgid = rec[W];
+                bool is_new;
+                find_or_claim(t, fingerprint<W>(ns), &is_new, &lc->err);
+                if (is_new) {
+                    const u32 kk = atomicAdd(&stage_n, 1u);  // < STAGE: one slot per thread
+#pragma unroll
+                    for (int x = 0; x < W; ++x) stage[kk * W + x] = ns[x];
+                    stage_par[kk] = pgid;
+                }
+            }
+        }
+        __syncthreads();
+        const u32 nl = stage_n;
+        if (threadIdx.x == 0) base = nl ? atomicAdd(&lc->claims, nl) : 0;
+        __syncthreads();
+        for (u32 k = threadIdx.x; k < nl; k += blockDim.x) {
+            const u32 pos = base + k;
+            u64 ns[W];
+#pragma unroll
+            for (int x = 0; x < W; ++x) ns[x] = stage[k * W + x];
+            if (pos < next_cap) {
+                store_state<W>(next, pos, ns);
+                next_par[pos] = stage_par[k];
+            } else {
+                atomicOr(&lc->err, (u32)ERR_FRONTIER_OVERFLOW);
+            }
+            eval_props(m, ns, pos, undiscovered, lc);
+        }
+        __syncthreads();  // the stage is reused by the next round
+    }
+    if (!last_block(lc)) return;
+    // every row (the bucket headers) to the host, then the close
+    const u32 rw = nparts + 6 + M::NPROPS;
+    for (u32 w = threadIdx.x; w < nparts * rw; w += blockDim.x) {
+        const u32 q = w / rw;
+        pub->rows[w] = recv[(u64)q * S + (w - q * rw)];
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    const u32 claims = __hip_atomic_load(&lc->claims, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const u32 err = __hip_atomic_load(&lc->err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    pub->claims = claims;
+    pub->err = err;
+    ctl->nb = nb + n;
+    ctl->n = min(claims, next_cap);
+#pragma unroll
+    for (int p = 0; p < M::NPROPS; ++p) {
+        ctl->disc_prev[p] = __hip_atomic_load(&lc->disc[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        lc->disc[p] = ~0u;
+    }
+    ctl->roots = 0;
+    lc->claims = 0;
+    lc->ticket = 0;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: host memory
+    __hip_atomic_store(&pub->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Copies the all-gathered rows to pinned host memory and then stores `seq` (the host spins on it).

@@ -117,3 +117,100 @@ def partitioned_bfs(n):
         frontier = new
         level += 1
     return unique, state_count, depth, len(visited)
+
+
+def pipelined_bfs(n, cmin=8192, big=262144):
+    """The PIPELINED level loop of dist.hpp (`lag_loop`): one exchange per level of fixed-capacity
+    buckets whose header carries the sender's row, planned from rows read one level behind (two
+    levels ahead of them), or one level ahead when the level is big. Every decision (bucket
+    capacity C, look-ahead, overflow) is a function of the rows alone, so all ranks agree. Returns
+    (unique, state_count, depth, visited, plan) where plan lists (level, C, overflowed); an
+    overflow ends the run (the engine then restarts in the synchronous mode)."""
+    rank, world = dist.get_rank(), dist.get_world_size()
+    visited, frontier = set(), []
+    if owner_of(fingerprint(0), world) == rank:
+        visited.add(0)
+        frontier.append(0)
+    roots = torch.tensor([len(frontier)], dtype=torch.int64)
+    dist.all_reduce(roots)
+    unique, state_count, depth = int(roots), 1, 0
+    plan = []
+    n_last = [max(1, int(roots) // world)] * world
+    n_hi = [0] * world
+    growth, pair_ratio, have_rows, prev = float(min(2 + 5 * n, 32)), 0.0, False, 0
+
+    def bucket_cap(ahead):
+        g = growth * 1.1
+        fr = 0
+        for q in range(world):
+            c1 = min(n_hi[q], int(n_last[q] * g) + 64) if have_rows else n_last[q]
+            fr += int(c1 * g) if ahead == 2 else c1
+        return max(cmin, int(pair_ratio * fr * 1.15) + 256) if have_rows else cmin
+
+    caps = {0: cmin}  # level -> C it runs with
+    level = 0
+    while True:
+        glob_last = sum(n_last)
+        is_big = have_rows and glob_last * growth * growth >= big
+        if level + 1 not in caps and not is_big:
+            caps[level + 1] = bucket_cap(2 if have_rows else 1)
+        C = caps[level]
+        # expand + route into buckets of capacity C (the row rides in every bucket's header)
+        buckets = [[] for _ in range(world)]
+        succ, local_new = 0, []
+        for s in frontier:
+            for t in twopc_successors(s, n):
+                succ += 1
+                if t == s:
+                    continue
+                o = owner_of(fingerprint(t), world)
+                if o == rank:
+                    if t not in visited:
+                        visited.add(t)
+                        local_new.append(t)
+                else:
+                    buckets[o].append(t)
+        row = [len(b) for b in buckets] + [len(frontier), succ, len(local_new)]
+        send = torch.full((world, len(row) + C), -1, dtype=torch.int64)
+        for q, b in enumerate(buckets):
+            send[q, :len(row)] = torch.tensor(row)
+            kept = b[:C]
+            if kept:
+                send[q, len(row):len(row) + len(kept)] = torch.tensor([x - (1 << 63) if x >= (1 << 63) else x for x in kept])
+        mats = [torch.empty_like(send) for _ in range(world)]
+        dist.all_gather(mats, send)  # gloo has no all_to_all: keep our column
+        recv = [mats[src][rank] for src in range(world)]
+        rows = [recv[src][:len(row)].tolist() for src in range(world)]
+        overflow = any(rows[src][q] > C for src in range(world) for q in range(world))
+        plan.append((level, C, overflow))
+        if overflow:
+            return unique, state_count, depth, len(visited), plan
+        new = list(local_new)
+        for src in range(world):
+            for x in recv[src][len(row):len(row) + rows[src][rank]].tolist():
+                if x not in visited:
+                    visited.add(x)
+                    new.append(x)
+        frontier = new
+        # the host reads the rows of this level
+        glob_n = sum(r[world] for r in rows)
+        maxpair = max(r[q] for r in rows for q in range(world))
+        for q in range(world):
+            n_hi[q] = rows[q][world + 2] + sum(rows[s][q] for s in range(world))
+            n_last[q] = rows[q][world]
+        if glob_n:
+            pair_ratio = maxpair / glob_n
+            if prev:
+                growth = glob_n / prev
+            have_rows = True
+        prev = glob_n
+        if glob_n == 0:
+            break
+        if level > 0:
+            unique += glob_n
+        depth = level
+        state_count += sum(r[world + 1] for r in rows)
+        if level + 1 not in caps:
+            caps[level + 1] = bucket_cap(1)
+        level += 1
+    return unique, state_count, depth, len(visited), plan

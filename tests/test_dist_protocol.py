@@ -18,13 +18,13 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, n, out):
+def _worker(rank, world, port, n, out, mode="sync", cmin=8192):
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    from dist_protocol_ref import partitioned_bfs
-    out[rank] = partitioned_bfs(n)
+    from dist_protocol_ref import partitioned_bfs, pipelined_bfs
+    out[rank] = partitioned_bfs(n) if mode == "sync" else pipelined_bfs(n, cmin=cmin)
     dist.destroy_process_group()
 
 
@@ -40,3 +40,31 @@ def test_two_rank_partitioned_protocol(n):
         assert (unique, state_count, depth) == (o.unique_state_count, o.state_count, o.max_depth)
     # the partitions are disjoint and together hold every state
     assert sum(out[r][3] for r in range(world)) == o.unique_state_count
+
+
+@pytest.mark.parametrize("n", [3, 5])
+def test_two_rank_pipelined_protocol(n):
+    # The pipelined loop: counts equal the oracle's and both ranks planned the same bucket
+    # capacity for every level (RCCL would hang on a mismatch).
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(world, _free_port(), n, out, "pipelined"), nprocs=world, join=True)
+    o = OracleRun(TWO_PHASE, [n])
+    for r in range(world):
+        unique, state_count, depth, _, plan = out[r]
+        assert (unique, state_count, depth) == (o.unique_state_count, o.state_count, o.max_depth)
+        assert not any(ov for _, _, ov in plan)
+    assert out[0][4] == out[1][4]
+    assert sum(out[r][3] for r in range(world)) == o.unique_state_count
+
+
+def test_two_rank_pipelined_overflow_is_collective():
+    # Buckets far too small: both ranks see the overflow in the same level (from the rows every
+    # rank receives) and stop together.
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(world, _free_port(), 5, out, "pipelined", 4), nprocs=world, join=True)
+    p0, p1 = out[0][4], out[1][4]
+    assert p0 == p1 and p0[-1][2]

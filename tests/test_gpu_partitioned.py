@@ -84,3 +84,28 @@ def test_rccl_single_rank():
     assert sorted(c.discoveries()) == o.discovery_names()
     del c
     comm.close()
+
+
+@pytest.mark.parametrize("parts", [2, 4, 8])
+def test_pipelined_plan_holds_on_bench_config(parts):
+    # The bench configuration (2pc N=9) must run pipelined without a capacity restart: the bucket
+    # plan depends only on the rows every rank sees, so T virtual partitions make exactly the
+    # decisions T RCCL ranks would make.
+    n = 9
+    want = 6 ** n + 4 ** n + 2 ** n
+    c = sr.TwoPhaseSys(n).checker().partitions(parts).capacity_hint(want).spawn_bfs().join()
+    st = c.stats()
+    assert c.unique_state_count() == want
+    assert st["pipelined"] == 1 and st["restarts"] == 0, st
+
+
+@pytest.mark.parametrize("sync", [False, True])
+def test_pipelined_and_synchronous_agree(sync, monkeypatch):
+    if sync:
+        monkeypatch.setenv("SR_DIST_SYNC", "1")
+    else:
+        monkeypatch.delenv("SR_DIST_SYNC", raising=False)
+    o = oracle(INCREMENT_LOCK, [7])
+    c = sr.IncrementLock(7).checker().partitions(3).spawn_bfs().join()
+    assert (c.unique_state_count(), c.state_count(), c.max_depth()) == (o.unique_state_count, o.state_count, o.max_depth)
+    assert c.stats()["pipelined"] == (0 if sync else 1)
