@@ -105,6 +105,7 @@ typedef struct sr_stats {
     uint32_t order_used;         /* enum sr_order actually used for the reported counts          */
     uint32_t restarts;           /* capacity restarts of this check (larger buffers / synchronous) */
     uint32_t pipelined;          /* partitioned search: 1 = levels pipelined, no host wait inside */
+    uint64_t bucketed_levels;    /* levels expanded by the bucketed path (expand_bucket + bucket_insert) */
 } sr_stats;
 
 typedef struct sr_bfs sr_bfs;

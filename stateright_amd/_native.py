@@ -50,6 +50,7 @@ class sr_stats(ctypes.Structure):
         ("order_used", ctypes.c_uint32),
         ("restarts", ctypes.c_uint32),
         ("pipelined", ctypes.c_uint32),
+        ("bucketed_levels", ctypes.c_uint64),
     ]
 
     def as_dict(self):

@@ -19,6 +19,7 @@
 #include "../../include/stateright_gpu.h"
 #include "device.hpp"
 #include "kernels.hpp"
+#include "kernels_bucket.hpp"
 #include "dgraph.hpp"
 #include "paxos.hpp"
 
@@ -722,6 +723,9 @@ class Engine final : public EngineBase {
         const u32 sq = next_seq();
         const u64 nbase = fbase + (dev_n ? 0 : n);  // start of the next level (dev_n: + n on the device)
         const u32 ncap = (u32)std::min<u64>(arena_cap_ - nbase, 0xffffffffu);
+        if constexpr (W == 1) {
+            if (bucket_min_ && shape >= bucket_min_) return launch_bucketed(fbase, n, dev_n, shape, undiscovered, sq, nbase, ncap);
+        }
         const u32 ppw_log2 = ppw_env_ >= 0 ? (u32)ppw_env_ : ppw_for(shape);
         const u32 grid = std::max<u32>(1, blocks_for((shape + (1u << ppw_log2) - 1) >> ppw_log2, 4));
         timed([&] {
@@ -736,6 +740,44 @@ class Engine final : public EngineBase {
             }
         });
         return sq;
+    }
+
+    // A big level (one-word states, FAST order) as expand_bucket + bucket_insert (kernels_bucket.hpp):
+    // B buckets sized so that a bucket's distinct states fit its LDS set (~1/3 load), regions sized
+    // from the successor estimate (a record that finds no room takes the direct path).
+    u32 launch_bucketed(u64 fbase, u32 n, bool dev_n, u64 shape, u32 undiscovered, u32 sq, u64 nbase, u32 ncap) {
+        const double est_new = (double)shape * std::max(ratio_, 0.5) * 1.15 + 1024.0;
+        u32 blog2 = 8;
+        while ((1u << blog2) < BK_MAXB && est_new / (double)(1u << blog2) > (double)BK_QS * 0.85) ++blog2;
+        const u32 B = 1u << blog2;
+        const double est_rec = (double)shape * en_ratio_ * 1.25 + 4096.0;  // an upper estimate (self-loops included)
+        const u32 nb = bk_blocks_;  // persistent grid: each block flushes thousands of records at a time
+        const u32 rcap = (u32)std::min<double>(est_rec / (double)(B * nb) * 1.5 + 32.0, 1u << 30);
+        ensure_buckets((u64)B * nb * rcap);
+        BucketView bk{bst_.p, bpar_.p, bcur_.p, rcap, blog2, nb};
+        const u32 ppw_log2 = 5;
+        const u32 grid = nb;
+        timed([&] {
+            expand_bucket<M><<<grid, 256, 0, stream_>>>(m_, arena_.p + fbase * W, 0u, n, view(), bk, arena_.p + nbase * W,
+                                                        apar_.p + nbase, ncap, lc_d_, undiscovered, ppw_log2, dev_n ? 1u : 0u);
+            SR_HIP(hipGetLastError());
+            bucket_insert<M><<<B, 1024, 0, stream_>>>(m_, view(), bk, arena_.p + nbase * W, apar_.p + nbase, ncap, lc_d_,
+                                                      undiscovered, hcd(sq), sq, 1u, dev_n ? 1u : 0u);
+        });
+        stats.bucketed_levels++;
+        return sq;
+    }
+
+    // Bucket regions for `records` records; grown only between levels (a stream synchronisation:
+    // launched levels may still read the old buffers).
+    void ensure_buckets(u64 records) {
+        if (!bcur_.p) bcur_.alloc(o_.device, (size_t)BK_MAXB * BK_MAXNB);
+        if (bcap_ >= records) return;
+        SR_HIP(hipStreamSynchronize(stream_));
+        const u64 cap = std::max<u64>(records, bcap_ * 2);
+        bst_.alloc(o_.device, cap);
+        bpar_.alloc(o_.device, cap);
+        bcap_ = cap;
     }
 
     // disc[p].fp from the discovering state in the arena (after the level loop).
@@ -895,6 +937,13 @@ class Engine final : public EngineBase {
     HostCounters lc_{};  // host copy of the last published counters
     LevelCounters* lc_d_ = nullptr;
     u64 cap_ = 0;
+    DBuf<u64> bst_;              // bucketed levels: bucket regions (states, parent ranks, cursors)
+    DBuf<u32> bpar_, bcur_;
+    u64 bcap_ = 0;
+    u32 bk_blocks_ = std::getenv("SR_BK_BLOCKS") ? (u32)std::atoi(std::getenv("SR_BK_BLOCKS")) : 512;
+    // Bucketed big levels are OPT-IN (SR_BUCKET_MIN = frontier size from which a level is bucketed):
+    // measured slower than expand_fast on 2pc N=9/10 ("bucketed levels").
+    u64 bucket_min_ = std::getenv("SR_BUCKET_MIN") ? std::strtoull(std::getenv("SR_BUCKET_MIN"), nullptr, 10) : 0;
     DBuf<u64> keys_, meta_;      // visited set
     DBuf<u64> arena_;            // BFS tree: every level's states in visit order
     DBuf<u32> apar_;             // parent rank (in the previous level) of each arena state

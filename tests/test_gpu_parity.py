@@ -250,3 +250,16 @@ def test_paxos_3_clients_matches_oracle(order):
     assert sorted(c.discoveries()) == ["value chosen"]
     if order == "fifo":
         assert c.discovery("value chosen").action_ids == o.discovery_actions("value chosen")
+
+
+@pytest.mark.parametrize("n", [6, 8, 9])
+def test_bucketed_levels_parity(n, monkeypatch):
+    # The opt-in bucketed path (kernels_bucket.hpp: expand into fingerprint buckets, LDS dedup per
+    # bucket, one probe per distinct state) on every level from 64 states up: counts are exact.
+    monkeypatch.setenv("SR_BUCKET_MIN", "64")
+    c = sr.TwoPhaseSys(n).checker().capacity_hint(6 ** n + 4 ** n + 2 ** n).spawn_bfs().join()
+    assert c.stats()["bucketed_levels"] > 0
+    assert c.unique_state_count() == 6 ** n + 4 ** n + 2 ** n
+    assert 3 * c.state_count() == 4 * n * 6 ** n + 3 * (n + 1) * 4 ** n + 3 * n * 2 ** n + 6
+    assert c.max_depth() == 3 * n + 1
+    assert sorted(c.discoveries()) == ["abort agreement", "commit agreement"]
