@@ -106,6 +106,7 @@ typedef struct sr_stats {
     uint32_t restarts;           /* capacity restarts of this check (larger buffers / synchronous) */
     uint32_t pipelined;          /* partitioned search: 1 = levels pipelined, no host wait inside */
     uint64_t bucketed_levels;    /* levels expanded by the bucketed path (expand_bucket + bucket_insert) */
+    uint64_t records_routed;     /* partitioned search: successor records sent between partitions (all ranks) */
 } sr_stats;
 
 typedef struct sr_bfs sr_bfs;

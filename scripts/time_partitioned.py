@@ -24,14 +24,16 @@ def timed(make, reps=5):
 
 def st(c):
     s = c.stats()
-    return f"pipelined={s['pipelined']} restarts={s['restarts']}"
+    return f"pipelined={s['pipelined']} restarts={s['restarts']} records={s['records_routed']}"
 
 
-for mode in ("pipelined", "sync"):
+for mode in ("pipelined", "sync", "nocache"):
     if mode == "sync":
         os.environ["SR_DIST_SYNC"] = "1"
     else:
         os.environ.pop("SR_DIST_SYNC", None)
+    if mode == "nocache":
+        os.environ["SR_SEND_CACHE"] = "0"
     print(f"== {mode}", flush=True)
     for parts in (1, 2, 4, 8):
         dt, c = timed(lambda: TwoPhaseSys(n).checker().partitions(parts).capacity_hint(want))

@@ -51,6 +51,7 @@ class sr_stats(ctypes.Structure):
         ("restarts", ctypes.c_uint32),
         ("pipelined", ctypes.c_uint32),
         ("bucketed_levels", ctypes.c_uint64),
+        ("records_routed", ctypes.c_uint64),
     ]
 
     def as_dict(self):

@@ -99,7 +99,7 @@ struct DistContext {
 
 template <class M>
 class DistEngine final : public EngineBase {
-    static constexpr int W = M::W, REC = W + 1;
+    static constexpr int W = M::W, REC = W, TREC = W + 1;  // record = state; tree entry = state + parent gid
     static constexpr u64 NONE = ~0ull;
 
     struct Part {
@@ -111,6 +111,8 @@ class DistEngine final : public EngineBase {
         u64 arena_cap = 0;
         std::vector<u64> lstart{0};      // arena offset of each level
         DBuf<u64> send;                  // [T][bucket_cap][REC]
+        DBuf<u64> sent;                  // sent cache (small T): fingerprints this partition routed
+        u64 sent_mask = 0;
         u64 bucket_cap = 0;
         DBuf<u32> sendc;                 // [T] records per destination (device)
         DBuf<u64> recv;
@@ -379,6 +381,16 @@ class DistEngine final : public EngineBase {
             ensure_arena(p, (per_part + per_part / 8 + 4096) * grow_factor_, 0);
             p.sendc.alloc(o_.device, T_);
             SR_HIP(hipMemsetAsync(p.sendc.p, 0, T_ * 4, stream_));
+            // sent cache: with few partitions a sender generates each remote state several times
+            // per level (in-degree / T), and every copy would cross the link
+            p.sent_mask = 0;
+            if (T_ >= 2 && T_ <= send_cache_max_parts_) {
+                u64 sc = 1u << 16;
+                while (sc < 2 * per_part * grow_factor_ && sc < ((u64)1 << 28)) sc <<= 1;
+                if (p.sent.n < sc) p.sent.alloc(o_.device, sc);
+                SR_HIP(hipMemsetAsync(p.sent.p, 0, sc * 8, stream_));
+                p.sent_mask = sc - 1;
+            }
             init_counters(p);
             insert_roots_part<M><<<1, 64, 0, stream_>>>(p.view(), dinit.p, (u32)k, p.id, T_, p.arena.p, p.apar.p, dn.p, p.lc);
             u32 n0 = 0;
@@ -450,7 +462,8 @@ class DistEngine final : public EngineBase {
                 u64* row = comm_ ? rows_mine_.p : rows_all_.p + (u64)p.id * RW;
                 expand_route<M, 1><<<grid, 256, filt_log2_ ? (8u << filt_log2_) : 0u, stream_>>>(
                     m_, p.arena.p, p.apar.p, nb, p.arena_cap, p.view(), p.id, T_, p.send.p, (u32)p.bucket_cap,
-                    p.sendc.p, p.lc, p.ctl, undiscovered, row, ppw_log2, filt_log2_, p.bucket_cap * REC, 0u);
+                    p.sendc.p, p.lc, p.ctl, undiscovered, row, ppw_log2, filt_log2_, p.bucket_cap * REC, 0u,
+                    p.sent_mask ? p.sent.p : nullptr, p.sent_mask);
                 SR_HIP(hipGetLastError());
                 if (o_.profile) SR_HIP(hipEventRecord(event(2 * stats.expand_launches + 1), stream_));
                 stats.expand_launches++;
@@ -520,6 +533,7 @@ class DistEngine final : public EngineBase {
                 for (u32 q = 0; q < T_; ++q)
                     for (u32 d = 0; d < T_; ++d) recs += all[q * RW + d];
                 rec_ratio_ = (double)recs / (double)glob_n;
+                stats.records_routed += recs;
             }
             prev_glob_n = glob_n;
             if (glob_n == 0) break;  // frontier exhausted everywhere
@@ -611,7 +625,8 @@ class DistEngine final : public EngineBase {
             u64* row = comm_ ? rows_mine_.p : rows_all_.p + (u64)p.id * RW;
             expand_route<M, 1><<<grid, 256, filt_log2_ ? (8u << filt_log2_) : 0u, stream_>>>(
                 m_, p.arena.p, p.apar.p, 0, p.arena_cap, p.view(), p.id, T_, p.send.p + DIST_HDR, (u32)C, p.sendc.p,
-                p.lc, p.ctl, undiscovered, row, ppw_log2, filt_log2_, S, 1u);
+                p.lc, p.ctl, undiscovered, row, ppw_log2, filt_log2_, S, 1u, p.sent_mask ? p.sent.p : nullptr,
+                p.sent_mask);
             SR_HIP(hipGetLastError());
             if (o_.profile) SR_HIP(hipEventRecord(event(2 * stats.expand_launches + 1), stream_));
             stats.expand_launches++;
@@ -778,6 +793,7 @@ class DistEngine final : public EngineBase {
                              (unsigned long long)maxpair, (unsigned long long)C, us);
                 t_trace_ = Clock::now();
             }
+            stats.records_routed += recs;
             if (glob_n) {
                 en_ratio_ = std::max(1.0, (double)glob_enabled / (double)glob_n);
                 rec_ratio_ = (double)recs / (double)glob_n;
@@ -852,30 +868,69 @@ class DistEngine final : public EngineBase {
         const DiscAt d = disc_at_[pr];
         // gid of the discovered state
         u64 gid = ((u64)d.part << GID_SHIFT) | (part_lstart(d.part, d.level) + d.rank);
+        u32 level = d.level;
         std::vector<u64> rev;
         DBuf<u64> buf;
-        buf.alloc(o_.device, REC);
+        DBuf<unsigned long long> best;
+        buf.alloc(o_.device, TREC);
+        best.alloc(o_.device, 1);
         for (int guard = 0; guard < (1 << 20); ++guard) {
             const u32 owner = (u32)(gid >> GID_SHIFT);
             const u64 idx = gid & (((u64)1 << GID_SHIFT) - 1);
-            u64 rec[REC];
+            u64 rec[TREC];
             if (!comm_) {
                 Part& p = parts_[owner];
-                SR_HIP(hipMemcpy(rec, p.arena.p + idx * W, W * 8, hipMemcpyDeviceToHost));
-                SR_HIP(hipMemcpy(&rec[W], p.apar.p + idx, 8, hipMemcpyDeviceToHost));
+                SR_HIP(hipMemcpy(buf.p, p.arena.p + idx * W, W * 8, hipMemcpyDeviceToDevice));
+                SR_HIP(hipMemcpy(buf.p + W, p.apar.p + idx, 8, hipMemcpyDeviceToDevice));
+                SR_HIP(hipMemcpy(rec, buf.p, TREC * 8, hipMemcpyDeviceToHost));
             } else {
                 if (owner == (u32)comm_->rank) {
                     Part& p = parts_[0];
                     SR_HIP(hipMemcpyAsync(buf.p, p.arena.p + idx * W, W * 8, hipMemcpyDeviceToDevice, stream_));
                     SR_HIP(hipMemcpyAsync(buf.p + W, p.apar.p + idx, 8, hipMemcpyDeviceToDevice, stream_));
                 }
-                SR_NCCL(ncclBroadcast(buf.p, buf.p, REC, ncclUint64, (int)owner, comm_->nccl, stream_));
-                SR_HIP(hipMemcpyAsync(rec, buf.p, REC * 8, hipMemcpyDeviceToHost, stream_));
+                SR_NCCL(ncclBroadcast(buf.p, buf.p, TREC, ncclUint64, (int)owner, comm_->nccl, stream_));
+                SR_HIP(hipMemcpyAsync(rec, buf.p, TREC * 8, hipMemcpyDeviceToHost, stream_));
                 SR_HIP(hipStreamSynchronize(stream_));
             }
             rev.insert(rev.end(), rec, rec + W);
             if (rec[W] == NONE) break;
-            gid = rec[W];
+            if (rec[W] == PAR_SEARCH) {
+                // inserted from a record: a generator in the previous level, the lowest gid among
+                // every partition's candidates (the same on every rank)
+                if (level == 0) throw Error(SR_ERR_NONDETERMINISM, "record state at level 0");
+                u64 found = NONE;
+                for (auto& p : parts_) {
+                    const u64 lo = part_lstart(p.id, level - 1), n = part_lstart(p.id, level) - lo;
+                    const unsigned long long init = ~0ull;
+                    SR_HIP(hipMemcpyAsync(best.p, &init, 8, hipMemcpyHostToDevice, stream_));
+                    if (n) find_pred<M><<<blocks_for(n, 256), 256, 0, stream_>>>(m_, p.arena.p + lo * W, (u32)n, buf.p, best.p);
+                    SR_HIP(hipGetLastError());
+                    unsigned long long h = ~0ull;
+                    if (comm_) {
+                        // local candidate as a gid, then the minimum over the ranks
+                        DBuf<unsigned long long> g;
+                        g.alloc(o_.device, 1);
+                        SR_HIP(hipMemcpyAsync(&h, best.p, 8, hipMemcpyDeviceToHost, stream_));
+                        SR_HIP(hipStreamSynchronize(stream_));
+                        unsigned long long lg = h == ~0ull ? ~0ull : (((u64)p.id << GID_SHIFT) | (lo + h));
+                        SR_HIP(hipMemcpyAsync(g.p, &lg, 8, hipMemcpyHostToDevice, stream_));
+                        SR_NCCL(ncclAllReduce(g.p, g.p, 1, ncclUint64, ncclMin, comm_->nccl, stream_));
+                        SR_HIP(hipMemcpyAsync(&h, g.p, 8, hipMemcpyDeviceToHost, stream_));
+                        SR_HIP(hipStreamSynchronize(stream_));
+                        found = std::min<u64>(found, h);
+                    } else {
+                        SR_HIP(hipMemcpyAsync(&h, best.p, 8, hipMemcpyDeviceToHost, stream_));
+                        SR_HIP(hipStreamSynchronize(stream_));
+                        if (h != ~0ull) found = std::min<u64>(found, ((u64)p.id << GID_SHIFT) | (lo + h));
+                    }
+                }
+                if (found == NONE) throw Error(SR_ERR_NONDETERMINISM, "Unable to reconstruct a `Path` across partitions");
+                gid = found;
+            } else {
+                gid = rec[W];
+            }
+            --level;
         }
         const size_t len = rev.size() / W;
         st.resize(rev.size());
@@ -900,6 +955,7 @@ class DistEngine final : public EngineBase {
     u64 lag_big_ = std::getenv("SR_LAG_BIG") ? std::strtoull(std::getenv("SR_LAG_BIG"), nullptr, 10) : 262144;
                                // global frontier from which a level is planned after the previous one's rows
     u32 restarts_ = 0;
+    u32 send_cache_max_parts_ = std::getenv("SR_SEND_CACHE") ? (u32)std::atoi(std::getenv("SR_SEND_CACHE")) : 4;
     u64 glob_prev_ = 0;        // pipelined mode: global frontier of the last level read
     u64 grow_factor_ = 1;
     bool early_exit_ = false;

@@ -9,13 +9,17 @@
 //                 {state[W], parent gid} in the send bucket of its owner (LDS-staged per owner,
 //                 one global atomic per (workgroup, owner));
 //   insert_recv   inserts the records received from every partition.
-// A parent gid is (partition << 40) | arena index: the BFS tree spans partitions.
+// A parent gid is (partition << 40) | arena index: the BFS tree spans partitions. A record carries
+// the state only (8 B for one-word states): the xGMI link is the scarce resource at small T. A
+// state inserted from a record gets the parent PAR_SEARCH, and a discovery path that reaches it
+// finds a parent in the previous level with find_pred (any generator is a valid FAST-order parent).
 #pragma once
 #include "kernels.hpp"
 
 namespace sr {
 
 constexpr int GID_SHIFT = 40;
+constexpr u64 PAR_SEARCH = ~0ull - 1;  // parent not recorded: search the previous level
 
 // Owner partition of a fingerprint: the high 32 bits scaled to [0, T) (any T, uniform).
 __device__ __host__ __forceinline__ u32 owner_of(u64 fp, u32 nparts) { return (u32)(((fp >> 32) * (u64)nparts) >> 32); }
@@ -76,8 +80,9 @@ __global__ void __launch_bounds__(256) expand_route(M m, u64* __restrict__ arena
                                                     u64 arena_cap, TableView t, u32 my_part, u32 nparts,
                                                     u64* __restrict__ send, u32 bucket_cap, u32* send_counts,
                                                     LevelCounters* lc, DistCtl* ctl, u32 undiscovered, u64* row,
-                                                    u32 ppw_log2, u32 filt_log2, u64 bucket_stride, u32 lag) {
-    constexpr int W = M::W, MW = M::MW, REC = W + 1;
+                                                    u32 ppw_log2, u32 filt_log2, u64 bucket_stride, u32 lag,
+                                                    u64* __restrict__ sent, u64 sent_mask) {
+    constexpr int W = M::W, MW = M::MW, REC = W;
     constexpr int STAGE = 512 / W;          // local new states staged per chunk
     constexpr int RSTAGE = 2048 / REC;      // remote records staged per chunk (all owners)
     extern __shared__ u64 filt[];           // 2^filt_log2 fingerprints (dynamic LDS; 0 = no filter)
@@ -184,6 +189,19 @@ __global__ void __launch_bounds__(256) expand_route(M m, u64* __restrict__ arena
                 }
                 own[j] = ok[j] ? owner_of(key[j], nparts) : my_part;
                 rem[j] = ok[j] && own[j] != my_part;
+                // Sent cache (small T): a lossy direct-mapped record of the fingerprints this
+                // partition already routed in this check. A hit is skipped: its owner received
+                // that state in this level's exchange or an earlier one, so it is visited. A miss,
+                // an eviction or a race only re-sends (the owner dedups).
+                if (sent && rem[j]) {
+                    u64* slot = &sent[key[j] & sent_mask];
+                    if (*slot == key[j]) {
+                        ++succ;
+                        ok[j] = rem[j] = false;
+                    } else {
+                        *slot = key[j];
+                    }
+                }
             }
 #pragma unroll
             for (int j = 0; j < PB; ++j) cur[j] = (ok[j] && !rem[j]) ? probe_load<0>(&t.keys[idx[j]]) : 0;
@@ -244,7 +262,6 @@ __global__ void __launch_bounds__(256) expand_route(M m, u64* __restrict__ arena
                     const u32 kk = rsb + rbelow;
 #pragma unroll
                     for (int x = 0; x < W; ++x) rstage[kk * REC + x] = ns[j][x];
-                    rstage[kk * REC + W] = pg;
                     rown[kk] = (u8)own[j];
                 }
                 // overflow (rare): per-wave reservations, owner by owner
@@ -264,7 +281,6 @@ __global__ void __launch_bounds__(256) expand_route(M m, u64* __restrict__ arena
                             u64* rec = &send[(u64)q * bucket_stride + (u64)pos * REC];
 #pragma unroll
                             for (int x = 0; x < W; ++x) rec[x] = ns[j][x];
-                            rec[W] = pg;
                         } else {
                             atomicOr(&lc->err, (u32)ERR_FRONTIER_OVERFLOW);
                         }
@@ -344,7 +360,7 @@ template <class M>
 __global__ void __launch_bounds__(256) insert_recv(M m, const u64* __restrict__ recv, u32 nrec, TableView t,
                                                    u64* __restrict__ next, u64* __restrict__ next_par, u32 next_cap,
                                                    LevelCounters* lc, u32 undiscovered, DistCtl* ctl) {
-    constexpr int W = M::W, REC = W + 1;
+    constexpr int W = M::W, REC = W;
     constexpr int STAGE = 1024 / W;
     __shared__ u64 stage[STAGE * W];
     __shared__ u64 stage_par[STAGE];
@@ -356,7 +372,7 @@ __global__ void __launch_bounds__(256) insert_recv(M m, const u64* __restrict__ 
         u64 ns[W];
 #pragma unroll
         for (int x = 0; x < W; ++x) ns[x] = recv[(u64)i * REC + x];
-        const u64 pgid = recv[(u64)i * REC + W];
+        const u64 pgid = PAR_SEARCH;
         bool is_new;
         find_or_claim(t, fingerprint<W>(ns), &is_new, &lc->err);
         if (is_new) {
@@ -436,7 +452,7 @@ __global__ void __launch_bounds__(256) insert_recv_lag(M m, const u64* __restric
                                                        u32 nparts, TableView t, u64* __restrict__ arena,
                                                        u64* __restrict__ apar, u64 arena_cap, LevelCounters* lc,
                                                        u32 undiscovered, DistCtl* ctl, LagPub* pub, u32 seq) {
-    constexpr int W = M::W, REC = W + 1;
+    constexpr int W = M::W, REC = W;
     constexpr int STAGE = 256;
     __shared__ u64 stage[STAGE * W];
     __shared__ u64 stage_par[STAGE];
@@ -459,7 +475,7 @@ __global__ void __launch_bounds__(256) insert_recv_lag(M m, const u64* __restric
                 u64 ns[W];
 #pragma unroll
                 for (int x = 0; x < W; ++x) ns[x] = rec[x];
-                const u64 pgid = rec[W];
+                const u64 pgid = PAR_SEARCH;
                 bool is_new;
                 find_or_claim(t, fingerprint<W>(ns), &is_new, &lc->err);
                 if (is_new) {
@@ -544,6 +560,23 @@ __global__ void insert_roots_part(TableView t, const u64* states, u32 n, u32 my_
         ++k;
     }
     *out_n = k;
+}
+
+// Parent search for a state inserted from a record (PAR_SEARCH): the lowest frontier index of
+// level [0, n) of this partition with a successor equal to `target` (within boundary), or ~0.
+template <class M>
+__global__ void find_pred(M m, const u64* __restrict__ level_states, u32 n, const u64* __restrict__ target_dev,
+                          unsigned long long* best) {
+    const u32 r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    u64 target[M::W];
+#pragma unroll
+    for (int x = 0; x < M::W; ++x) target[x] = target_dev[x];
+    u64 s[M::W];
+    load_state<M::W>(level_states, r, s);
+    bool hit = false;
+    for_each_successor(m, s, [&](int, const u64* ns) { hit |= same_state<M::W>(ns, target); });
+    if (hit) atomicMin(best, (unsigned long long)r);
 }
 
 }  // namespace sr
