@@ -240,7 +240,8 @@ def main():
             "algorithmic_bytes_per_step": alg_bytes / args.steps,
             "profiled_ms_per_step": profiled_elapsed / args.steps * 1e3,
         },
-        "engine": {k: st[k] for k in ("levels", "table_capacity", "rehashes", "level_loop_sec", "total_sec")},
+        "engine": {k: st[k] for k in ("levels", "table_capacity", "rehashes", "level_loop_sec", "total_sec",
+                                      "restarts", "pipelined", "records_routed")},
     }
     if args.cpu_baseline and world == 1:
         try:
