@@ -5,7 +5,16 @@
 // the protocol is tested on a single device). FAST order only (the reference's single-threaded
 // FIFO order is a single-GPU mode).
 //
-// One level, per partition p (ONE host synchronisation per level):
+// Two level loops share the kernels:
+//
+// PIPELINED (default, `lag_loop`): no host wait inside a level. expand_route writes its row into
+// the header of every fixed-capacity send bucket; ONE ncclAllToAll moves buckets and rows;
+// insert_recv_lag closes the level on the device and publishes every row to pinned memory. The
+// host enqueues level L+1 before reading level L's rows (bucket capacity planned from the rows of
+// level L-1, the same on every rank).
+//
+// SYNCHRONOUS (SR_DIST_SYNC=1, and the restart after a pipelined overflow), one host
+// synchronisation per level:
 //   1. expand_route: reads its frontier size from the device control block (DistCtl); local
 //      successors are inserted directly, the others become records for their owner's send bucket
 //      (staged in LDS per chunk, one global reservation per chunk and owner). Its last workgroup
@@ -18,7 +27,7 @@
 //      device (next frontier size, discoveries among it) so that the NEXT expand_route, enqueued
 //      right behind it, needs nothing from the host.
 // Capacity planning is optimistic; an overflow on any partition is seen by every rank in the
-// next all-gather and all of them restart the check together with larger buffers.
+// rows and all of them restart the check together with larger buffers.
 #pragma once
 #include <rccl/rccl.h>
 
