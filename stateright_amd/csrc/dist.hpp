@@ -469,10 +469,10 @@ class DistEngine final : public EngineBase {
                 const u32 ppw_log2 = route_ppw_env_ >= 0 ? (u32)route_ppw_env_ : ppw_for(p.n_est);
                 const u32 grid = (u32)std::min<u64>(std::max<u64>(1, blocks_for(p.n_hi, 4u << ppw_log2)), 8192);
                 u64* row = comm_ ? rows_mine_.p : rows_all_.p + (u64)p.id * RW;
-                expand_route<M, 1><<<grid, 256, filt_log2_ ? (8u << filt_log2_) : 0u, stream_>>>(
+                expand_route<M, 1><<<grid, 256, route_lds(), stream_>>>(
                     m_, p.arena.p, p.apar.p, nb, p.arena_cap, p.view(), p.id, T_, p.send.p, (u32)p.bucket_cap,
                     p.sendc.p, p.lc, p.ctl, undiscovered, row, ppw_log2, filt_log2_, p.bucket_cap * REC, 0u,
-                    p.sent_mask ? p.sent.p : nullptr, p.sent_mask);
+                    p.sent_mask ? p.sent.p : nullptr, p.sent_mask, rstage_recs());
                 SR_HIP(hipGetLastError());
                 if (o_.profile) SR_HIP(hipEventRecord(event(2 * stats.expand_launches + 1), stream_));
                 stats.expand_launches++;
@@ -632,10 +632,10 @@ class DistEngine final : public EngineBase {
             const u32 ppw_log2 = route_ppw_env_ >= 0 ? (u32)route_ppw_env_ : ppw_for(n_plan[p.id]);
             const u32 grid = (u32)std::min<u64>(std::max<u64>(1, blocks_for(n_plan[p.id], 4u << ppw_log2)), 8192);
             u64* row = comm_ ? rows_mine_.p : rows_all_.p + (u64)p.id * RW;
-            expand_route<M, 1><<<grid, 256, filt_log2_ ? (8u << filt_log2_) : 0u, stream_>>>(
+            expand_route<M, 1><<<grid, 256, route_lds(), stream_>>>(
                 m_, p.arena.p, p.apar.p, 0, p.arena_cap, p.view(), p.id, T_, p.send.p + DIST_HDR, (u32)C, p.sendc.p,
                 p.lc, p.ctl, undiscovered, row, ppw_log2, filt_log2_, S, 1u, p.sent_mask ? p.sent.p : nullptr,
-                p.sent_mask);
+                p.sent_mask, rstage_recs());
             SR_HIP(hipGetLastError());
             if (o_.profile) SR_HIP(hipEventRecord(event(2 * stats.expand_launches + 1), stream_));
             stats.expand_launches++;
@@ -974,7 +974,7 @@ class DistEngine final : public EngineBase {
     DBuf<u64> rows_all_, rows_mine_;  // gathered rows (T x RW) / this rank's row (RCCL mode)
     DistContext* ctx_ = nullptr;      // pooled stream, counters, pinned mirrors, events
     double en_ratio_ = 8.0;  // enabled action slots per parent, last level
-    u32 filt_log2_ = W >= 4 ? 10 : 9;
+    u32 filt_log2_ = std::getenv("SR_FILTER_LOG2") ? (u32)std::atoi(std::getenv("SR_FILTER_LOG2")) : (W >= 4 ? 10 : 9);
 
     // Parents per wave (log2) for a frontier of ~c states (the single-GPU engine's rule,
     // Engine::ppw_for): ~16 successor rounds per wave for 1-2 word states, 4 for wider ones, and
@@ -985,12 +985,18 @@ class DistEngine final : public EngineBase {
         u32 l = 2;
         while (l < 6 && (double)(2u << l) <= ppw) ++l;
         while (l > 2 && ((c + (1u << l) - 1) >> l) < 1024) --l;
-        // a chunk (4 waves) must fit the LDS record stage: 2048 / REC records
-        const double rstage = (double)(2048 / REC);
+        // a chunk (4 waves) must fit the LDS record stage
+        const double rstage = (double)std::max<u32>(rstage_recs(), 1);
         while (l > 2 && 4.0 * (double)(1u << l) * rec_ratio_ * 1.3 > rstage) --l;
         return l;
     }
     double rec_ratio_ = 4.0;  // remote records per parent, last level
+    // Records staged per chunk in LDS (none with one partition), and expand_route's dynamic LDS.
+    u32 rstage_recs() const { return T_ > 1 ? rstage_words_ / REC : 0u; }
+    size_t route_lds() const {
+        return (filt_log2_ ? (8u << filt_log2_) : 0u) + (size_t)rstage_recs() * (REC * 8 + 2 + 1);
+    }
+    u32 rstage_words_ = std::getenv("SR_RSTAGE_WORDS") ? (u32)std::atoi(std::getenv("SR_RSTAGE_WORDS")) : 1024;
     int route_ppw_env_ = std::getenv("SR_ROUTE_PPW_LOG2") ? std::atoi(std::getenv("SR_ROUTE_PPW_LOG2")) : -1;
     bool trace_ = std::getenv("SR_DIST_TRACE") != nullptr;
     Clock::time_point t_trace_ = Clock::now();

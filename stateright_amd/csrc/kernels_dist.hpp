@@ -81,16 +81,20 @@ __global__ void __launch_bounds__(256) expand_route(M m, u64* __restrict__ arena
                                                     u64* __restrict__ send, u32 bucket_cap, u32* send_counts,
                                                     LevelCounters* lc, DistCtl* ctl, u32 undiscovered, u64* row,
                                                     u32 ppw_log2, u32 filt_log2, u64 bucket_stride, u32 lag,
-                                                    u64* __restrict__ sent, u64 sent_mask) {
+                                                    u64* __restrict__ sent, u64 sent_mask, u32 rs) {
     constexpr int W = M::W, MW = M::MW, REC = W;
     constexpr int STAGE = 512 / W;          // local new states staged per chunk
-    constexpr int RSTAGE = 2048 / REC;      // remote records staged per chunk (all owners)
-    extern __shared__ u64 filt[];           // 2^filt_log2 fingerprints (dynamic LDS; 0 = no filter)
+    // Dynamic LDS: [filter: 2^filt_log2 fingerprints][record stage: rs x REC words][ranks: rs u16]
+    // [owners: rs u8]. rs (records staged per chunk, all owners) is chosen on the host: 0 with one
+    // partition, so the one-partition launch keeps expand_fast's occupancy.
+    extern __shared__ u64 dyn[];
+    const u32 RSTAGE = rs;
+    u64* filt = dyn;
+    u64* rstage = dyn + (filt_log2 ? (1u << filt_log2) : 0u);
+    u16* rrank = reinterpret_cast<u16*>(rstage + (u64)rs * REC);
+    u8* rown = reinterpret_cast<u8*>(rrank + rs);
     __shared__ u64 stage[STAGE * W];
     __shared__ u64 stage_par[STAGE];
-    __shared__ u64 rstage[RSTAGE * REC];
-    __shared__ u8 rown[RSTAGE];
-    __shared__ u16 rrank[RSTAGE];
     __shared__ u32 ocnt[MAX_PARTS], obase[MAX_PARTS];
     __shared__ u64 pst[4][64 * W];
     __shared__ u64 pmask[4][64 * MW];
@@ -257,7 +261,7 @@ __global__ void __launch_bounds__(256) expand_route(M m, u64* __restrict__ arena
                 u32 rsb = 0;
                 if (lane == rleader) rsb = atomicAdd(&rstage_n, rcnt);
                 rsb = __shfl(rsb, rleader, 64);
-                const u32 rin = rsb >= (u32)RSTAGE ? 0u : min(rcnt, (u32)RSTAGE - rsb);
+                const u32 rin = rsb >= RSTAGE ? 0u : min(rcnt, RSTAGE - rsb);
                 if (rem[j] && rbelow < rin) {
                     const u32 kk = rsb + rbelow;
 #pragma unroll
@@ -292,7 +296,7 @@ __global__ void __launch_bounds__(256) expand_route(M m, u64* __restrict__ arena
         // ---- block flush of the chunk's stages ----
         __syncthreads();
         const u32 nl = min(stage_n, (u32)STAGE);
-        const u32 nr = min(rstage_n, (u32)RSTAGE);
+        const u32 nr = min(rstage_n, RSTAGE);
         for (u32 i = threadIdx.x; i < nr; i += blockDim.x) rrank[i] = (u16)atomicAdd(&ocnt[rown[i]], 1u);
         if (threadIdx.x == 0 && nl) base = atomicAdd(&lc->claims, nl);
         __syncthreads();
