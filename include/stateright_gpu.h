@@ -107,6 +107,7 @@ typedef struct sr_stats {
     uint32_t pipelined;          /* partitioned search: 1 = levels pipelined, no host wait inside */
     uint64_t bucketed_levels;    /* levels expanded by the bucketed path (expand_bucket + bucket_insert) */
     uint64_t records_routed;     /* partitioned search: successor records sent between partitions (all ranks) */
+    uint64_t head_levels;        /* partitioned search: levels run replicated before partitioning */
 } sr_stats;
 
 typedef struct sr_bfs sr_bfs;

@@ -23,14 +23,14 @@ def best(make, reps=5):
     return t * 1e3, c.stats()
 
 
-for rs, filt in [(1024, 9), (2048, 9), (1024, 0), (512, 9)]:
-    os.environ["SR_RSTAGE_WORDS"] = str(rs)
-    os.environ["SR_FILTER_LOG2"] = str(filt)
-    line = [f"rs={rs} filt={filt}:"]
+for head in ["0", "65536"]:
+    os.environ["SR_HEAD_MAX"] = head
+    line = [f"head_max={head}:"]
     for parts in (2, 4, 8):
         ms, st = best(lambda: TwoPhaseSys(n).checker().partitions(parts).capacity_hint(want))
-        line.append(f"T{parts} {ms:.2f}ms rec={st['records_routed'] / 1e6:.1f}M")
+        line.append(f"T{parts} {ms:.2f}ms rec={st['records_routed'] / 1e6:.1f}M head={st['head_levels']} "
+                    f"restarts={st['restarts']}")
     ms, st = best(lambda: TwoPhaseSys(n).checker().comm(comm).capacity_hint(want))
-    line.append(f"rccl1 {ms:.2f}ms")
+    line.append(f"rccl1 {ms:.2f}ms head={st['head_levels']} restarts={st['restarts']}")
     print("  ".join(line), flush=True)
 comm.close()

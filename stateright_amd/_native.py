@@ -52,6 +52,7 @@ class sr_stats(ctypes.Structure):
         ("pipelined", ctypes.c_uint32),
         ("bucketed_levels", ctypes.c_uint64),
         ("records_routed", ctypes.c_uint64),
+        ("head_levels", ctypes.c_uint64),
     ]
 
     def as_dict(self):

@@ -201,6 +201,11 @@ class DistEngine final : public EngineBase {
                 SR_HIP(hipStreamSynchronize(stream_));
                 stats.restarts++;
                 restarts_++;
+                if (head_failed_) {  // the head's scratch buffers were too small: no head
+                    head_ok_ = false;
+                    head_failed_ = false;
+                    continue;
+                }
                 if (lag_) {
                     // the pipelined plan under-estimated a level: rerun with one host
                     // synchronisation per level (exact bucket sizes)
@@ -257,6 +262,7 @@ class DistEngine final : public EngineBase {
     struct DiscAt {
         bool found = false;
         u32 level = 0, part = 0, rank = 0;
+        bool head = false;  // found in the replicated head: rank is in the head arena's level
     };
 
     // ---- exchange ---------------------------------------------------------------------------
@@ -362,6 +368,10 @@ class DistEngine final : public EngineBase {
         const u64 hint = o_.capacity_hint ? o_.capacity_hint : (u64)1 << 22;
         gl_lstart_.assign(T_, {});
         gl_off_.assign(T_, 0);
+        lvl0_ = 0;
+        head_done_ = false;
+        head_undiscovered_ = (1u << M::NPROPS) - 1;
+        const bool use_head = head_max_ > 0 && head_ok_ && T_ > 1;  // one partition: nothing to save
         const u64 per_part = hint / T_ + 1;
 
         // ---- partitions: visited sets, arenas, level 0 ----
@@ -401,6 +411,7 @@ class DistEngine final : public EngineBase {
                 p.sent_mask = sc - 1;
             }
             init_counters(p);
+            if (use_head) continue;  // the replicated head seeds the partitions (run_head)
             insert_roots_part<M><<<1, 64, 0, stream_>>>(p.view(), dinit.p, (u32)k, p.id, T_, p.arena.p, p.apar.p, dn.p, p.lc);
             u32 n0 = 0;
             SR_HIP(hipMemcpyAsync(&n0, dn.p, 4, hipMemcpyDeviceToHost, stream_));
@@ -426,10 +437,11 @@ class DistEngine final : public EngineBase {
         SR_HIP(hipStreamSynchronize(stream_));
         state_count = (u64)k;
         u64 unique_total = 0;
+        if (use_head) run_head(rev, k, unique_total);
         u64 glob_est = 0;  // estimated global frontier size of the level being expanded
         for (auto& p : parts_) glob_est += p.n;  // virtual mode: exact; RCCL: own share
         if (comm_) glob_est *= T_;
-        u32 undiscovered = (1u << M::NPROPS) - 1;
+        u32 undiscovered = head_undiscovered_;
         double ratio = (double)D_;  // non-self-loop successors per parent, last level
         double new_frac = 1.0;      // received records that were new, last level
         double growth = 2.0;        // global frontier growth, last level
@@ -440,8 +452,10 @@ class DistEngine final : public EngineBase {
         // insert_recv and the NEXT level's expand_route are enqueued right after it; the next
         // expand reads its frontier size from the device (DistCtl), so the GPU never waits for
         // the host between the insert and the next expansion.
-        if (lag_) lag_loop(unique_total, undiscovered);
-        else for (u32 level = 0;; ++level) {
+        if (head_done_) {
+            // the replicated head explored everything (or discovered every property)
+        } else if (lag_) lag_loop(unique_total, undiscovered);
+        else for (u32 level = lvl0_;; ++level) {
             // ---- 1. expand + route (grid sized from an upper bound of the frontier) ----
             const u64 d_eff = pessimistic_ ? D_ : std::min<u64>(D_, (u64)std::ceil(1.5 * ratio + 1.0));
             for (auto& p : parts_) {
@@ -501,7 +515,7 @@ class DistEngine final : public EngineBase {
             if (glob_err & ERR_FRONTIER_OVERFLOW) throw Error(SR_ERR_CAPACITY, "frontier or send bucket overflow");
             for (auto& p : parts_) {
                 const u64* row = &all[p.id * RW];
-                if (level > 0) {
+                if (level > lvl0_) {
                     // the frontier just expanded is exact now: what the last insert_recv received new
                     const u64 recv_new = row[T_ + 0] - std::min<u64>(row[T_ + 0], p.local_prev);
                     if (p.nrec_prev) new_frac = std::min(1.0, (double)recv_new / (double)p.nrec_prev);
@@ -510,7 +524,7 @@ class DistEngine final : public EngineBase {
                 p.n = row[T_ + 0];
                 p.lstart.push_back(p.lstart.back() + p.n);  // where the next frontier starts
             }
-            if (level == 0) unique_total = glob_roots;
+            if (level == 0) unique_total = glob_roots;  // (a replicated head sets it instead)
             // discoveries among this level's states: the lowest (partition, rank) per property
             u32 newly = 0;
             for (int pr = 0; pr < M::NPROPS; ++pr) {
@@ -546,7 +560,7 @@ class DistEngine final : public EngineBase {
             }
             prev_glob_n = glob_n;
             if (glob_n == 0) break;  // frontier exhausted everywhere
-            if (level > 0) unique_total += glob_n;  // every state is in exactly one frontier
+            if (level > lvl0_) unique_total += glob_n;  // every state is in exactly one frontier
             max_depth = level;
             unique = unique_total;
             if (M::NPROPS == 0 || (newly && undiscovered == 0)) {
@@ -611,6 +625,130 @@ class DistEngine final : public EngineBase {
     // decision). An under-estimated bucket, arena or table shows up as an error bit in the rows of
     // that level or the next one on every rank, and all ranks restart together in the synchronous
     // mode (`run`).
+    // ---- replicated head -----------------------------------------------------------------------
+    // The first levels are tiny, and partitioning them buys nothing but one all-to-all each. Every
+    // rank (or, with virtual partitions, the process once) runs them as a one-GPU search on a
+    // scratch visited set and a head arena (expand_fast, one host wait per level, no collective):
+    // the counts of a level do not depend on the order inside it, so every rank agrees. When the
+    // next frontier exceeds head_max_ states, each partition takes its owned share: the owned
+    // states of every head level into its visited set, the owned states of the last level as its
+    // first frontier (parent PAR_SEARCH: a path through them searches the head arena).
+    void run_head(const std::vector<u64>& rev, int k, u64& unique_total) {
+        Part& p0 = parts_[0];
+        const u64 cap_states = head_max_ * (u64)(D_ + 4) * 2 + 4096;
+        u64 hcap = 1u << 12;
+        while ((double)hcap * 0.5 < (double)cap_states) hcap <<= 1;
+        if (hkeys_.n < hcap) hkeys_.alloc(o_.device, hcap);
+        if (harena_.n < cap_states * W) {
+            harena_.alloc(o_.device, cap_states * W);
+            hpar_.alloc(o_.device, cap_states);
+        }
+        SR_HIP(hipMemsetAsync(hkeys_.p, 0, hcap * 8, stream_));
+        const TableView hv{hkeys_.p, nullptr, hcap - 1};
+        hlstart_.assign(1, 0);
+        SR_HIP(hipMemcpyAsync(harena_.p, rev.data(), rev.size() * 8, hipMemcpyHostToDevice, stream_));
+        SR_HIP(hipMemsetAsync(hpar_.p, 0xff, (size_t)k * 4, stream_));
+        init_counters(p0);
+        insert_roots<M><<<blocks_for(k, 64), 64, 0, stream_>>>(hv, harena_.p, (u32)k, p0.lc);
+        u32 und = (1u << M::NPROPS) - 1;
+        eval_roots<M><<<blocks_for(k, 64), 64, 0, stream_>>>(m_, harena_.p, (u32)k, p0.lc, und);
+        p0.seq++;
+        publish_kernel<<<1, 64, 0, stream_>>>(p0.lc, p0.hc_dev, p0.seq, 1, nullptr);
+        SR_HIP(hipGetLastError());
+        wait(p0);
+        unique_total = p0.last.claims;
+        u64 n = (u64)k;
+        hlstart_.push_back(n);
+        auto discover = [&](u32 level) {
+            u32 newly = 0;
+            for (int pr = 0; pr < M::NPROPS; ++pr) {
+                if (!(und >> pr & 1) || p0.last.disc[pr] == ~0u) continue;
+                disc_at_[pr] = DiscAt{true, level, 0, p0.last.disc[pr], true};
+                disc[pr].found = true;
+                disc[pr].level = level;
+                disc[pr].rank = p0.last.disc[pr];
+                newly |= 1u << pr;
+            }
+            und &= ~newly;
+            return newly;
+        };
+        u32 newly = discover(0);
+        u32 level = 0;
+        for (;;) {
+            if (M::NPROPS == 0 || (newly && und == 0)) {  // early exit inside the head
+                reference_done = true;
+                early_exit_ = true;
+                head_done_ = true;
+                break;
+            }
+            if (n > head_max_) break;  // this level is partitioned
+            // expand level `level` (n states at hlstart_[level]) into the head arena
+            const u64 fb = hlstart_[level], nb = fb + n;
+            const u32 ncap = (u32)std::min<u64>(cap_states - nb, 0xffffffffu);
+            const u32 ppw_log2 = std::max<u32>(2, std::min<u32>(6, ppw_for(n)));
+            const u32 grid = std::max<u32>(1, blocks_for((n + (1u << ppw_log2) - 1) >> ppw_log2, 4));
+            p0.seq++;
+            expand_fast<M, 1, 0><<<grid, 256, filt_log2_ ? (8u << filt_log2_) : 0u, stream_>>>(
+                m_, harena_.p + fb * W, 0u, (u32)n, hv, harena_.p + nb * W, hpar_.p + nb, ncap, p0.lc, und, p0.hc_dev, p0.seq,
+                1u, ppw_log2, filt_log2_, 0u);
+            SR_HIP(hipGetLastError());
+            wait(p0);
+            if (p0.last.err) {
+                head_failed_ = true;
+                throw Error(SR_ERR_CAPACITY, "replicated head: scratch buffers too small");
+            }
+            state_count += p0.last.successors;
+            stats.successors += p0.last.successors;
+            stats.levels++;
+            const u64 produced = p0.last.claims;
+            if (produced == 0) {  // exhausted inside the head
+                reference_done = true;
+                head_done_ = true;
+                break;
+            }
+            ++level;
+            unique_total += produced;
+            max_depth = level;
+            hlstart_.push_back(nb + produced);
+            head_growth_ = (double)produced / (double)n;
+            head_spp_ = (double)p0.last.successors / (double)n;
+            head_prev_n_ = n;
+            n = produced;
+            newly = discover(level);
+        }
+        head_undiscovered_ = und;
+        unique = unique_total;
+        init_counters(p0);
+        if (head_done_) return;
+        // ---- hand-over: level `level` (n states) is the first partitioned level ----
+        lvl0_ = level;
+        head_n_ = n;
+        const u64 total = hlstart_[level] + n;  // head states, every level
+        DBuf<u32> cnt;
+        cnt.alloc(o_.device, 2);
+        for (auto& p : parts_) {
+            SR_HIP(hipMemsetAsync(cnt.p, 0, 8, stream_));
+            take_owned<M><<<blocks_for(total, 256), 256, 0, stream_>>>(harena_.p, (u32)total, (u32)hlstart_[level], p.id, T_,
+                                                                      p.view(), p.arena.p, p.apar.p, (u32)p.arena_cap, cnt.p,
+                                                                      p.lc);
+            SR_HIP(hipGetLastError());
+            u32 h[2];
+            SR_HIP(hipMemcpyAsync(h, cnt.p, 8, hipMemcpyDeviceToHost, stream_));
+            SR_HIP(hipStreamSynchronize(stream_));
+            if (h[0] > p.arena_cap) throw Error(SR_ERR_CAPACITY, "replicated head: arena of a partition too small");
+            p.n = h[0];
+            p.uniq = h[1];
+            p.n_hi = p.n_est = p.n;
+            DistCtl c0;
+            std::memset(&c0, 0, sizeof(c0));
+            c0.n = h[0];
+            for (int pr = 0; pr < MAX_PROPS; ++pr) c0.disc_prev[pr] = ~0u;  // evaluated in the head
+            SR_HIP(hipMemcpyAsync(p.ctl, &c0, sizeof(c0), hipMemcpyHostToDevice, stream_));
+        }
+        SR_HIP(hipStreamSynchronize(stream_));
+        stats.head_levels = level;
+    }
+
     u64 lag_S(u64 C) const { return DIST_HDR + C * REC; }
 
     void lag_enqueue(u32 level, u64 C, u32 undiscovered, const std::vector<u64>& n_plan) {
@@ -696,13 +834,28 @@ class DistEngine final : public EngineBase {
         double growth = (double)std::min<u32>(D_, 32);  // first levels: no measurement yet
         double pair_ratio = 0.0;
         bool have_rows = false;
+        u64 C0 = cmin;
+        const bool head_start = lvl0_ > 0;
+        if (head_start) {
+            // the head measured the first partitioned level exactly, its growth and its successors
+            // per parent: plan as if its rows had been read
+            for (u32 q = 0; q < T_; ++q) {
+                n_last[q] = head_n_ / T_ + 1;
+                n_hi[q] = (u64)((double)n_last[q] * std::max(1.0, head_growth_) * 2.0) + 64;
+            }
+            growth = head_growth_;
+            pair_ratio = head_spp_ / ((double)T_ * (double)T_);
+            have_rows = true;
+            glob_prev_ = head_prev_n_;  // the level before: the growth of the first rows is measured from it
+            C0 = std::max<u64>(cmin, (u64)(pair_ratio * (double)head_n_ * 1.3) + 256);
+        }
         for (u32 q = 0; q < T_; ++q) n_plan[q] = n_last[q];
-        lag_enqueue(0, cmin, undiscovered, n_plan);
+        lag_enqueue(0, C0, undiscovered, n_plan);
         std::vector<u32> seq0(parts_.size());
         for (size_t i = 0; i < parts_.size(); ++i) seq0[i] = parts_[i].seq;  // level L: seq0 + L
         // Plan and enqueue the next level, `ahead` levels past the last rows read (1 or 2).
-        u32 enq = 1;  // the next level to enqueue
-        u64 C = cmin;
+        u32 enq = lvl0_ + 1;  // the next level to enqueue
+        u64 C = C0;
         auto plan_enqueue = [&](u32 ahead) {
             // growth of the last exact step with a margin (no floor at 1: shrinking tails shrink the
             // buckets too); it compounds once per level of look-ahead
@@ -729,18 +882,18 @@ class DistEngine final : public EngineBase {
             C = have_rows ? std::max<u64>(cmin, (u64)(pair_ratio * (double)glob_fr * 1.15) + 256) : cmin;
             lag_enqueue(enq++, C, undiscovered, n_plan);
         };
-        for (u32 level = 0;; ++level) {
+        for (u32 level = lvl0_;; ++level) {
             // ---- level+1 is enqueued before the rows of `level` are read, unless it is big: then
             // its buckets are planned one level closer (one host round trip, tighter buckets) ----
             u64 glob_last = 0;
             for (u32 q = 0; q < T_; ++q) glob_last += n_last[q];
             const bool big = have_rows && (double)glob_last * growth * growth >= (double)lag_big_;
-            if (enq == level + 1 && !big) plan_enqueue(have_rows ? 2 : 1);
+            if (enq == level + 1 && !big) plan_enqueue(have_rows && !(head_start && level == lvl0_) ? 2 : 1);
 
             // ---- the rows of `level` ----
             const LagPub* pub = nullptr;
             for (size_t i = 0; i < parts_.size(); ++i) {
-                const LagPub* pb = lag_wait(parts_[i], seq0[i] + level);
+                const LagPub* pb = lag_wait(parts_[i], seq0[i] + (level - lvl0_));
                 if (i == 0) pub = pb;
             }
             rows_.assign(pub->rows, pub->rows + RW * T_);
@@ -774,11 +927,11 @@ class DistEngine final : public EngineBase {
                 n_last[q] = nq;
             }
             for (auto& p : parts_) {
-                if (level > 0) p.uniq += n_last[p.id];
+                if (level > lvl0_) p.uniq += n_last[p.id];
                 p.n = n_last[p.id];
                 p.lstart.push_back(p.lstart.back() + p.n);
             }
-            if (level == 0) unique_total = glob_roots;
+            if (level == 0) unique_total = glob_roots;  // (a replicated head sets it instead)
             u32 newly = 0;
             for (int pr = 0; pr < M::NPROPS; ++pr) {
                 if (!(undiscovered >> pr & 1)) continue;
@@ -812,7 +965,7 @@ class DistEngine final : public EngineBase {
             }
             glob_prev_ = glob_n;
             if (glob_n == 0) break;  // frontier exhausted everywhere
-            if (level > 0) unique_total += glob_n;
+            if (level > lvl0_) unique_total += glob_n;
             max_depth = level;
             unique = unique_total;
             if (M::NPROPS == 0 || (newly && undiscovered == 0)) {
@@ -875,15 +1028,29 @@ class DistEngine final : public EngineBase {
         if (pr < 0 || pr >= M::NPROPS || !disc_at_.size() || !disc_at_[pr].found) return false;
         SR_HIP(hipSetDevice(o_.device));
         const DiscAt d = disc_at_[pr];
-        // gid of the discovered state
-        u64 gid = ((u64)d.part << GID_SHIFT) | (part_lstart(d.part, d.level) + d.rank);
         u32 level = d.level;
+        // gid of the discovered state (partitioned levels) or its index in the head arena
+        u64 gid = d.head ? 0 : ((u64)d.part << GID_SHIFT) | (part_lstart(d.part, d.level) + d.rank);
+        bool in_head = d.head;
+        u64 hidx = d.head ? hlstart_[level] + d.rank : 0;
         std::vector<u64> rev;
         DBuf<u64> buf;
         DBuf<unsigned long long> best;
         buf.alloc(o_.device, TREC);
         best.alloc(o_.device, 1);
         for (int guard = 0; guard < (1 << 20); ++guard) {
+            if (in_head) {
+                // the replicated head is local to every rank (no collective)
+                u64 hs[W];
+                u32 prank = 0;
+                SR_HIP(hipMemcpy(hs, harena_.p + hidx * W, W * 8, hipMemcpyDeviceToHost));
+                SR_HIP(hipMemcpy(&prank, hpar_.p + hidx, 4, hipMemcpyDeviceToHost));
+                rev.insert(rev.end(), hs, hs + W);
+                if (level == 0) break;
+                --level;
+                hidx = hlstart_[level] + prank;
+                continue;
+            }
             const u32 owner = (u32)(gid >> GID_SHIFT);
             const u64 idx = gid & (((u64)1 << GID_SHIFT) - 1);
             u64 rec[TREC];
@@ -904,6 +1071,22 @@ class DistEngine final : public EngineBase {
             }
             rev.insert(rev.end(), rec, rec + W);
             if (rec[W] == NONE) break;
+            if (rec[W] == PAR_SEARCH && level == lvl0_ && lvl0_ > 0) {
+                // handed over by the replicated head: a generator in the head's last level
+                const u64 lo = hlstart_[level - 1], n = hlstart_[level] - lo;
+                const unsigned long long init = ~0ull;
+                SR_HIP(hipMemcpyAsync(best.p, &init, 8, hipMemcpyHostToDevice, stream_));
+                find_pred<M><<<blocks_for(n, 256), 256, 0, stream_>>>(m_, harena_.p + lo * W, (u32)n, buf.p, best.p);
+                SR_HIP(hipGetLastError());
+                unsigned long long h = ~0ull;
+                SR_HIP(hipMemcpyAsync(&h, best.p, 8, hipMemcpyDeviceToHost, stream_));
+                SR_HIP(hipStreamSynchronize(stream_));
+                if (h == ~0ull) throw Error(SR_ERR_NONDETERMINISM, "Unable to reconstruct a `Path` into the replicated head");
+                in_head = true;
+                --level;
+                hidx = lo + h;
+                continue;
+            }
             if (rec[W] == PAR_SEARCH) {
                 // inserted from a record: a generator in the previous level, the lowest gid among
                 // every partition's candidates (the same on every rank)
@@ -949,7 +1132,7 @@ class DistEngine final : public EngineBase {
 
     // arena offset of `level` in partition `part`, as known on every rank (lstart of remote
     // partitions is rebuilt from the all-gathered frontier sizes)
-    u64 part_lstart(u32 part, u32 level) { return gl_lstart_[part][level]; }
+    u64 part_lstart(u32 part, u32 level) { return gl_lstart_[part][level - lvl0_]; }
 
     M m_;
     sr_opts o_;
@@ -966,6 +1149,16 @@ class DistEngine final : public EngineBase {
     u32 restarts_ = 0;
     u32 send_cache_max_parts_ = std::getenv("SR_SEND_CACHE") ? (u32)std::atoi(std::getenv("SR_SEND_CACHE")) : 4;
     u64 glob_prev_ = 0;        // pipelined mode: global frontier of the last level read
+    // replicated head (SR_HEAD_MAX: largest head frontier; 0 disables)
+    u64 head_max_ = std::getenv("SR_HEAD_MAX") ? std::strtoull(std::getenv("SR_HEAD_MAX"), nullptr, 10) : 65536;
+    bool head_ok_ = true, head_failed_ = false, head_done_ = false;
+    u32 lvl0_ = 0;                      // first partitioned level
+    u64 head_n_ = 0, head_prev_n_ = 0;  // its global frontier size, and the head's last one
+    double head_growth_ = 1.0, head_spp_ = 1.0;  // last head level: growth, successors per parent
+    u32 head_undiscovered_ = (1u << M::NPROPS) - 1;
+    DBuf<u64> hkeys_, harena_;          // head: scratch visited set, every head level's states
+    DBuf<u32> hpar_;                    // head: parent rank in the previous head level
+    std::vector<u64> hlstart_;          // head arena offset of each head level
     u64 grow_factor_ = 1;
     bool early_exit_ = false;
     std::vector<DiscAt> disc_at_;

@@ -566,6 +566,40 @@ __global__ void insert_roots_part(TableView t, const u64* states, u32 n, u32 my_
     *out_n = k;
 }
 
+// Hand-over from the replicated head: this partition's share of every head state goes into its
+// visited set (cnt[1] = claims) and its share of the last head level [first_front, total) becomes
+// its first frontier (cnt[0] = size; parent PAR_SEARCH). Wave-aggregated counters.
+template <class M>
+__global__ void take_owned(const u64* __restrict__ hstates, u32 total, u32 first_front, u32 my_part, u32 nparts,
+                           TableView t, u64* __restrict__ arena, u64* __restrict__ apar, u32 arena_cap, u32* cnt,
+                           LevelCounters* lc) {
+    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    bool mine = false, nw = false;
+    u64 s[M::W];
+    if (i < total) {
+        load_state<M::W>(hstates, i, s);
+        const u64 fp = fingerprint<M::W>(s);
+        mine = owner_of(fp, nparts) == my_part;
+        if (mine) find_or_claim(t, fp, &nw, &lc->err);
+    }
+    const u64 cm = __ballot(nw);
+    if (cm && lane == __builtin_ctzll(cm)) atomicAdd(&cnt[1], (u32)__popcll(cm));
+    const bool front = mine && i >= first_front;
+    const u64 fm = __ballot(front);
+    if (!fm) return;
+    const int leader = __builtin_ctzll(fm);
+    u32 base = 0;
+    if (lane == leader) base = atomicAdd(&cnt[0], (u32)__popcll(fm));
+    base = __shfl(base, leader, 64);
+    if (!front) return;
+    const u32 pos = base + __popcll(fm & ((1ull << lane) - 1));
+    if (pos < arena_cap) {
+        store_state<M::W>(arena, pos, s);
+        apar[pos] = PAR_SEARCH;
+    }
+}
+
 // Parent search for a state inserted from a record (PAR_SEARCH): the lowest frontier index of
 // level [0, n) of this partition with a successor equal to `target` (within boundary), or ~0.
 template <class M>

@@ -109,3 +109,27 @@ def test_pipelined_and_synchronous_agree(sync, monkeypatch):
     c = sr.IncrementLock(7).checker().partitions(3).spawn_bfs().join()
     assert (c.unique_state_count(), c.state_count(), c.max_depth()) == (o.unique_state_count, o.state_count, o.max_depth)
     assert c.stats()["pipelined"] == (0 if sync else 1)
+
+
+@pytest.mark.parametrize("head", ["0", "64", "65536"])
+@pytest.mark.parametrize("case", [(TWO_PHASE, [5]), (INCREMENT_LOCK, [6]), (LINEAR_EQUATION, [2, 4, 7])], ids=ids)
+def test_replicated_head_counts_and_paths(case, head, monkeypatch):
+    # The replicated head (SR_HEAD_MAX: largest frontier run on every rank before partitioning;
+    # 0 = none): counts equal the oracle's whatever the hand-over level, and discovery paths that
+    # cross from the partitioned levels into the head replay on the CPU model.
+    monkeypatch.setenv("SR_HEAD_MAX", head)
+    model, params = case
+    o = oracle(model, params)
+    c = MODELS[model](params).checker().partitions(3).spawn_bfs().join()
+    assert (c.unique_state_count(), c.state_count(), c.max_depth()) == (o.unique_state_count, o.state_count, o.max_depth)
+    assert sorted(c.discoveries()) == o.discovery_names()
+    props = c.properties()
+    names = [n for n, _ in props]
+    for name, path in c.discoveries().items():
+        r = replay(model, params, path.action_ids, n_props=len(props))
+        assert r is not None  # every action of the path is enabled where it is taken
+        want = 1 if props[names.index(name)][1] == sr.Expectation.Sometimes else 0
+        assert r[1][names.index(name)] == want
+        assert len(path) == len(o.discovery_actions(name))  # a shortest path, as BFS reports
+    if head == "0":
+        assert c.stats()["head_levels"] == 0
