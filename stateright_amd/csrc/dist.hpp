@@ -727,6 +727,10 @@ class DistEngine final : public EngineBase {
         DBuf<u32> cnt;
         cnt.alloc(o_.device, 2);
         for (auto& p : parts_) {
+            // sized from the global head (the same on every rank): a rank-local overflow here would
+            // leave the other ranks waiting in the first all-to-all
+            while ((double)total > 0.5 * (double)p.cap) grow_table(p);
+            ensure_arena(p, n + n / 4 + 4096, 0);
             SR_HIP(hipMemsetAsync(cnt.p, 0, 8, stream_));
             take_owned<M><<<blocks_for(total, 256), 256, 0, stream_>>>(harena_.p, (u32)total, (u32)hlstart_[level], p.id, T_,
                                                                       p.view(), p.arena.p, p.apar.p, (u32)p.arena_cap, cnt.p,

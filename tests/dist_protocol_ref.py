@@ -119,7 +119,7 @@ def partitioned_bfs(n):
     return unique, state_count, depth, len(visited)
 
 
-def pipelined_bfs(n, cmin=8192, big=262144):
+def pipelined_bfs(n, cmin=8192, big=262144, head_max=0):
     """The PIPELINED level loop of dist.hpp (`lag_loop`): one exchange per level of fixed-capacity
     buckets whose header carries the sender's row, planned from rows read one level behind (two
     levels ahead of them), or one level ahead when the level is big. Every decision (bucket
@@ -128,16 +128,46 @@ def pipelined_bfs(n, cmin=8192, big=262144):
     overflow ends the run (the engine then restarts in the synchronous mode)."""
     rank, world = dist.get_rank(), dist.get_world_size()
     visited, frontier = set(), []
-    if owner_of(fingerprint(0), world) == rank:
-        visited.add(0)
-        frontier.append(0)
-    roots = torch.tensor([len(frontier)], dtype=torch.int64)
-    dist.all_reduce(roots)
-    unique, state_count, depth = int(roots), 1, 0
     plan = []
-    n_last = [max(1, int(roots) // world)] * world
-    n_hi = [0] * world
     growth, pair_ratio, have_rows, prev = float(min(2 + 5 * n, 32)), 0.0, False, 0
+    level = 0
+    if head_max:
+        # replicated head (dist.hpp run_head): every rank runs the small levels alone, no exchange
+        seen, cur, state_count, depth, prev_n, spp = {0}, [0], 1, 0, 1, 1.0
+        while len(cur) <= head_max:
+            nxt, succ = [], 0
+            for s in cur:
+                for t in twopc_successors(s, n):
+                    succ += 1
+                    if t not in seen:
+                        seen.add(t)
+                        nxt.append(t)
+            state_count += succ
+            if not nxt:
+                return len(seen), state_count, depth, len([x for x in seen if owner_of(fingerprint(x), world) == rank]), plan
+            spp, prev_n = succ / len(cur), len(cur)
+            cur, level, depth = nxt, level + 1, level + 1
+        # hand-over: owned head states visited, owned last level = first frontier
+        visited = {x for x in seen if owner_of(fingerprint(x), world) == rank}
+        frontier = [x for x in cur if owner_of(fingerprint(x), world) == rank]
+        unique = len(seen)
+        growth, have_rows, prev = len(cur) / prev_n, True, prev_n
+        pair_ratio = spp / (world * world)
+        n_last = [len(cur) // world + 1] * world
+        n_hi = [int(n_last[0] * max(1.0, growth) * 2) + 64] * world
+        caps = {level: max(cmin, int(pair_ratio * len(cur) * 1.3) + 256)}
+        head_levels = level
+    else:
+        if owner_of(fingerprint(0), world) == rank:
+            visited.add(0)
+            frontier.append(0)
+        roots = torch.tensor([len(frontier)], dtype=torch.int64)
+        dist.all_reduce(roots)
+        unique, state_count, depth = int(roots), 1, 0
+        n_last = [max(1, int(roots) // world)] * world
+        n_hi = [0] * world
+        caps = {0: cmin}
+        head_levels = 0
 
     def bucket_cap(ahead):
         g = growth * 1.1
@@ -147,13 +177,12 @@ def pipelined_bfs(n, cmin=8192, big=262144):
             fr += int(c1 * g) if ahead == 2 else c1
         return max(cmin, int(pair_ratio * fr * 1.15) + 256) if have_rows else cmin
 
-    caps = {0: cmin}  # level -> C it runs with
-    level = 0
     while True:
         glob_last = sum(n_last)
         is_big = have_rows and glob_last * growth * growth >= big
         if level + 1 not in caps and not is_big:
-            caps[level + 1] = bucket_cap(2 if have_rows else 1)
+            first_after_head = head_levels and level == head_levels
+            caps[level + 1] = bucket_cap(2 if have_rows and not first_after_head else 1)
         C = caps[level]
         # expand + route into buckets of capacity C (the row rides in every bucket's header)
         buckets = [[] for _ in range(world)]
@@ -206,7 +235,7 @@ def pipelined_bfs(n, cmin=8192, big=262144):
         prev = glob_n
         if glob_n == 0:
             break
-        if level > 0:
+        if level > head_levels:
             unique += glob_n
         depth = level
         state_count += sum(r[world + 1] for r in rows)

@@ -18,13 +18,13 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, n, out, mode="sync", cmin=8192):
+def _worker(rank, world, port, n, out, mode="sync", cmin=8192, head_max=0):
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from dist_protocol_ref import partitioned_bfs, pipelined_bfs
-    out[rank] = partitioned_bfs(n) if mode == "sync" else pipelined_bfs(n, cmin=cmin)
+    out[rank] = partitioned_bfs(n) if mode == "sync" else pipelined_bfs(n, cmin=cmin, head_max=head_max)
     dist.destroy_process_group()
 
 
@@ -68,3 +68,19 @@ def test_two_rank_pipelined_overflow_is_collective():
     mp.spawn(_worker, args=(world, _free_port(), 5, out, "pipelined", 4), nprocs=world, join=True)
     p0, p1 = out[0][4], out[1][4]
     assert p0 == p1 and p0[-1][2]
+
+
+@pytest.mark.parametrize("head_max", [1, 30, 10**6])
+def test_two_rank_pipelined_with_replicated_head(head_max):
+    # The replicated head hands over at different levels (10**6: the whole 2pc N=4 space runs
+    # replicated); counts equal the oracle's and both ranks plan identically.
+    n, world = 4, 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(world, _free_port(), n, out, "pipelined", 8192, head_max), nprocs=world, join=True)
+    o = OracleRun(TWO_PHASE, [n])
+    for r in range(world):
+        unique, state_count, depth, _, plan = out[r]
+        assert (unique, state_count, depth) == (o.unique_state_count, o.state_count, o.max_depth)
+    assert out[0][4] == out[1][4]
+    assert sum(out[r][3] for r in range(world)) == o.unique_state_count
