@@ -921,14 +921,11 @@ class DistEngine final : public EngineBase {
             // one level later, the receiver's) error bit is in these rows on every rank.
             if (glob_err & ERR_TABLE_FULL) throw Error(SR_ERR_CAPACITY, "visited set probe limit exceeded");
             if (glob_err & ERR_FRONTIER_OVERFLOW) throw Error(SR_ERR_CAPACITY, "frontier or send bucket overflow");
-            u64 glob_hi = 0;
             for (u32 q = 0; q < T_; ++q) {
                 u64 r = 0;
                 for (u32 s2 = 0; s2 < T_; ++s2) r += all[s2 * RW + q];
-                const u64 nq = all[q * RW + T_ + 0];
                 n_hi[q] = all[q * RW + T_ + 2] + r;  // upper bound of partition q's next frontier
-                glob_hi += n_hi[q];
-                n_last[q] = nq;
+                n_last[q] = all[q * RW + T_ + 0];
             }
             for (auto& p : parts_) {
                 if (level > lvl0_) p.uniq += n_last[p.id];
@@ -980,7 +977,6 @@ class DistEngine final : public EngineBase {
             state_count += glob_succ;
             stats.successors += glob_succ;
             stats.levels++;
-            (void)glob_hi;
             if (enq == level + 1) plan_enqueue(1);
         }
         SR_HIP(hipStreamSynchronize(stream_));  // the speculative level enqueued past the end
