@@ -472,6 +472,10 @@ class Engine final : public EngineBase {
         u32 sq = next_seq();
         publish_kernel<<<1, 64, 0, stream_>>>(lc_d_, hcd(sq), sq, 1, nullptr);
         SR_HIP(hipGetLastError());
+        // FAST pipelined order: level 0 is enqueued before the host reads the roots' outcome (it is
+        // ignored if the roots already discover every property)
+        const bool pipelined = !fifo_ && !emask_ && !o_.target_state_count && M::NPROPS > 0 && pipeline_;
+        const u32 sq_level0 = pipelined ? launch_sync((u64)k, (1u << M::NPROPS) - 1) : 0u;
         wait_publish(sq);
         state_count = (u64)k;
         unique = lc_.claims;
@@ -481,8 +485,7 @@ class Engine final : public EngineBase {
         u32 level = 0;
         bool order_dependent = false;
         auto t_loop = Clock::now();
-        const bool pipelined = !fifo_ && !emask_ && !o_.target_state_count && M::NPROPS > 0 && pipeline_;
-        if (pipelined) order_dependent = pipeline_levels(n);
+        if (pipelined) order_dependent = pipeline_levels(n, sq_level0);
         else for (;;) {
             // 1. Discoveries among this level's states (evaluated when they were produced).
             u32 newly = 0, max_rank = 0;
@@ -627,7 +630,7 @@ class Engine final : public EngineBase {
     // the visited set or the arena might not hold it (that level is then launched after the wait,
     // sized exactly). A speculative level launched past the end (an exhausted frontier or an early
     // exit) is ignored. Returns whether the run stopped early inside a level.
-    bool pipeline_levels(u64 n) {
+    bool pipeline_levels(u64 n, u32 sq_level0) {
         u32 undiscovered = (1u << M::NPROPS) - 1;
         u32 level = 0;
         bool order_dependent = false;
@@ -649,10 +652,11 @@ class Engine final : public EngineBase {
         if (newly && undiscovered == 0) {
             lvisited_.push_back(max_rank + 1);
             reference_done = true;
+            SR_HIP(hipStreamSynchronize(stream_));  // the level-0 launch is not counted
             fill_discovery_fps();
             return true;
         }
-        u32 sq = launch_sync(n, undiscovered);
+        u32 sq = sq_level0;  // enqueued before the roots' outcome was read
         for (;;) {
             // enqueue the next level before waiting for this one
             const double g = std::max(ratio_, 1.0) * 1.5;
@@ -781,14 +785,21 @@ class Engine final : public EngineBase {
     }
 
     // disc[p].fp from the discovering state in the arena (after the level loop).
+    // The copies are queued together into pinned memory and waited for once (one round trip, not
+    // one blocking copy per property).
     void fill_discovery_fps() {
+        static_assert((size_t)M::NPROPS * W <= Ctx::STAGE_WORDS, "discovery staging");
+        bool any = false;
         for (int p = 0; p < M::NPROPS; ++p) {
             if (!disc[p].found) continue;
-            u64 s[W];
-            SR_HIP(hipMemcpy(s, arena_.p + (lstart_[disc[p].level] + disc[p].rank) * W, W * sizeof(u64),
-                             hipMemcpyDeviceToHost));
-            disc[p].fp = fingerprint<W>(s);
+            SR_HIP(hipMemcpyAsync(ctx_->stage + (size_t)p * W, arena_.p + (lstart_[disc[p].level] + disc[p].rank) * W,
+                                  W * sizeof(u64), hipMemcpyDeviceToHost, stream_));
+            any = true;
         }
+        if (!any) return;
+        SR_HIP(hipStreamSynchronize(stream_));
+        for (int p = 0; p < M::NPROPS; ++p)
+            if (disc[p].found) disc[p].fp = fingerprint<W>(ctx_->stage + (size_t)p * W);
     }
 
     // Smallest 1500-pop block boundary inside this level at which state_count >= target.
