@@ -165,9 +165,11 @@ void sr_gpu_bfs_free(sr_bfs* bfs);
 /* ---- Partitioned search over several GPUs (no counterpart in the reference,
  * which is single-process shared-memory: src/checker/bfs.rs:70-152) ----
  * One process per GPU. Rank 0 creates a unique id, every rank receives it out of band (e.g. a
- * torch.distributed broadcast) and calls sr_dist_init with its rank; RCCL then carries one
- * all-gather and one all-to-all of successor records per BFS level over xGMI. Counts reported by
- * every rank are global. Discovery paths are collective: every rank must call
+ * torch.distributed broadcast) and calls sr_dist_init with its rank. The first small levels run
+ * replicated on every rank with no collective; after them RCCL carries ONE all-to-all of
+ * fixed-capacity buckets of successor records (8*W bytes each, every rank's row in the bucket
+ * headers) per BFS level over xGMI, enqueued without a host wait inside the level.
+ * Counts reported by every rank are global. Discovery paths are collective: every rank must call
  * sr_gpu_bfs_discovery(_path) for the same property in the same order. */
 #define SR_DIST_ID_BYTES 128
 typedef struct sr_dist sr_dist;
