@@ -79,6 +79,11 @@ def cpu_baseline(args):
     }
 
 
+# Random 64-bit atomicCAS into a >= 64 MiB table on MI355X, measured by scripts/microbench_random.hip
+# (profiles/r01_microbench_random_access.txt): the ceiling of the visited-set claims.
+RANDOM_CAS_PEAK = 26.9e9
+
+
 def pmc_traffic(n, world):
     """Beyond-L2 bytes per expand launch from the committed rocprofv3 PMC passes of this bench
     (scripts/pmc_traffic.sh -> profiles/pmc_traffic.json), or None if not measured for this config."""
@@ -87,10 +92,10 @@ def pmc_traffic(n, world):
         with open(path) as f:
             d = json.load(f)
         if d.get("rm_count") == n and d.get("n_gpus", 1) == world:
-            return d["bytes_per_launch"]
+            return d["bytes_per_launch"], d.get("atomics_per_launch")
     except (OSError, ValueError, KeyError):
         pass
-    return None
+    return None, None
 
 
 def main():
@@ -203,7 +208,8 @@ def main():
     if partitioned:
         alg_bytes /= world  # this rank's share of the check's algorithmic bytes
     achieved_gbps = alg_bytes / (kernel_ms * 1e-3) / 1e9 if kernel_ms else 0.0
-    traffic = pmc_traffic(n, world) if args.model == "2pc" else None
+    traffic, atomics = pmc_traffic(n, world) if args.model == "2pc" and not partitioned else (None, None)
+    launch_s = avg_launch_ms * 1e-3
     res = {
         "metric": "unique states/sec (whole node) + HBM GB/s, 2pc N=9 at 1/2/4/8 MI355X",
         "value": unique_total / elapsed,
@@ -235,6 +241,10 @@ def main():
             "unit": "GB/s",
             "frac": achieved_gbps / HBM_PEAK_GBPS,
             "traffic": traffic,
+            # the PMC bytes and memory-side atomics per launch over the event-timed launch duration
+            "traffic_gbps": traffic / launch_s / 1e9 if traffic and launch_s else None,
+            "atomics_per_s": atomics / launch_s if atomics and launch_s else None,
+            "atomics_peak_per_s": RANDOM_CAS_PEAK if atomics else None,
             "avg_launch_ms": avg_launch_ms,
             "launches_per_step": launches / args.steps,
             "algorithmic_bytes_per_step": alg_bytes / args.steps,
