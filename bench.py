@@ -64,12 +64,16 @@ def cpu_baseline(args):
         cmd, what = ["increment_lock", str(min(args.threads, 9))], f"increment_lock N={min(args.threads, 9)}"
     else:
         cmd, what = ["2pc", str(args.cpu_rm_count)], f"2pc N={args.cpu_rm_count}"
-    out = subprocess.run([cli] + cmd + [str(threads)], capture_output=True, text=True,
-                         timeout=600, check=True).stdout
-    m = re.search(r"RESULT state_count=(\d+) unique=(\d+) max_depth=(\d+) threads=(\d+) sec=([\d.e+-]+)", out)
-    sc, uq, _, th, sec = int(m[1]), int(m[2]), int(m[3]), int(m[4]), float(m[5])
+    def timed(t):
+        out = subprocess.run([cli] + cmd + [str(t)], capture_output=True, text=True, timeout=600, check=True).stdout
+        m = re.search(r"RESULT state_count=(\d+) unique=(\d+) max_depth=(\d+) threads=(\d+) sec=([\d.e+-]+)", out)
+        return int(m[1]), int(m[2]), int(m[4]), float(m[5])
+
+    sc, uq, th, sec = timed(threads)
+    _, uq1, _, sec1 = timed(1)  # the reference's default thread_count (src/checker.rs:45)
     return {
         "value": uq / sec,
+        "single_thread_value": uq1 / sec1,
         "unit": "unique states/s",
         "cores": th,
         "kind": "port",
