@@ -390,11 +390,38 @@ struct Paxos {
     SR_HD static u32 hist(const u64* s) { return (u32)(s[0] >> 48); }
     SR_HD static u32 phase(const u64* s, int c) { return (u32)(s[0] >> (px::SBITS + 2 * c) & 3); }
 
-    SR_HD void enabled(const u64* s, u64* m) const {  // every envelope is deliverable (model.rs:238-257)
-        u32 n = 0;
+    // Every envelope is deliverable (model.rs:238-257), but most deliveries are no-ops
+    // (`next_state` = None, src/actor/model.rs:299-301: the actor ignores the message). The mask
+    // keeps the slots whose delivery changes the state: the exact complement of apply's `false`
+    // returns below, so the successors and their slot order are unchanged, and the load-balanced
+    // expansion spends its lanes on real successors only.
+    SR_HD bool delivers(const u64* s, u32 e) const {
+        const u32 dst = px::e_dst(e), kind = px::e_kind(e), bal = px::e_bal(e);
+        if (dst >= 3) {
+            const u32 ph = phase(s, (int)(dst - 3)), req = px::e_req(e);
+            return (ph == 0 && kind == px::PUTOK && req == dst) || (ph == 1 && kind == px::GETOK && req == 2 * dst);
+        }
+        const u64 sw = s[dst] & (dst == 0 ? ((1ull << px::SBITS) - 1) : ~0ull);
+        const u32 sbal = (u32)(sw & 15), sprop = (u32)(sw >> 4 & 7), decided = (u32)(sw >> 41 & 1);
+        if (decided) return kind == px::GET;  // answered with GetOk, the state untouched
+        switch (kind) {
+            case px::PUT: return sprop == 0;
+            case px::PREPARE: return sbal < bal;
+            case px::PREPARED: return bal == sbal;
+            case px::ACCEPT: return !(bal < sbal);
+            case px::ACCEPTED: return bal == sbal;
+            case px::DECIDED: return true;
+            default: return false;
+        }
+    }
+    SR_HD void enabled(const u64* s, u64* m) const {
+        u64 mk = 0;
 #pragma unroll
-        for (int k = 0; k < px::SLOTS; ++k) n += slot(s, k) != px::EMPTY;
-        m[0] = (1ull << n) - 1;
+        for (int k = 0; k < px::SLOTS; ++k) {
+            const u32 e = slot(s, k);
+            if (e != px::EMPTY && delivers(s, e)) mk |= 1ull << k;
+        }
+        m[0] = mk;
     }
 
     // Deliver the a-th envelope (src/actor/model.rs:259-327); false = no-op (None).
