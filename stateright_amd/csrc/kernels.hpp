@@ -27,6 +27,10 @@ constexpr u32 CAND_NONE = 0xffffffffu;
 constexpr int MAX_PROBE = 1 << 16;
 constexpr int MAX_PROPS = 32;
 constexpr int MAX_PARTS = 64;  // visited-set partitions (one per GPU, or virtual ones on one GPU)
+// expand_fast's LDS stage of new states, in 64-bit words (its size sets the blocks per CU).
+#ifndef SR_STAGE_WORDS
+#define SR_STAGE_WORDS 1024
+#endif
 
 enum ErrBits { ERR_TABLE_FULL = 1, ERR_FRONTIER_OVERFLOW = 2 };
 
@@ -304,7 +308,7 @@ __global__ void __launch_bounds__(256) expand_fast(M m, const u64* __restrict__ 
                                                    HostCounters* hc, u32 seq, u32 reset, u32 ppw_log2,
                                                    u32 filt_log2, u32 dev_n) {
     constexpr int W = M::W, MW = M::MW;
-    constexpr int STAGE = 1024 / W;
+    constexpr int STAGE = SR_STAGE_WORDS / W;
     extern __shared__ u64 filt[];       // 2^filt_log2 fingerprints (dynamic LDS; 0 = no filter)
     __shared__ u64 stage[STAGE * W];
     __shared__ u32 stage_par[STAGE];
