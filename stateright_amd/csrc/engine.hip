@@ -95,6 +95,7 @@ class Engine final : public EngineBase {
         if (const char* e = std::getenv("SR_PPW_LOG2")) ppw_env_ = std::atoi(e);
         if (const char* e = std::getenv("SR_FILTER_LOG2")) filt_log2_ = (u32)std::atoi(e);
         if (const char* e = std::getenv("SR_PIPELINE")) pipeline_ = std::atoi(e) != 0;
+        if (const char* e = std::getenv("SR_QUERY_LOG2")) query_mask_ = (1ull << std::atoi(e)) - 1;
     }
     ~Engine() override = default;
 
@@ -391,7 +392,7 @@ class Engine final : public EngineBase {
         volatile u32* flag = &ctx_->hc[seq & 1].seq;
         for (u64 spin = 1;; ++spin) {
             if (*flag == seq) break;
-            if ((spin & 4095) == 0) {
+            if ((spin & query_mask_) == 0) {
                 hipError_t e = hipStreamQuery(stream_);
                 if (e != hipSuccess && e != hipErrorNotReady) SR_HIP(e);
                 if (e == hipSuccess && *flag != seq) {
@@ -936,6 +937,7 @@ class Engine final : public EngineBase {
     int probe_batch_ = 1;
     int probe_load_ = 0;
     int ppw_env_ = -1;
+    u64 query_mask_ = 4095;  // spins between hipStreamQuery calls in wait_publish (SR_QUERY_LOG2)
     bool pipeline_ = true;  // FAST-order level pipelining (SR_PIPELINE=0 disables, for A/B runs)
     u32 filt_log2_ = W >= 4 ? 10 : 9;  // block-local duplicate filter (SR_FILTER_LOG2 sweep in profiles/)
     bool pessimistic_ = false;  // size chunks for max out-degree new states per parent
