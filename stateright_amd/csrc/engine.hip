@@ -96,6 +96,7 @@ class Engine final : public EngineBase {
         if (const char* e = std::getenv("SR_FILTER_LOG2")) filt_log2_ = (u32)std::atoi(e);
         if (const char* e = std::getenv("SR_PIPELINE")) pipeline_ = std::atoi(e) != 0;
         if (const char* e = std::getenv("SR_QUERY_LOG2")) query_mask_ = (1ull << std::atoi(e)) - 1;
+        if (const char* e = std::getenv("SR_GRID_MAX")) grid_max_ = std::max(1, std::atoi(e));
     }
     ~Engine() override = default;
 
@@ -721,6 +722,21 @@ class Engine final : public EngineBase {
         return launch_expand(fbase, (u32)n, false, n, undiscovered);
     }
 
+    // expand_fast's grid is capped at two full residencies of the device (resident blocks per CU
+    // at its LDS footprint x CUs); the kernel strides over any further parents. Whole residencies
+    // avoid a partial last wave of workgroups: 2pc N=9 2.61 -> 2.55 ms per check
+    // (`profiles/r01_grid_sweep.jsonl`; SR_GRID_MAX overrides).
+    u32 expand_grid_cap() {
+        if (grid_max_) return grid_max_;
+        int per_cu = 0, cus = 0;
+        const size_t dyn = filt_log2_ ? (8u << filt_log2_) : 0u;
+        const void* k = probe_batch_ == 2 ? (const void*)expand_fast<M, 2, 0> : (const void*)expand_fast<M, 1, 0>;
+        SR_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 256, dyn));
+        SR_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, o_.device));
+        grid_max_ = per_cu > 0 && cus > 0 ? (u32)(2 * per_cu * cus) : ~0u;
+        return grid_max_;
+    }
+
     // One expand_fast launch over a whole level whose frontier starts at arena offset `fbase`:
     // n states (dev_n = 0), or the previous level's claims read on the device (dev_n = 1, `shape`
     // is then an estimate used only for the launch shape; the grid strides over any excess).
@@ -732,7 +748,7 @@ class Engine final : public EngineBase {
             if (bucket_min_ && shape >= bucket_min_) return launch_bucketed(fbase, n, dev_n, shape, undiscovered, sq, nbase, ncap);
         }
         const u32 ppw_log2 = ppw_env_ >= 0 ? (u32)ppw_env_ : ppw_for(shape);
-        const u32 grid = std::max<u32>(1, blocks_for((shape + (1u << ppw_log2) - 1) >> ppw_log2, 4));
+        const u32 grid = std::min(expand_grid_cap(), std::max<u32>(1, blocks_for((shape + (1u << ppw_log2) - 1) >> ppw_log2, 4)));
         timed([&] {
             auto launch = [&](auto kern) {
                 kern<<<grid, 256, filt_log2_ ? (8u << filt_log2_) : 0u, stream_>>>(
@@ -937,6 +953,7 @@ class Engine final : public EngineBase {
     int probe_batch_ = 1;
     int probe_load_ = 0;
     int ppw_env_ = -1;
+    u32 grid_max_ = 0;       // cap on expand_fast's grid, 0 = two device residencies (SR_GRID_MAX)
     u64 query_mask_ = 4095;  // spins between hipStreamQuery calls in wait_publish (SR_QUERY_LOG2)
     bool pipeline_ = true;  // FAST-order level pipelining (SR_PIPELINE=0 disables, for A/B runs)
     u32 filt_log2_ = W >= 4 ? 10 : 9;  // block-local duplicate filter (SR_FILTER_LOG2 sweep in profiles/)
