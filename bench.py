@@ -8,20 +8,29 @@ set is inside the timed region).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
 
-N > 1 runs under torch.distributed.run, one process per GPU, and partitions ONE check over the
-GPUs: the visited set and frontier are hash-partitioned by fingerprint owner and
-every BFS level does one RCCL all-gather + one all-to-all of successor records over xGMI. The
-workload stays 2pc N=9 at every N ("scaling": "strong"); value = unique states of the check /
+N > 1: one process per GPU. If WORLD_SIZE is not set, this script starts
+`python -m torch.distributed.run --nproc-per-node N ... bench.py ...` as a CHILD process (before
+anything touches the GPU) and exits with its status; under the launcher every rank checks
+WORLD_SIZE == N. The ranks partition ONE check: the visited set and the frontier
+are hash-partitioned by fingerprint owner; after a few replicated head levels, every BFS level does
+ONE RCCL all-to-all of fixed-capacity buckets whose headers carry every rank's row.
+The workload stays 2pc N=9 at every N ("scaling": "strong"); value = unique states of the check /
 max-over-ranks time. `--mode replicas` instead runs an independent full check per GPU.
 
+torch is never imported: the engine library (and with it /opt/rocm's HIP runtime and RCCL, the ones
+it was compiled against) is the only GPU runtime in the process; ranks bootstrap RCCL from the
+launcher's environment (stateright_amd.distributed.Communicator.from_env) and the timing barrier /
+max-over-ranks are the engine's own (sr_dist_barrier, sr_dist_allreduce_f64).
+
 Prints ONE JSON line on rank 0 with `roofline` (dominant kernel = the expand kernel, HIP-event
-timed on its own stream inside the engine) and `cpu_baseline` (the CPU restatement of the
-reference `spawn_bfs`, oracle/bfs_cli, timed on this host's cores on a bounded sample).
+timed on the engine's stream) and, at N=1, `cpu_baseline` (the CPU restatement of the reference
+`spawn_bfs`, oracle/bfs_cli, on the same 2pc N=9 check, host threads and 1 thread).
 """
 import argparse
 import json
 import os
 import re
+import socket
 import subprocess
 import sys
 import time
@@ -30,13 +39,19 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+# Random-access ceilings of the visited set on MI355X, measured by scripts/microbench_random.hip
+# (profiles/r01_microbench_random_access.txt, table 64 MB-2 GB): the 80/20 load/CAS probe mix and
+# random 64-bit atomicCAS.
+PROBE_MIX_PEAK = 49.0e9
+RANDOM_CAS_PEAK = 26.9e9
+BIG_LEVEL_MS = 0.1  # levels whose expand launch takes >= 100 us count as "big"
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--model", default="2pc", choices=["2pc", "paxos", "increment_lock"],
                     help="workload (the BASELINE metric is 2pc; the others are side measurements)")
     ap.add_argument("--rm-count", type=int, default=9)
@@ -44,48 +59,89 @@ def parse():
     ap.add_argument("--threads", type=int, default=10, help="increment_lock thread count")
     ap.add_argument("--order", default="fast", choices=["fast", "fifo"])
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU restatement (rank 0, N=1)")
-    ap.add_argument("--cpu-threads", type=int, default=16, help="host threads for the CPU baseline")
-    ap.add_argument("--cpu-rm-count", type=int, default=8, help="2pc size of the bounded CPU sample")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="host threads for the CPU baseline (0 = usable CPUs)")
     ap.add_argument("--mode", default="partitioned", choices=["partitioned", "replicas", "rccl1"],
                     help="N>1: one check partitioned over the GPUs, or one independent check per GPU; "
                          "rccl1: the partitioned RCCL path on a one-rank communicator (N=1 rehearsal)")
     return ap.parse_args()
 
 
-def cpu_baseline(args):
-    """The oracle's restatement of the multi-threaded reference BFS (oracle/bfs_cli), bounded sample."""
+def launch_ranks(args):
+    """Starts one process per GPU under torch.distributed.run as a child and returns its status."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return subprocess.run(cmd, env=env).returncode
+
+
+def cpu_info():
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = os.cpu_count() or 1
+    try:  # a cgroup CPU quota (the GPU box gives a share of the machine) bounds it further
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            usable = max(1, min(usable, int(int(quota) / int(period))))
+    except (OSError, ValueError):
+        pass
+    return model, os.cpu_count() or 1, usable
+
+
+def cpu_baseline(args, n):
+    """The oracle's restatement of the multi-threaded reference BFS (oracle/bfs_cli) on the SAME
+    check as the GPU line, at the usable host threads and at 1 thread (the reference's default
+    thread_count, src/checker.rs:45)."""
     cli = os.path.join(ROOT, "oracle", "bfs_cli")
     if not os.path.exists(cli):
         subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
-    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    model, nproc, usable = cpu_info()
+    threads = args.cpu_threads or usable
     if args.model == "paxos":
         cmd, what = ["paxos", str(args.clients)], f"paxos C={args.clients}"
     elif args.model == "increment_lock":
         cmd, what = ["increment_lock", str(min(args.threads, 9))], f"increment_lock N={min(args.threads, 9)}"
     else:
-        cmd, what = ["2pc", str(args.cpu_rm_count)], f"2pc N={args.cpu_rm_count}"
+        cmd, what = ["2pc", str(n)], f"2pc N={n}"
+
     def timed(t):
-        out = subprocess.run([cli] + cmd + [str(t)], capture_output=True, text=True, timeout=600, check=True).stdout
+        out = subprocess.run([cli] + cmd + [str(t)], capture_output=True, text=True, timeout=900, check=True).stdout
         m = re.search(r"RESULT state_count=(\d+) unique=(\d+) max_depth=(\d+) threads=(\d+) sec=([\d.e+-]+)", out)
-        return int(m[1]), int(m[2]), int(m[4]), float(m[5])
+        done = next((ln for ln in out.splitlines() if ln.startswith("Done. ")), None)
+        return {"state_count": int(m[1]), "unique": int(m[2]), "threads": int(m[4]), "sec": float(m[5]), "done": done}
 
-    runs = [timed(threads), timed(1)]  # nproc-like threads, and the reference's default thread_count (src/checker.rs:45)
-    sc, uq, th, sec = max(runs, key=lambda r: r[1] / r[3])  # the better of the two is the baseline
+    runs = [timed(threads)] + ([timed(1)] if threads != 1 else [])
+    best = max(runs, key=lambda r: r["unique"] / r["sec"])
     return {
-        "value": uq / sec,
-        "by_threads": {str(r[2]): r[1] / r[3] for r in runs},
+        "value": best["unique"] / best["sec"],
         "unit": "unique states/s",
-        "cores": th,
+        "cores": best["threads"],
         "kind": "port",
-        "sample": f"full {what} check ({uq} unique / {sc} generated states) in {sec:.2f} s "
-                  f"on {th} host threads: C++ restatement of src/checker/bfs.rs (job market, sharded "
-                  f"visited map, shared state_count atomic); the Rust reference cannot be built here",
+        "by_threads": {str(r["threads"]): r["unique"] / r["sec"] for r in runs},
+        "done_lines": {str(r["threads"]): r["done"] for r in runs},
+        "nproc": nproc,
+        "usable_cpus": usable,
+        "cpu_model": model,
+        "sample": f"full {what} check ({best['unique']} unique / {best['state_count']} generated states) in "
+                  f"{best['sec']:.2f} s on {best['threads']} host threads (also timed: "
+                  f"{', '.join(str(r['threads']) for r in runs)} threads): the C++ restatement of "
+                  f"src/checker/bfs.rs (job market, sharded visited map, shared state_count atomic); the Rust "
+                  f"reference cannot be built here (no cargo/rustc)",
     }
-
-
-# Random 64-bit atomicCAS into a >= 64 MiB table on MI355X, measured by scripts/microbench_random.hip
-# (profiles/r01_microbench_random_access.txt): the ceiling of the visited-set claims.
-RANDOM_CAS_PEAK = 26.9e9
 
 
 def pmc_traffic(n, world):
@@ -104,22 +160,27 @@ def pmc_traffic(n, world):
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    import torch
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl")
-    else:
-        torch.cuda.set_device(0)
-    dev = torch.cuda.current_device()
+    if world != args.gpus:
+        raise SystemExit(f"rank {rank}: WORLD_SIZE={world} but --gpus {args.gpus}")
 
     import math
 
     from stateright_amd import IncrementLock, Paxos, TwoPhaseSys
+    from stateright_amd import _native as N
+    lib = N.load()
+    dev = local_rank if world > 1 else 0
+    versions = N.runtime_versions()
+    hip_rt, hip_cc = versions["hip"]
+    rccl_rt, rccl_cc = versions["rccl"]
+    if rccl_rt != rccl_cc or (hip_rt or 0) // 100000 != (hip_cc or 0) // 100000:
+        raise SystemExit(f"runtime skew: engine built against HIP {hip_cc} / RCCL {rccl_cc}, "
+                         f"running HIP {hip_rt} / RCCL {rccl_rt} ({N.loaded_runtime_paths()})")
+
     n = args.rm_count
     if args.model == "paxos":
         make = lambda: Paxos(args.clients)  # noqa: E731
@@ -136,13 +197,20 @@ def main():
         label = f"2pc N={n}"
     partitioned = (world > 1 and args.mode == "partitioned") or args.mode == "rccl1"
     comm = None
-    if partitioned:
+    if world > 1:
         from stateright_amd.distributed import Communicator
-        comm = Communicator.from_torch(device=dev) if world > 1 else Communicator(0, 1, Communicator.unique_id(), dev)
+        comm = Communicator.from_env(device=dev)
+    elif args.mode == "rccl1":
+        from stateright_amd.distributed import Communicator
+        comm = Communicator(0, 1, Communicator.unique_id(), dev)
 
-    def step(profile=False):
+    def step(profile=False, counters=False):
         b = make().checker().capacity_hint(expect_unique).device(dev)
-        b = b.comm(comm) if partitioned else b.order(args.order)
+        if counters:
+            b = b.counters()
+        # the reference's join reconstructs no paths (discoveries() does, bfs.rs:289-298): the
+        # partitioned check skips gathering them at join as well
+        b = b.comm(comm).defer_paths() if partitioned else b.order(args.order)
         if profile:
             b = b.profile()
         c = b.spawn_bfs().join()
@@ -154,9 +222,10 @@ def main():
         step()
 
     def barrier():
-        if dist is not None:
-            dist.barrier()
-        torch.cuda.synchronize()
+        if comm is not None and world > 1:
+            comm.barrier()  # device sync of this rank + collective
+        elif lib.sr_device_synchronize(dev) != 0:
+            raise SystemExit(N.last_error())
 
     # Timed region of `value`: K full checks without per-launch events (a HIP event pair around
     # every level launch adds a marker packet between the kernels: ~7% of a 2pc N=9 check).
@@ -186,34 +255,43 @@ def main():
         last = (c, st)
     barrier()
     profiled_elapsed = time.perf_counter() - t1
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        if partitioned:
-            unique_total = float(unique)  # every rank reports the global count of the shared check
-        else:
-            u = torch.tensor([unique], dtype=torch.float64, device="cuda")
-            dist.all_reduce(u)
-            unique_total = float(u.item())
-    else:
-        unique_total = float(unique)
-
-    if rank != 0:
-        del c
-        if comm is not None:
-            comm.close()
-        if dist is not None:
-            dist.destroy_process_group()
-        return
+    # Counter pass (untimed): visited-set probes and CAS claims per check, from a counting variant
+    # of the expand kernel; the rates divide them by the event-timed kernel time of the pass above.
+    probes = cas = 0
+    for _ in range(args.steps):
+        stc = step(counters=True).stats()
+        probes += stc["probes"]
+        cas += stc["cas"]
+    if world > 1:
+        elapsed = comm.allreduce([elapsed], "max")[0]
+    unique_total = float(unique) if partitioned or world == 1 else float(unique) * world
 
     c, st = last
+    if rank != 0:
+        del c
+        comm.close()
+        return
+
     avg_launch_ms = kernel_ms / max(1, launches)
     if partitioned:
         alg_bytes /= world  # this rank's share of the check's algorithmic bytes
-    achieved_gbps = alg_bytes / (kernel_ms * 1e-3) / 1e9 if kernel_ms else 0.0
+    kernel_s = kernel_ms * 1e-3
+    achieved_gbps = alg_bytes / kernel_s / 1e9 if kernel_ms else 0.0
     traffic, atomics = pmc_traffic(n, world) if args.model == "2pc" and not partitioned else (None, None)
     launch_s = avg_launch_ms * 1e-3
+    probe_rate = probes / kernel_s if kernel_s and probes else None
+    cas_rate = cas / kernel_s if kernel_s and cas else None
+    fracs = {"hbm_bytes": achieved_gbps / HBM_PEAK_GBPS}
+    if probe_rate:
+        fracs["probe_rate"] = probe_rate / PROBE_MIX_PEAK
+    if cas_rate:
+        fracs["cas_rate"] = cas_rate / RANDOM_CAS_PEAK
+    # Per-level split of the last profiled check: big levels, small levels, and the span between
+    # launches (level boundaries: dispatch, ramp/drain, host planning).
+    prof = c.launch_profile() if not partitioned else []
+    big = sum(ms for ms, _ in prof if ms >= BIG_LEVEL_MS)
+    small = sum(ms for ms, _ in prof if ms < BIG_LEVEL_MS)
+    span_ms = st["level_loop_sec"] * 1e3
     res = {
         "metric": "unique states/sec (whole node) + HBM GB/s, 2pc N=9 at 1/2/4/8 MI355X",
         "value": unique_total / elapsed,
@@ -231,13 +309,18 @@ def main():
             "workload": f"{label} spawn_bfs, full check per step ({expect_unique} unique states)",
             "model": args.model,
             "rm_count": n if args.model == "2pc" else None,
-            "order": args.order,
+            "order": "fast" if partitioned else args.order,
             "parallelism": (f"partitioned{world} (RCCL all-to-all per level)" if partitioned else
                             f"replicas{world}" if world > 1 else "1 GPU"),
+            "world_size": world,
+            "comm": comm.kind() if comm is not None else None,
+            "rccl_nranks": comm.nranks() if comm is not None else None,
         },
-        "state_count_per_sec": float(c.state_count()) * world * args.steps / elapsed,
+        "state_count_per_sec": float(c.state_count()) * (1 if partitioned else world) * args.steps / elapsed,
         "roofline": {
             "bound": "hbm",
+            "limiter": max(fracs, key=fracs.get),
+            "fractions": fracs,
             "kernel": ("expand_route" if partitioned else "expand_fast") +
                       " (expand + fingerprint + visited-set probe/claim + append + properties)",
             "achieved": achieved_gbps,
@@ -245,28 +328,42 @@ def main():
             "unit": "GB/s",
             "frac": achieved_gbps / HBM_PEAK_GBPS,
             "traffic": traffic,
-            # the PMC bytes and memory-side atomics per launch over the event-timed launch duration
+            # the random-transaction view: visited-set probes and claims per second of kernel time
+            # (device counters), against the microbenchmarked ceilings
+            "probe_rate": probe_rate,
+            "probe_peak": PROBE_MIX_PEAK if probe_rate else None,
+            "cas_rate": cas_rate,
+            "cas_peak": RANDOM_CAS_PEAK if cas_rate else None,
+            "probes_per_step": probes / args.steps,
             "traffic_gbps": traffic / launch_s / 1e9 if traffic and launch_s else None,
             "atomics_per_s": atomics / launch_s if atomics and launch_s else None,
-            "atomics_peak_per_s": RANDOM_CAS_PEAK if atomics else None,
             "avg_launch_ms": avg_launch_ms,
             "launches_per_step": launches / args.steps,
             "algorithmic_bytes_per_step": alg_bytes / args.steps,
             "profiled_ms_per_step": profiled_elapsed / args.steps * 1e3,
         },
+        "levels": {
+            "span_ms": span_ms,
+            "big_levels_ms": big,
+            "big_levels": sum(1 for ms, _ in prof if ms >= BIG_LEVEL_MS),
+            "small_levels_ms": small,
+            "small_levels": sum(1 for ms, _ in prof if ms < BIG_LEVEL_MS),
+            "gaps_ms": max(0.0, span_ms - big - small) if prof else None,
+            "kernel_us": [round(ms * 1e3, 1) for ms, _ in prof],
+            "frontier": [fr for _, fr in prof],
+        } if prof else None,
         "engine": {k: st[k] for k in ("levels", "table_capacity", "rehashes", "level_loop_sec", "total_sec",
-                                      "restarts", "pipelined", "records_routed")},
+                                      "restarts", "pipelined", "records_routed", "head_levels")},
+        "runtime": {"hip": versions["hip"], "rccl": versions["rccl"], "libs": N.loaded_runtime_paths()},
     }
     if args.cpu_baseline and world == 1:
         try:
-            res["cpu_baseline"] = cpu_baseline(args)
+            res["cpu_baseline"] = cpu_baseline(args, n)
         except Exception as e:  # the GPU number stands on its own
             res["cpu_baseline"] = {"error": str(e)}
-    print(json.dumps(res))
+    print(json.dumps(res), flush=True)
     if comm is not None:
         comm.close()
-    if dist is not None:
-        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -87,6 +87,15 @@ typedef struct sr_opts {
     uint64_t capacity_hint;      /* expected unique states; 0 = grow the visited table on demand */
     int32_t profile;             /* time every expand launch with HIP events                     */
     int32_t verbose;             /* per-level log lines on stderr                                */
+    int32_t counters;            /* count visited-set probes and CAS attempts (sr_stats.probes/cas)
+                                    with a counting variant of the expand kernel (slower)        */
+    int32_t defer_paths;         /* partitioned search: 0 = at join, every rank gathers the states
+                                    of every discovery path (collectively), so sr_gpu_bfs_discovery*
+                                    work on any single rank afterwards; 1 = skip that at join and
+                                    reconstruct on demand (then collective: every rank must call
+                                    sr_gpu_bfs_discovery* for the same property in the same order).
+                                    The reference's join reconstructs nothing either
+                                    (src/checker/bfs.rs:289-298 builds paths in discoveries()). */
 } sr_opts;
 
 /* Timing/throughput counters of a finished run (sr_gpu_bfs_stats). */
@@ -108,6 +117,8 @@ typedef struct sr_stats {
     uint64_t bucketed_levels;    /* levels expanded by the bucketed path (expand_bucket + bucket_insert) */
     uint64_t records_routed;     /* partitioned search: successor records sent between partitions (all ranks) */
     uint64_t head_levels;        /* partitioned search: levels run replicated before partitioning */
+    uint64_t probes;             /* visited-set slots loaded by the expand kernels (first probe + linear steps) */
+    uint64_t cas;                /* 64-bit atomicCAS claims attempted on the visited set */
 } sr_stats;
 
 typedef struct sr_bfs sr_bfs;
@@ -126,6 +137,10 @@ uint64_t sr_gpu_bfs_state_count(const sr_bfs* bfs);
 uint64_t sr_gpu_bfs_unique_state_count(const sr_bfs* bfs);
 uint32_t sr_gpu_bfs_max_depth(const sr_bfs* bfs);
 int32_t sr_gpu_bfs_stats(const sr_bfs* bfs, sr_stats* out);
+/* profile=1: HIP-event duration (ms) of every expand launch in launch order and the frontier size
+ * it expanded (0 if unknown); returns the number of launches (FAST pipelined order: launch i
+ * expands level i, a last launch past the end expands nothing). */
+int64_t sr_gpu_bfs_launch_profile(const sr_bfs* bfs, double* kernel_ms, uint64_t* frontier, int64_t cap);
 
 int32_t sr_gpu_bfs_property_count(const sr_bfs* bfs);
 /* Copies the property name (NUL-terminated) and its expectation; returns the name length. */
@@ -169,13 +184,36 @@ void sr_gpu_bfs_free(sr_bfs* bfs);
  * replicated on every rank with no collective; after them RCCL carries ONE all-to-all of
  * fixed-capacity buckets of successor records (8*W bytes each, every rank's row in the bucket
  * headers) per BFS level over xGMI, enqueued without a host wait inside the level.
- * Counts reported by every rank are global. Discovery paths are collective: every rank must call
- * sr_gpu_bfs_discovery(_path) for the same property in the same order. */
+ * Counts reported by every rank are global. Discovery paths are gathered on every rank at join
+ * (sr_opts.defer_paths = 0, the default), so any rank may ask for them alone. */
 #define SR_DIST_ID_BYTES 128
 typedef struct sr_dist sr_dist;
 int32_t sr_dist_unique_id(uint8_t* id_out);
+/* An RCCL communicator (one process per GPU). */
 sr_dist* sr_dist_init(int32_t rank, int32_t world, const uint8_t* id, int32_t device);
+/* `world` communicators whose ranks are threads of THIS process (rank r on devices[r], or device 0
+ * when devices is NULL): the same stream-ordered collectives as RCCL, carried by device copies
+ * across the ranks' streams, with a host rendezvous per call that rejects ranks issuing different
+ * collectives. Runs the partitioned engine's multi-rank code path on one GPU (tests). */
+int32_t sr_dist_local_group(int32_t world, const int32_t* devices, sr_dist** comms_out);
+int32_t sr_dist_rank(const sr_dist* comm);
+int32_t sr_dist_world(const sr_dist* comm);
+/* Ranks the transport reports (RCCL: ncclCommCount). */
+int32_t sr_dist_nranks(const sr_dist* comm);
+/* "rccl" or "local". */
+int32_t sr_dist_kind(const sr_dist* comm, char* buf, int32_t cap);
+/* Device synchronisation of this rank, then a collective barrier (bench timing brackets). */
+int32_t sr_dist_barrier(sr_dist* comm);
+/* Element-wise min (op 0) or max (op 1) of n doubles over the ranks, in place. */
+int32_t sr_dist_allreduce_f64(sr_dist* comm, double* values, int32_t n, int32_t op);
 void sr_dist_free(sr_dist* comm);
+
+/* Versions: runtime = what the loaded library reports, compiled = the headers the engine was built
+ * against (RCCL: NCCL_VERSION_CODE; HIP: HIP_VERSION). A mismatch means another process-wide copy
+ * of the runtime (e.g. one bundled with a Python framework) was loaded first. */
+int32_t sr_rccl_version(int32_t* runtime, int32_t* compiled);
+int32_t sr_hip_runtime_version(int32_t* runtime, int32_t* compiled);
+int32_t sr_device_synchronize(int32_t device);
 /* comm == NULL: `virtual_partitions` partitions in this process on opts->device (same protocol,
  * device-copy exchange). FAST order only. */
 sr_bfs* sr_gpu_bfs_spawn_partitioned(sr_dist* comm, int32_t virtual_partitions, int32_t model_id,

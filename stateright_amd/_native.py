@@ -32,6 +32,8 @@ class sr_opts(ctypes.Structure):
         ("capacity_hint", ctypes.c_uint64),
         ("profile", ctypes.c_int32),
         ("verbose", ctypes.c_int32),
+        ("counters", ctypes.c_int32),
+        ("defer_paths", ctypes.c_int32),
     ]
 
 
@@ -53,6 +55,8 @@ class sr_stats(ctypes.Structure):
         ("bucketed_levels", ctypes.c_uint64),
         ("records_routed", ctypes.c_uint64),
         ("head_levels", ctypes.c_uint64),
+        ("probes", ctypes.c_uint64),
+        ("cas", ctypes.c_uint64),
     ]
 
     def as_dict(self):
@@ -74,6 +78,8 @@ SIGNATURES = [
     ("sr_gpu_bfs_unique_state_count", ctypes.c_uint64, [_P]),
     ("sr_gpu_bfs_max_depth", ctypes.c_uint32, [_P]),
     ("sr_gpu_bfs_stats", ctypes.c_int32, [_P, ctypes.POINTER(sr_stats)]),
+    ("sr_gpu_bfs_launch_profile", ctypes.c_int64, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64),
+                                                   ctypes.c_int64]),
     ("sr_gpu_bfs_property_count", ctypes.c_int32, [_P]),
     ("sr_gpu_bfs_property", ctypes.c_int32, [_P, ctypes.c_int32, ctypes.c_char_p, ctypes.c_int32,
                                              ctypes.POINTER(ctypes.c_int32)]),
@@ -90,7 +96,17 @@ SIGNATURES = [
     ("sr_gpu_bfs_free", None, [_P]),
     ("sr_dist_unique_id", ctypes.c_int32, [ctypes.c_char_p]),
     ("sr_dist_init", _P, [ctypes.c_int32, ctypes.c_int32, ctypes.c_char_p, ctypes.c_int32]),
+    ("sr_dist_local_group", ctypes.c_int32, [ctypes.c_int32, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(_P)]),
+    ("sr_dist_rank", ctypes.c_int32, [_P]),
+    ("sr_dist_world", ctypes.c_int32, [_P]),
+    ("sr_dist_nranks", ctypes.c_int32, [_P]),
+    ("sr_dist_kind", ctypes.c_int32, [_P, ctypes.c_char_p, ctypes.c_int32]),
+    ("sr_dist_barrier", ctypes.c_int32, [_P]),
+    ("sr_dist_allreduce_f64", ctypes.c_int32, [_P, ctypes.POINTER(ctypes.c_double), ctypes.c_int32, ctypes.c_int32]),
     ("sr_dist_free", None, [_P]),
+    ("sr_rccl_version", ctypes.c_int32, [ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32)]),
+    ("sr_hip_runtime_version", ctypes.c_int32, [ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32)]),
+    ("sr_device_synchronize", ctypes.c_int32, [ctypes.c_int32]),
     ("sr_gpu_bfs_spawn_partitioned", _P, [_P, ctypes.c_int32, ctypes.c_int32, _I64P, ctypes.c_int32,
                                           ctypes.POINTER(sr_opts)]),
 ]
@@ -119,3 +135,27 @@ def load():
 
 def last_error():
     return load().sr_last_error().decode(errors="replace")
+
+
+def runtime_versions():
+    """{"hip": (runtime, compiled), "rccl": (runtime, compiled)} as the engine library sees them."""
+    lib = load()
+    out = {}
+    for key, fn in (("hip", lib.sr_hip_runtime_version), ("rccl", lib.sr_rccl_version)):
+        r, c = ctypes.c_int32(), ctypes.c_int32()
+        out[key] = (r.value, c.value) if fn(ctypes.byref(r), ctypes.byref(c)) == 0 else (None, None)
+    return out
+
+
+def loaded_runtime_paths():
+    """Paths of the HIP runtime and RCCL libraries mapped into this process (Linux)."""
+    paths = set()
+    try:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                p = line.split()[-1] if line.count(" ") >= 5 else ""
+                if "libamdhip64" in p or "librccl" in p:
+                    paths.add(p)
+    except OSError:
+        pass
+    return sorted(paths)

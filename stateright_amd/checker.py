@@ -167,6 +167,18 @@ class CheckerBuilder:
         self._comm = communicator
         return self
 
+    def defer_paths(self, on=True):
+        """Partitioned search: skip gathering the discovery paths at join (they are then built on
+        demand, collectively: every rank must ask for the same property in the same order)."""
+        self._opts.defer_paths = int(bool(on))
+        return self
+
+    def counters(self, on=True):
+        """Count visited-set probes and CAS claims (stats()["probes"], ["cas"]) with a counting
+        variant of the expand kernel (slower; for measurement passes only)."""
+        self._opts.counters = int(bool(on))
+        return self
+
     def profile(self, on=True):
         self._opts.profile = int(bool(on))
         return self
@@ -367,6 +379,14 @@ class GpuBfsChecker:
         s = N.sr_stats()
         self._lib.sr_gpu_bfs_stats(self._h, ctypes.byref(s))
         return s.as_dict()
+
+    def launch_profile(self):
+        """profile(): [(kernel_ms, frontier)] of every expand launch, in launch order."""
+        n = self._lib.sr_gpu_bfs_launch_profile(self._h, None, None, 0)
+        ms = (ctypes.c_double * max(1, n))()
+        fr = (ctypes.c_uint64 * max(1, n))()
+        self._lib.sr_gpu_bfs_launch_profile(self._h, ms, fr, n)
+        return [(ms[i], fr[i]) for i in range(n)]
 
     # --- report / asserts (src/checker.rs:216-337) ---------------------------------------------
     def discovery_classification(self, name):

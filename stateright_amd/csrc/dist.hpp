@@ -31,9 +31,25 @@
 #pragma once
 #include <rccl/rccl.h>
 
+#include <condition_variable>
+#include <memory>
+#include <mutex>
+
 #include "kernels_dist.hpp"
 
 namespace sr {
+
+// Element-wise reduction of `rows` vectors of n words (rows x n, row-major) into out.
+__global__ void reduce_rows(const u64* in, u32 rows, u64 n, u32 op, u64* out) {
+    const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    u64 v = in[i];
+    for (u32 r = 1; r < rows; ++r) {
+        const u64 x = in[(u64)r * n + i];
+        v = op == 0 ? (x < v ? x : v) : op == 1 ? (x > v ? x : v) : v + x;
+    }
+    out[i] = v;
+}
 
 #define SR_NCCL(expr)                                                                         \
     do {                                                                                      \
@@ -42,9 +58,214 @@ namespace sr {
             throw ::sr::Error(SR_ERR_HIP, std::string(#expr) + ": " + ncclGetErrorString(r_)); \
     } while (0)
 
+// The collectives the partitioned level loop issues, stream-ordered like RCCL's (every rank issues
+// the same sequence; a call returns once its work is ENQUEUED on `s`).
+//   all_to_all   count words from send[q*count] to rank q's recv[me*count]
+//   all_gather   count words from every rank into all[q*count]
+//   exchange     grouped point-to-point of per-peer spans (the synchronous mode's exact sizes)
+//   broadcast    count words of root's buf to every rank's buf
+//   all_reduce   element-wise min / max / sum of count u64 words
+enum class RedOp { Min, Max, Sum };
 struct Comm {
     int rank = 0, world = 1, device = 0;
+    virtual ~Comm() = default;
+    virtual const char* kind() const = 0;
+    virtual int nranks() const = 0;  // ranks the transport itself reports (RCCL: ncclCommCount)
+    virtual void all_to_all(const u64* send, u64* recv, u64 count, hipStream_t s) = 0;
+    virtual void all_gather(const u64* mine, u64* all, u64 count, hipStream_t s) = 0;
+    virtual void exchange(const std::vector<const u64*>& send, const std::vector<u64>& scount,
+                          const std::vector<u64*>& recv, const std::vector<u64>& rcount, hipStream_t s) = 0;
+    virtual void broadcast(u64* buf, u64 count, int root, hipStream_t s) = 0;
+    virtual void all_reduce(u64* buf, u64 count, RedOp op, hipStream_t s) = 0;
+    // Host barrier (bench timing): every rank's device work issued so far on `s` is finished.
+    void barrier(hipStream_t s) {
+        DBuf<u64> one;
+        one.alloc(device, 1);
+        SR_HIP(hipMemsetAsync(one.p, 0, 8, s));
+        all_reduce(one.p, 1, RedOp::Sum, s);
+        SR_HIP(hipStreamSynchronize(s));
+    }
+};
+
+// One process per GPU over RCCL (xGMI).
+struct RcclComm final : Comm {
     ncclComm_t nccl = nullptr;
+    ~RcclComm() override {
+        if (nccl) (void)ncclCommDestroy(nccl);
+    }
+    const char* kind() const override { return "rccl"; }
+    int nranks() const override {
+        int n = 0;
+        if (ncclCommCount(nccl, &n) != ncclSuccess) return -1;
+        return n;
+    }
+    void all_to_all(const u64* send, u64* recv, u64 count, hipStream_t s) override {
+        SR_NCCL(ncclAllToAll(send, recv, count, ncclUint64, nccl, s));
+    }
+    void all_gather(const u64* mine, u64* all, u64 count, hipStream_t s) override {
+        SR_NCCL(ncclAllGather(mine, all, count, ncclUint64, nccl, s));
+    }
+    void exchange(const std::vector<const u64*>& send, const std::vector<u64>& scount, const std::vector<u64*>& recv,
+                  const std::vector<u64>& rcount, hipStream_t s) override {
+        SR_NCCL(ncclGroupStart());
+        for (int peer = 0; peer < world; ++peer) {
+            if (peer == rank) {
+                if (scount[peer]) SR_HIP(hipMemcpyAsync(recv[peer], send[peer], scount[peer] * 8, hipMemcpyDeviceToDevice, s));
+                continue;
+            }
+            if (scount[peer]) SR_NCCL(ncclSend(send[peer], scount[peer], ncclUint64, peer, nccl, s));
+            if (rcount[peer]) SR_NCCL(ncclRecv(recv[peer], rcount[peer], ncclUint64, peer, nccl, s));
+        }
+        SR_NCCL(ncclGroupEnd());
+    }
+    void broadcast(u64* buf, u64 count, int root, hipStream_t s) override {
+        SR_NCCL(ncclBroadcast(buf, buf, count, ncclUint64, root, nccl, s));
+    }
+    void all_reduce(u64* buf, u64 count, RedOp op, hipStream_t s) override {
+        const ncclRedOp_t o = op == RedOp::Min ? ncclMin : op == RedOp::Max ? ncclMax : ncclSum;
+        SR_NCCL(ncclAllReduce(buf, buf, count, ncclUint64, o, nccl, s));
+    }
+};
+
+// Ranks that are threads of ONE process (each with its own driver thread, stream and device).
+// Collectives keep RCCL's contract: a call is stream-ordered on the caller's stream, every rank
+// issues the same sequence, and a call only ENQUEUES work. The ranks meet on a host barrier at
+// each call (which also checks that they issue the same collective with the same size: a
+// mismatch, which would hang RCCL, raises on every rank), and the data moves by device copies
+// ordered with HIP events across the ranks' streams. This runs the partitioned engine's real
+// multi-rank code (rank-local partitions, every collective in its order) on one GPU.
+struct LocalGroup {
+    explicit LocalGroup(int w) : world(w), slots(w), ready(w, nullptr), done(w, nullptr) {}
+    ~LocalGroup() {
+        for (auto e : ready)
+            if (e) (void)hipEventDestroy(e);
+        for (auto e : done)
+            if (e) (void)hipEventDestroy(e);
+    }
+    struct Slot {
+        int op = 0;
+        u64 count = 0;
+        const u64* send = nullptr;
+        const std::vector<const u64*>* sends = nullptr;
+        const std::vector<u64>* scount = nullptr;
+        int root = 0;
+    };
+    const int world;
+    std::vector<Slot> slots;
+    std::vector<hipEvent_t> ready, done;
+    std::mutex mu;
+    std::condition_variable cv;
+    int arrived = 0;
+    u64 generation = 0;
+
+    // All ranks arrive; false on timeout (a rank issued a different collective sequence, or failed).
+    bool barrier() {
+        std::unique_lock<std::mutex> g(mu);
+        const u64 gen = generation;
+        if (++arrived == world) {
+            arrived = 0;
+            ++generation;
+            cv.notify_all();
+            return true;
+        }
+        return cv.wait_for(g, std::chrono::seconds(60), [&] { return generation != gen; });
+    }
+};
+
+struct LocalComm final : Comm {
+    std::shared_ptr<LocalGroup> g;
+    const char* kind() const override { return "local"; }
+    int nranks() const override { return g->world; }
+
+    enum Op { A2A = 1, AGATHER, EXCH, BCAST, RMIN, RMAX, RSUM };
+
+    // Phase 1: publish this rank's call and a "ready" event (its inputs are written once the
+    // stream reaches it); every rank checks that all ranks issued the same call, then orders its
+    // stream after every rank's ready event.
+    void arrive(int op, u64 count, const u64* send, hipStream_t s, int root = 0,
+                const std::vector<const u64*>* sends = nullptr, const std::vector<u64>* scount = nullptr) {
+        SR_HIP(hipSetDevice(device));
+        if (!g->ready[rank]) {
+            SR_HIP(hipEventCreateWithFlags(&g->ready[rank], hipEventDisableTiming));
+            SR_HIP(hipEventCreateWithFlags(&g->done[rank], hipEventDisableTiming));
+        }
+        auto& sl = g->slots[rank];
+        sl.op = op;
+        sl.count = count;
+        sl.send = send;
+        sl.root = root;
+        sl.sends = sends;
+        sl.scount = scount;
+        SR_HIP(hipEventRecord(g->ready[rank], s));
+        sync("arrive");
+        for (int q = 0; q < world; ++q) {
+            const auto& o = g->slots[q];
+            if (o.op != op || o.count != count || o.root != root)
+                throw Error(SR_ERR_HIP, "local collective mismatch: rank " + std::to_string(q) + " issued op " +
+                                            std::to_string(o.op) + " of " + std::to_string(o.count) + " words, rank " +
+                                            std::to_string(rank) + " op " + std::to_string(op) + " of " +
+                                            std::to_string(count));
+        }
+        for (int q = 0; q < world; ++q) SR_HIP(hipStreamWaitEvent(s, g->ready[q], 0));
+    }
+    // Phase 2, after this rank's reads are enqueued: no rank may overwrite an input before every
+    // rank has read it, and no slot or event is reused before every rank has waited on it.
+    void leave(hipStream_t s) {
+        SR_HIP(hipEventRecord(g->done[rank], s));
+        sync("reads");
+        for (int q = 0; q < world; ++q) SR_HIP(hipStreamWaitEvent(s, g->done[q], 0));
+        sync("leave");
+    }
+    void sync(const char* where) {
+        if (!g->barrier())
+            throw Error(SR_ERR_HIP, std::string("local collective: ranks did not meet (") + where +
+                                        "): a rank issued a different sequence or failed");
+    }
+    void copy(void* dst, const void* src, u64 bytes, hipStream_t s) {
+        if (bytes) SR_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, s));
+    }
+
+    void all_to_all(const u64* send, u64* recv, u64 count, hipStream_t s) override {
+        arrive(A2A, count, send, s);
+        for (int q = 0; q < world; ++q) copy(recv + (u64)q * count, g->slots[q].send + (u64)rank * count, count * 8, s);
+        leave(s);
+    }
+    void all_gather(const u64* mine, u64* all, u64 count, hipStream_t s) override {
+        arrive(AGATHER, count, mine, s);
+        for (int q = 0; q < world; ++q) copy(all + (u64)q * count, g->slots[q].send, count * 8, s);
+        leave(s);
+    }
+    void exchange(const std::vector<const u64*>& send, const std::vector<u64>& scount, const std::vector<u64*>& recv,
+                  const std::vector<u64>& rcount, hipStream_t s) override {
+        arrive(EXCH, 0, nullptr, s, 0, &send, &scount);
+        for (int q = 0; q < world; ++q) {
+            const u64 c = (*g->slots[q].scount)[rank];
+            if (c != rcount[q])
+                throw Error(SR_ERR_HIP, "local exchange: rank " + std::to_string(q) + " sends " + std::to_string(c) +
+                                            " words, rank " + std::to_string(rank) + " expects " + std::to_string(rcount[q]));
+            copy(recv[q], (*g->slots[q].sends)[rank], c * 8, s);
+        }
+        leave(s);
+    }
+    void broadcast(u64* buf, u64 count, int root, hipStream_t s) override {
+        DBuf<u64> tmp;  // the root's buffer is source and destination: copy through scratch
+        tmp.alloc(device, count);
+        arrive(BCAST, count, buf, s, root);
+        copy(tmp.p, g->slots[root].send, count * 8, s);
+        leave(s);
+        copy(buf, tmp.p, count * 8, s);
+        SR_HIP(hipStreamSynchronize(s));  // tmp returns to the pool at scope exit
+    }
+    void all_reduce(u64* buf, u64 count, RedOp op, hipStream_t s) override {
+        DBuf<u64> all;  // every rank's vector, reduced locally on the device
+        all.alloc(device, count * world);
+        arrive(op == RedOp::Min ? RMIN : op == RedOp::Max ? RMAX : RSUM, count, buf, s);
+        for (int q = 0; q < world; ++q) copy(all.p + (u64)q * count, g->slots[q].send, count * 8, s);
+        leave(s);
+        reduce_rows<<<blocks_for(count, 256), 256, 0, s>>>(all.p, (u32)world, count, (u32)op, buf);
+        SR_HIP(hipGetLastError());
+        SR_HIP(hipStreamSynchronize(s));  // `all` returns to the pool at scope exit
+    }
 };
 
 // Per-device resources of the partitioned engine, pooled across checks like the single-GPU
@@ -195,6 +416,7 @@ class DistEngine final : public EngineBase {
         for (int attempt = 0;; ++attempt) {
             try {
                 run_once();
+                gather_paths();
                 return;
             } catch (const Error& e) {
                 if (e.code != SR_ERR_CAPACITY || attempt >= 3) throw;
@@ -220,18 +442,57 @@ class DistEngine final : public EngineBase {
         }
     }
 
-    // `reconstruct_path` across partitions: walk parent gids (collective in the RCCL mode: every
-    // rank must call it).
+    // Every discovery path, gathered on every rank at the end of the run (one collective walk per
+    // discovered property, in property order: `disc_at_` is the same on every rank), so that a
+    // single rank may ask for a path later. Deferred (sr_opts.defer_paths) paths are walked on
+    // demand, collectively.
+    void gather_paths() {
+        paths_.assign(M::NPROPS, {});
+        paths_ready_ = false;
+        if (o_.defer_paths || !comm_) return;  // virtual partitions walk on demand, locally
+        for (int p = 0; p < M::NPROPS; ++p) {
+            if (!disc_at_[p].found) continue;
+            tree_path(p, paths_[p]);
+            // A walk through the replicated head is local to each rank, whose head arena holds
+            // each level in its own (FAST) order: every rank's path is valid, but they may differ.
+            // Rank 0's path goes to every rank, so that all report the same one.
+            DBuf<u64> buf;
+            buf.alloc(o_.device, 1);
+            u64 len = paths_[p].size();
+            SR_HIP(hipMemcpyAsync(buf.p, &len, 8, hipMemcpyHostToDevice, stream_));
+            comm_->broadcast(buf.p, 1, 0, stream_);
+            SR_HIP(hipMemcpyAsync(&len, buf.p, 8, hipMemcpyDeviceToHost, stream_));
+            SR_HIP(hipStreamSynchronize(stream_));
+            buf.alloc(o_.device, std::max<u64>(1, len));
+            if (comm_->rank == 0 && len)
+                SR_HIP(hipMemcpyAsync(buf.p, paths_[p].data(), len * 8, hipMemcpyHostToDevice, stream_));
+            comm_->broadcast(buf.p, std::max<u64>(1, len), 0, stream_);
+            paths_[p].resize(len);
+            if (len) SR_HIP(hipMemcpyAsync(paths_[p].data(), buf.p, len * 8, hipMemcpyDeviceToHost, stream_));
+            SR_HIP(hipStreamSynchronize(stream_));
+        }
+        paths_ready_ = true;
+    }
+    bool path_states(int p, std::vector<u64>& st) {
+        if (p < 0 || p >= M::NPROPS) return false;
+        if (paths_ready_) {
+            st = paths_[p];
+            return !st.empty();
+        }
+        return tree_path(p, st);
+    }
+
+    // `reconstruct_path` across partitions: walk parent gids.
     int chain(int p, std::vector<u64>& out) override {
         out.clear();
         std::vector<u64> st;
-        if (!tree_path(p, st)) return 0;
+        if (!path_states(p, st)) return 0;
         for (size_t i = 0; i < st.size() / W; ++i) out.push_back(fingerprint<W>(&st[i * W]));
         return (int)out.size();
     }
     int path(int p, std::vector<i64>& actions, std::vector<i64>& states) override {
         std::vector<u64> st;
-        if (!tree_path(p, st)) return -1;
+        if (!path_states(p, st)) return -1;
         const int wd = m_.describe_width();
         const size_t len = st.size() / W;
         for (size_t i = 0; i < len; ++i) {
@@ -492,7 +753,7 @@ class DistEngine final : public EngineBase {
                 stats.expand_launches++;
             }
             // ---- 2. all-gather one row per partition; the host waits for it ----
-            if (comm_) SR_NCCL(ncclAllGather(rows_mine_.p, rows_all_.p, RW, ncclUint64, comm_->nccl, stream_));
+            if (comm_) comm_->all_gather(rows_mine_.p, rows_all_.p, RW, stream_);
             const u32 rseq = ++ctx_->rows_seq;
             u32* hseq = reinterpret_cast<u32*>(ctx_->hrows_dev);
             rows_publish<<<1, 64, 0, stream_>>>(rows_all_.p, ctx_->hrows_dev + 8, (u32)(RW * T_), hseq, rseq);
@@ -783,7 +1044,7 @@ class DistEngine final : public EngineBase {
             stats.expand_launches++;
         }
         if (comm_) {
-            SR_NCCL(ncclAllToAll(parts_[0].send.p, parts_[0].recv.p, S, ncclUint64, comm_->nccl, stream_));
+            comm_->all_to_all(parts_[0].send.p, parts_[0].recv.p, S, stream_);
         } else {
             for (auto& dst : parts_)
                 for (auto& src : parts_)
@@ -1006,22 +1267,19 @@ class DistEngine final : public EngineBase {
             return;
         }
         Part& p = parts_[0];
-        const int me = comm_->rank;
-        SR_NCCL(ncclGroupStart());
+        const int me = comm_->rank, world = comm_->world;
+        std::vector<const u64*> sp(world);
+        std::vector<u64*> rp(world);
+        std::vector<u64> sc(world), rc(world);
         u64 off = 0;
-        for (int peer = 0; peer < comm_->world; ++peer) {
-            u64 sc = all[(u64)me * RW + peer];     // I send to peer
-            u64 rc = all[(u64)peer * RW + me];     // peer sends to me
-            if (peer == me) {
-                if (sc) SR_HIP(hipMemcpyAsync(p.recv.p + off * REC, p.send.p + (u64)me * p.bucket_cap * REC, sc * REC * 8,
-                                              hipMemcpyDeviceToDevice, stream_));
-            } else {
-                if (sc) SR_NCCL(ncclSend(p.send.p + (u64)peer * p.bucket_cap * REC, sc * REC, ncclUint64, peer, comm_->nccl, stream_));
-                if (rc) SR_NCCL(ncclRecv(p.recv.p + off * REC, rc * REC, ncclUint64, peer, comm_->nccl, stream_));
-            }
-            off += rc;
+        for (int peer = 0; peer < world; ++peer) {
+            sc[peer] = all[(u64)me * RW + peer] * REC;  // words I send to peer
+            rc[peer] = all[(u64)peer * RW + me] * REC;  // words peer sends to me (source-major)
+            sp[peer] = p.send.p + (u64)peer * p.bucket_cap * REC;
+            rp[peer] = p.recv.p + off;
+            off += rc[peer];
         }
-        SR_NCCL(ncclGroupEnd());
+        comm_->exchange(sp, sc, rp, rc, stream_);
     }
 
     bool tree_path(int pr, std::vector<u64>& st) {
@@ -1065,7 +1323,7 @@ class DistEngine final : public EngineBase {
                     SR_HIP(hipMemcpyAsync(buf.p, p.arena.p + idx * W, W * 8, hipMemcpyDeviceToDevice, stream_));
                     SR_HIP(hipMemcpyAsync(buf.p + W, p.apar.p + idx, 8, hipMemcpyDeviceToDevice, stream_));
                 }
-                SR_NCCL(ncclBroadcast(buf.p, buf.p, TREC, ncclUint64, (int)owner, comm_->nccl, stream_));
+                comm_->broadcast(buf.p, TREC, (int)owner, stream_);
                 SR_HIP(hipMemcpyAsync(rec, buf.p, TREC * 8, hipMemcpyDeviceToHost, stream_));
                 SR_HIP(hipStreamSynchronize(stream_));
             }
@@ -1107,7 +1365,7 @@ class DistEngine final : public EngineBase {
                         SR_HIP(hipStreamSynchronize(stream_));
                         unsigned long long lg = h == ~0ull ? ~0ull : (((u64)p.id << GID_SHIFT) | (lo + h));
                         SR_HIP(hipMemcpyAsync(g.p, &lg, 8, hipMemcpyHostToDevice, stream_));
-                        SR_NCCL(ncclAllReduce(g.p, g.p, 1, ncclUint64, ncclMin, comm_->nccl, stream_));
+                        comm_->all_reduce(reinterpret_cast<u64*>(g.p), 1, RedOp::Min, stream_);
                         SR_HIP(hipMemcpyAsync(&h, g.p, 8, hipMemcpyDeviceToHost, stream_));
                         SR_HIP(hipStreamSynchronize(stream_));
                         found = std::min<u64>(found, h);
@@ -1195,6 +1453,8 @@ class DistEngine final : public EngineBase {
     Clock::time_point t_trace_ = Clock::now();
     u64 arena_grows_ = 0;
     std::vector<u64> rows_;
+    std::vector<std::vector<u64>> paths_;  // per property: the discovery path's states (gather_paths)
+    bool paths_ready_ = false;
 };
 
 }  // namespace sr

@@ -77,6 +77,8 @@ class EngineBase {
     std::string error;
     sr_stats stats{};
     std::vector<DiscoveryRec> disc;
+    std::vector<double> launch_ms;    // per timed launch (profile=1), in launch order
+    std::vector<u64> launch_frontier; // the frontier each launch expanded (0 if unknown)
 };
 
 template <class M>
@@ -96,7 +98,7 @@ class Engine final : public EngineBase {
         if (const char* e = std::getenv("SR_FILTER_LOG2")) filt_log2_ = (u32)std::atoi(e);
         if (const char* e = std::getenv("SR_PIPELINE")) pipeline_ = std::atoi(e) != 0;
         if (const char* e = std::getenv("SR_QUERY_LOG2")) query_mask_ = (1ull << std::atoi(e)) - 1;
-        if (const char* e = std::getenv("SR_GRID_MAX")) grid_max_ = std::max(1, std::atoi(e));
+        if (const char* e = std::getenv("SR_GRID_MAX")) grid_max_ = (u32)std::max(0, std::atoi(e));  // <= 0: unset
     }
     ~Engine() override = default;
 
@@ -412,22 +414,25 @@ class Engine final : public EngineBase {
     // Launch bracketed by pooled events (profile=1); durations are summed once at the end of the
     // run, so timing adds no synchronisation to the level loop.
     template <class F>
-    void timed(F&& launch) {
+    void timed(F&& launch, u64 frontier = 0) {
         size_t i = 2 * stats.expand_launches;
         if (o_.profile) SR_HIP(hipEventRecord(ctx_->event(i), stream_));
         launch();
         SR_HIP(hipGetLastError());
         if (o_.profile) SR_HIP(hipEventRecord(ctx_->event(i + 1), stream_));
         stats.expand_launches++;
+        launch_frontier.push_back(frontier);
     }
     void collect_timing() {
         if (!o_.profile || !stats.expand_launches) return;
         SR_HIP(hipEventSynchronize(ctx_->event(2 * stats.expand_launches - 1)));
         double ms = 0;
+        launch_ms.assign(stats.expand_launches, 0.0);
         for (u64 i = 0; i < stats.expand_launches; ++i) {
             float t = 0;
             SR_HIP(hipEventElapsedTime(&t, ctx_->event(2 * i), ctx_->event(2 * i + 1)));
             ms += t;
+            launch_ms[i] = t;
         }
         stats.expand_kernel_ms = ms;
     }
@@ -443,6 +448,8 @@ class Engine final : public EngineBase {
         stats = sr_stats{};
         stats.words_per_state = W;
         stats.order_used = (u32)order;
+        launch_ms.clear();
+        launch_frontier.clear();
 
         // Visited set sized for <= table_load_ load at the hinted unique count.
         u64 cap = (u64)(1u << 20) * grow_factor_;
@@ -597,6 +604,8 @@ class Engine final : public EngineBase {
             state_count += lc_.successors;
             unique += lc_.claims;
             stats.successors += lc_.successors;
+            stats.probes += lc_.probes;
+            stats.cas += lc_.cas;
             stats.algorithmic_bytes += limit * 8 * W + lc_.successors * 8 + (u64)lc_.claims * (16 + 8 * W);
             stats.levels++;
             if (produced) max_depth = level + 1;
@@ -676,6 +685,9 @@ class Engine final : public EngineBase {
             state_count += lc_.successors;
             unique += produced;
             stats.successors += lc_.successors;
+            stats.probes += lc_.probes;
+            stats.cas += lc_.cas;
+            if (level < launch_frontier.size()) launch_frontier[level] = n;  // one launch per level
             stats.algorithmic_bytes += n * 8 * W + lc_.successors * 8 + produced * (16 + 8 * W);
             stats.levels++;
             ratio_ = (double)produced / (double)n;
@@ -724,8 +736,9 @@ class Engine final : public EngineBase {
 
     // expand_fast's grid is capped at two full residencies of the device (resident blocks per CU
     // at its LDS footprint x CUs); the kernel strides over any further parents. Whole residencies
-    // avoid a partial last wave of workgroups: 2pc N=9 2.61 -> 2.55 ms per check
-    // (`profiles/r01_grid_sweep.jsonl`; SR_GRID_MAX overrides).
+    // avoid a partial last wave of workgroups. The measured gain is small and of the order of the
+    // ±3% run-to-run noise (`profiles/r01_grid_sweep.jsonl`, `r01_gridcap_default.jsonl`); the cap
+    // is printed with verbose=1. SR_GRID_MAX > 0 overrides it (<= 0 or unparsable: the default).
     u32 expand_grid_cap() {
         if (grid_max_) return grid_max_;
         int per_cu = 0, cus = 0;
@@ -734,6 +747,7 @@ class Engine final : public EngineBase {
         SR_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 256, dyn));
         SR_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, o_.device));
         grid_max_ = per_cu > 0 && cus > 0 ? (u32)(2 * per_cu * cus) : ~0u;
+        if (o_.verbose) std::fprintf(stderr, "[sr] expand grid cap %u blocks (%d per CU x %d CUs x 2)\n", grid_max_, per_cu, cus);
         return grid_max_;
     }
 
@@ -755,11 +769,12 @@ class Engine final : public EngineBase {
                     m_, arena_.p + fbase * W, 0u, n, view(), arena_.p + nbase * W, apar_.p + nbase, ncap, lc_d_,
                     undiscovered, hcd(sq), sq, 1u, ppw_log2, filt_log2_, dev_n ? 1u : 0u);
             };
-            switch (probe_batch_ * 10 + probe_load_) {
+            if (o_.counters) launch(expand_fast<M, 1, 0, true>);
+            else switch (probe_batch_ * 10 + probe_load_) {
                 case 20: launch(expand_fast<M, 2, 0>); break;
                 default: launch(expand_fast<M, 1, 0>); break;
             }
-        });
+        }, n);
         return sq;
     }
 
@@ -873,14 +888,15 @@ class Engine final : public EngineBase {
                 u64* next = arena_.p + nbase * W;
                 u32* npar = apar_.p + nbase;
                 const u32 ppw_log2 = ppw_env_ >= 0 ? (u32)ppw_env_ : ppw_for(c);
-                const u32 grid = blocks_for((c + (1u << ppw_log2) - 1) >> ppw_log2, 4);
+                const u32 grid = std::min(expand_grid_cap(), blocks_for((c + (1u << ppw_log2) - 1) >> ppw_log2, 4));
                 timed([&] {
                     auto launch = [&](auto kern) {
                         kern<<<grid, 256, filt_log2_ ? (8u << filt_log2_) : 0u, stream_>>>(
                             m_, cur(), ulo, uhi, view(), next, npar, ncap, lc_d_, undiscovered, hcd(sq), sq,
                             last ? 1u : 0u, ppw_log2, filt_log2_, 0u);
                     };
-                    switch (probe_batch_ * 10 + probe_load_) {
+                    if (o_.counters) launch(expand_fast<M, 1, 0, true>);
+                    else switch (probe_batch_ * 10 + probe_load_) {
                         case 11: launch(expand_fast<M, 1, 1>); break;
                         case 12: launch(expand_fast<M, 1, 2>); break;
                         case 13: launch(expand_fast<M, 1, 3>); break;
@@ -1108,6 +1124,18 @@ int32_t sr_gpu_bfs_stats(const sr_bfs* b, sr_stats* out) {
     return SR_OK;
 }
 
+int64_t sr_gpu_bfs_launch_profile(const sr_bfs* b, double* kernel_ms, uint64_t* frontier, int64_t cap) {
+    if (!b) return SR_ERR_ARG;
+    const auto& ms = b->e->launch_ms;
+    const auto& fr = b->e->launch_frontier;
+    const int64_t n = (int64_t)ms.size();
+    for (int64_t i = 0; i < std::min(n, cap); ++i) {
+        if (kernel_ms) kernel_ms[i] = ms[i];
+        if (frontier) frontier[i] = i < (int64_t)fr.size() ? fr[i] : 0;
+    }
+    return n;
+}
+
 int32_t sr_gpu_bfs_property_count(const sr_bfs* b) { return b ? b->e->nprops() : 0; }
 
 int32_t sr_gpu_bfs_property(const sr_bfs* b, int32_t p, char* name, int32_t cap, int32_t* expectation) {
@@ -1197,7 +1225,15 @@ int32_t sr_gpu_bfs_replay(const sr_bfs* b, int32_t init, const int64_t* ids, int
 }
 
 struct sr_dist {
-    Comm c;
+    std::unique_ptr<Comm> c;
+    hipStream_t stream = nullptr;  // for sr_dist_barrier / sr_dist_allreduce_f64
+    hipStream_t get_stream() {
+        if (!stream) {
+            SR_HIP(hipSetDevice(c->device));
+            SR_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+        }
+        return stream;
+    }
 };
 
 int32_t sr_dist_unique_id(uint8_t* out) {
@@ -1215,13 +1251,15 @@ sr_dist* sr_dist_init(int32_t rank, int32_t world, const uint8_t* idb, int32_t d
     try {
         if (world < 1 || rank < 0 || rank >= world) throw Error(SR_ERR_ARG, "bad rank/world");
         SR_HIP(hipSetDevice(device));
-        auto d = std::make_unique<sr_dist>();
-        d->c.rank = rank;
-        d->c.world = world;
-        d->c.device = device;
+        auto c = std::make_unique<RcclComm>();
+        c->rank = rank;
+        c->world = world;
+        c->device = device;
         ncclUniqueId id;
         std::memcpy(&id, idb, sizeof(id));
-        SR_NCCL(ncclCommInitRank(&d->c.nccl, world, id, rank));
+        SR_NCCL(ncclCommInitRank(&c->nccl, world, id, rank));
+        auto d = std::make_unique<sr_dist>();
+        d->c = std::move(c);
         return d.release();
     } catch (const std::exception& x) {
         set_error(x.what());
@@ -1229,10 +1267,108 @@ sr_dist* sr_dist_init(int32_t rank, int32_t world, const uint8_t* idb, int32_t d
     }
 }
 
+int32_t sr_dist_local_group(int32_t world, const int32_t* devices, sr_dist** out) {
+    try {
+        if (world < 1 || !out) throw Error(SR_ERR_ARG, "bad world/out");
+        auto g = std::make_shared<LocalGroup>(world);
+        for (int r = 0; r < world; ++r) {
+            auto c = std::make_unique<LocalComm>();
+            c->rank = r;
+            c->world = world;
+            c->device = devices ? devices[r] : 0;
+            c->g = g;
+            auto d = std::make_unique<sr_dist>();
+            d->c = std::move(c);
+            out[r] = d.release();
+        }
+        return SR_OK;
+    } catch (const std::exception& x) {
+        set_error(x.what());
+        return SR_ERR_ARG;
+    }
+}
+
+int32_t sr_dist_rank(const sr_dist* d) { return d ? d->c->rank : SR_ERR_ARG; }
+int32_t sr_dist_world(const sr_dist* d) { return d ? d->c->world : SR_ERR_ARG; }
+int32_t sr_dist_nranks(const sr_dist* d) { return d ? d->c->nranks() : SR_ERR_ARG; }
+int32_t sr_dist_kind(const sr_dist* d, char* buf, int32_t cap) {
+    if (!d) return SR_ERR_ARG;
+    const char* k = d->c->kind();
+    if (buf && cap > 0) std::snprintf(buf, (size_t)cap, "%s", k);
+    return (int32_t)std::strlen(k);
+}
+
+int32_t sr_dist_barrier(sr_dist* d) {
+    try {
+        if (!d) return SR_ERR_ARG;
+        SR_HIP(hipSetDevice(d->c->device));
+        SR_HIP(hipDeviceSynchronize());
+        d->c->barrier(d->get_stream());
+        return SR_OK;
+    } catch (const Error& x) {
+        set_error(x.what());
+        return x.code;
+    }
+}
+
+int32_t sr_dist_allreduce_f64(sr_dist* d, double* values, int32_t n, int32_t op) {
+    try {
+        if (!d || !values || n < 1 || op < 0 || op > 2) return SR_ERR_ARG;
+        // doubles travel as order-preserving u64 keys, so min and max are exact (no sum)
+        if (op == 2) throw Error(SR_ERR_ARG, "sr_dist_allreduce_f64: only min (0) and max (1)");
+        std::vector<u64> k(n);
+        for (int i = 0; i < n; ++i) {
+            u64 b;
+            std::memcpy(&b, &values[i], 8);
+            k[i] = (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+        }
+        SR_HIP(hipSetDevice(d->c->device));
+        hipStream_t s = d->get_stream();
+        DBuf<u64> buf;
+        buf.alloc(d->c->device, n);
+        SR_HIP(hipMemcpyAsync(buf.p, k.data(), n * 8, hipMemcpyHostToDevice, s));
+        d->c->all_reduce(buf.p, n, op == 0 ? RedOp::Min : RedOp::Max, s);
+        SR_HIP(hipMemcpyAsync(k.data(), buf.p, n * 8, hipMemcpyDeviceToHost, s));
+        SR_HIP(hipStreamSynchronize(s));
+        for (int i = 0; i < n; ++i) {
+            const u64 b = (k[i] >> 63) ? (k[i] & 0x7fffffffffffffffull) : ~k[i];
+            std::memcpy(&values[i], &b, 8);
+        }
+        return SR_OK;
+    } catch (const Error& x) {
+        set_error(x.what());
+        return x.code;
+    }
+}
+
 void sr_dist_free(sr_dist* d) {
     if (!d) return;
-    if (d->c.nccl) (void)ncclCommDestroy(d->c.nccl);
+    if (d->stream) (void)hipStreamDestroy(d->stream);
     delete d;
+}
+
+int32_t sr_rccl_version(int32_t* runtime, int32_t* compiled) {
+    int v = 0;
+    if (ncclGetVersion(&v) != ncclSuccess) return SR_ERR_HIP;
+    if (runtime) *runtime = v;
+    if (compiled) *compiled = NCCL_VERSION_CODE;
+    return SR_OK;
+}
+
+int32_t sr_hip_runtime_version(int32_t* runtime, int32_t* compiled) {
+    int v = 0;
+    if (hipRuntimeGetVersion(&v) != hipSuccess) return SR_ERR_HIP;
+    if (runtime) *runtime = v;
+    if (compiled) *compiled = HIP_VERSION;
+    return SR_OK;
+}
+
+int32_t sr_device_synchronize(int32_t device) {
+    if (hipSetDevice(device) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+        set_error("hipDeviceSynchronize failed");
+        return SR_ERR_HIP;
+    }
+    return SR_OK;
 }
 
 sr_bfs* sr_gpu_bfs_spawn_partitioned(sr_dist* comm, int32_t virtual_parts, int32_t model_id, const int64_t* params,
@@ -1241,10 +1377,10 @@ sr_bfs* sr_gpu_bfs_spawn_partitioned(sr_dist* comm, int32_t virtual_parts, int32
         sr_opts o;
         sr_opts_init(&o);
         if (opts) std::memcpy(&o, opts, std::min<size_t>(sizeof(o), opts->struct_size ? opts->struct_size : sizeof(o)));
-        if (comm) o.device = comm->c.device;
+        if (comm) o.device = comm->c->device;
         if (sr_device_count() <= 0) throw Error(SR_ERR_NO_DEVICE, "no HIP device visible");
         auto b = std::make_unique<sr_bfs>();
-        b->e = make_model_engine<DistEngine>(model_id, params, nparams, o, comm ? &comm->c : nullptr, (int)virtual_parts);
+        b->e = make_model_engine<DistEngine>(model_id, params, nparams, o, comm ? comm->c.get() : nullptr, (int)virtual_parts);
         EngineBase* e = b->e.get();
         b->th = std::thread([e] {
             try {

@@ -17,6 +17,8 @@
 // slot costs a 64-bit atomicCAS. A successor equal to its parent (a self-loop: 37% of 2pc's
 // successors) is a duplicate by construction and is counted without touching the table.
 #pragma once
+#include <cstddef>
+
 #include "models.hpp"
 
 namespace sr {
@@ -48,7 +50,9 @@ constexpr u32 NO_PARENT = 0xffffffffu;
 struct LevelCounters {
     u64 successors;        // successors within boundary (state_count increments, bfs.rs:235)
     u64 enabled;           // enabled action slots of the expanded parents (launch-shape statistic)
-    u64 pad0[14];
+    u64 probes;            // visited-set slots loaded (first probe + linear-probe steps)
+    u64 cas;               // 64-bit atomicCAS claims attempted on the visited set
+    u64 pad0[12];
     u32 claims;            // new states inserted into the visited set (= next-frontier cursor)
     u32 pad1[31];
     u32 ticket;            // workgroups finished in this launch
@@ -64,6 +68,8 @@ struct LevelCounters {
 struct HostCounters {
     u64 successors;
     u64 enabled;
+    u64 probes;
+    u64 cas;
     u32 claims;
     u32 err;
     u32 aux;               // launch-specific value (FIFO: number of owners from the scan)
@@ -76,6 +82,8 @@ template <int NP>
 __device__ __forceinline__ void reset_counters(LevelCounters* lc) {
     lc->successors = 0;
     lc->enabled = 0;
+    lc->probes = 0;
+    lc->cas = 0;
     lc->claims = 0;
     lc->err = 0;
 #pragma unroll
@@ -95,37 +103,68 @@ __device__ __forceinline__ void reset_counters(LevelCounters* lc) {
 // arrives last copies the counters to host memory, optionally resets them for the next level,
 // and finally stores `seq` (Guideline 16: release before the ticket, acquire after it). NP = the
 // number of properties whose discovery ranks are live.
+//
+// The snapshot is gathered by the 64 lanes of wave 0 at once: lane i loads counter word i (every
+// load is an agent-scope round trip to the coherence point, ≈1 µs; issued by one thread they
+// were ~12 dependent round trips at the tail of EVERY level, the floor of a small level), then
+// writes it to its host word. u64 counters move as two u32 words: no workgroup updates them any
+// more once the ticket has been taken by the last one.
 template <int NP>
 __device__ __forceinline__ void publish(LevelCounters* lc, HostCounters* h, u32 seq, bool reset, const u32* aux,
                                         const u32* sendc = nullptr, u32 nparts = 0) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (threadIdx.x != 0) return;
+    if (threadIdx.x >= 64) return;
+    const u32 lane = threadIdx.x;
+    u32 last = 0;
+    if (lane == 0) {
 #if SR_TICKET_FENCE
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
 #endif
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    u32 t = atomicAdd(&lc->ticket, 1u);
-    if (t != gridDim.x - 1) return;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        last = atomicAdd(&lc->ticket, 1u) == gridDim.x - 1;
+    }
+    if (!__shfl(last, 0, 64)) return;
 #if SR_TICKET_FENCE
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 #endif
-    h->successors = __hip_atomic_load(&lc->successors, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    h->enabled = __hip_atomic_load(&lc->enabled, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const u32 claims = __hip_atomic_load(&lc->claims, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    h->claims = claims;
-    h->err = __hip_atomic_load(&lc->err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    h->aux = aux ? __hip_atomic_load(aux, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
-#pragma unroll
-    for (int p = 0; p < NP; ++p) h->disc[p] = __hip_atomic_load(&lc->disc[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    for (u32 q = 0; q < nparts; ++q) h->sendc[q] = __hip_atomic_load(&sendc[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (reset) {
-        lc->prev_claims = claims;
-        reset_counters<NP>(lc);
+    // word map: [0, 8) successors/enabled/probes/cas (same offsets in both structs), 8 claims,
+    // 9 err, 10 aux, 11 + p disc[p], 11 + NP + q sendc[q]
+    u32* lcw = reinterpret_cast<u32*>(lc);
+    u32* hw = reinterpret_cast<u32*>(h);
+    constexpr u32 O_CLAIMS = offsetof(LevelCounters, claims) / 4, O_ERR = offsetof(LevelCounters, err) / 4;
+    constexpr u32 O_DISC = offsetof(LevelCounters, disc) / 4;
+    constexpr u32 H_CLAIMS = offsetof(HostCounters, claims) / 4, H_ERR = offsetof(HostCounters, err) / 4;
+    constexpr u32 H_AUX = offsetof(HostCounters, aux) / 4, H_DISC = offsetof(HostCounters, disc) / 4;
+    constexpr u32 H_SENDC = offsetof(HostCounters, sendc) / 4;
+    const u32 nwords = 11 + NP + nparts;
+    u32 claims = 0;
+    for (u32 i0 = 0; i0 < nwords; i0 += 64) {
+        const u32 i = i0 + lane;
+        const u32* src = nullptr;
+        u32 dst = 0;
+        if (i < 8) src = lcw + i, dst = i;
+        else if (i == 8) src = lcw + O_CLAIMS, dst = H_CLAIMS;
+        else if (i == 9) src = lcw + O_ERR, dst = H_ERR;
+        else if (i == 10) src = aux, dst = H_AUX;
+        else if (i < 11 + NP) src = lcw + O_DISC + (i - 11), dst = H_DISC + (i - 11);
+        else if (i < nwords) src = sendc + (i - 11 - NP), dst = H_SENDC + (i - 11 - NP);
+        const u32 v = src ? __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+        if (i < nwords) hw[dst] = v;
+        if (i0 == 0) claims = __shfl(v, 8, 64);
     }
-    lc->ticket = 0;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: host memory
-    __hip_atomic_store(&h->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every word read before any is reset
+    if (reset) {
+        if (lane < 8) lcw[lane] = 0;  // successors, enabled, probes, cas
+        if (lane == 8) lc->claims = 0;
+        if (lane == 9) lc->err = 0;
+        if (lane >= 11 && lane < 11 + NP) lc->disc[lane - 11] = ~0u;
+        if (lane == 0) lc->prev_claims = claims;
+    }
+    if (lane == 0) lc->ticket = 0;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the whole wave's host stores issued and acked
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");     // system scope: host memory
+    if (lane == 0) __hip_atomic_store(&h->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Standalone publish (after kernels that do not publish themselves).
@@ -145,14 +184,17 @@ __device__ __forceinline__ u64 probe_load(const u64* p) {
 
 // Find `key` or claim a vacant slot for it, starting at slot i whose key `cur` was already loaded.
 // Returns the slot; *is_new tells whether we claimed it.
+// *probes / *cas (optional) count the further slot loads and the CAS attempts.
 template <int POL = 0>
-__device__ __forceinline__ u64 find_or_claim_from(const TableView& t, u64 key, u64 i, u64 cur, bool* is_new, u32* err) {
+__device__ __forceinline__ u64 find_or_claim_from(const TableView& t, u64 key, u64 i, u64 cur, bool* is_new, u32* err,
+                                                  u32* probes = nullptr, u32* cas = nullptr) {
     for (int probe = 0; probe < MAX_PROBE; ++probe) {
         if (cur == key) {
             *is_new = false;
             return i;
         }
         if (cur == 0) {
+            if (cas) ++*cas;
             u64 prev = atomicCAS(reinterpret_cast<unsigned long long*>(&t.keys[i]), 0ull,
                                  (unsigned long long)key);
             if (prev == 0) {
@@ -166,6 +208,7 @@ __device__ __forceinline__ u64 find_or_claim_from(const TableView& t, u64 key, u
         }
         i = (i + 1) & t.mask;
         cur = probe_load<POL>(&t.keys[i]);
+        if (probes) ++*probes;
     }
     atomicOr(err, (u32)ERR_TABLE_FULL);
     *is_new = false;
@@ -301,7 +344,10 @@ __device__ __forceinline__ u32 select_bit(u64 m, u32 k) {
 // the workgroup reserves its span of the next frontier with ONE global atomic, copies the staged
 // states out contiguously, and evaluates the properties there (rank = frontier position). A
 // workgroup that stages more than STAGE states appends the overflow directly.
-template <class M, int PB, int POL>
+// STATS = 1 also counts visited-set probes and CAS attempts (sr_opts.counters): a separate
+// instantiation, because the per-lane counters cost registers (SGPR spills 8 -> 47) and ~20% of
+// the kernel's time.
+template <class M, int PB, int POL, bool STATS = false>
 __global__ void __launch_bounds__(256) expand_fast(M m, const u64* __restrict__ frontier, u32 lo, u32 hi,
                                                    TableView t, u64* __restrict__ next, u32* __restrict__ next_par,
                                                    u32 next_cap, LevelCounters* lc, u32 undiscovered,
@@ -335,7 +381,7 @@ __global__ void __launch_bounds__(256) expand_fast(M m, const u64* __restrict__ 
     const u32 fmask = filt_log2 ? (1u << filt_log2) - 1 : 0;
     if (lo + (u64)blockIdx.x * chunk < hi)  // blocks past the frontier only take their ticket
         for (u32 i = threadIdx.x; i < (fmask ? fmask + 1 : 0u); i += blockDim.x) filt[i] = 0;
-    u32 succ = 0, enabled = 0;
+    u32 succ = 0, enabled = 0, probes = 0, cas = 0;
     for (u64 c0 = lo + (u64)blockIdx.x * chunk; c0 < hi; c0 += (u64)gridDim.x * chunk) {
         const u32 wave0 = (u32)(c0 + ((u64)wid << ppw_log2));  // first parent of the wave
         const u32 r = wave0 + lane;
@@ -420,7 +466,10 @@ __global__ void __launch_bounds__(256) expand_fast(M m, const u64* __restrict__ 
                 }
             }
 #pragma unroll
-            for (int j = 0; j < PB; ++j) cur[j] = ok[j] ? probe_load<POL>(&t.keys[idx[j]]) : 0;
+            for (int j = 0; j < PB; ++j) {
+                cur[j] = ok[j] ? probe_load<POL>(&t.keys[idx[j]]) : 0;
+                if constexpr (STATS) probes += ok[j];
+            }
             bool nw[PB];
 #pragma unroll
             for (int j = 0; j < PB; ++j) {
@@ -428,7 +477,8 @@ __global__ void __launch_bounds__(256) expand_fast(M m, const u64* __restrict__ 
                 if (!ok[j]) continue;
                 ++succ;
                 if (cur[j] == key[j]) continue;  // the common case: an already visited state
-                find_or_claim_from<POL>(t, key[j], idx[j], cur[j], &nw[j], &lc->err);
+                find_or_claim_from<POL>(t, key[j], idx[j], cur[j], &nw[j], &lc->err, STATS ? &probes : nullptr,
+                                        STATS ? &cas : nullptr);
             }
             // Append the new states of this round, aggregated per wave: one LDS atomic reserves the
             // wave's span of the stage; what does not fit goes straight to the next frontier with
@@ -469,11 +519,15 @@ __global__ void __launch_bounds__(256) expand_fast(M m, const u64* __restrict__ 
     }
     u32 total_succ = block_sum(succ, scratch);
     u32 total_enabled = block_sum(enabled, scratch);
+    u32 total_probes = STATS ? block_sum(probes, scratch) : 0u;
+    u32 total_cas = STATS ? block_sum(cas, scratch) : 0u;
     const u32 n = min(stage_n, (u32)STAGE);
     if (threadIdx.x == 0) {
         base = n ? atomicAdd(&lc->claims, n) : 0;
         if (total_succ) atomicAdd(reinterpret_cast<unsigned long long*>(&lc->successors), (unsigned long long)total_succ);
         if (total_enabled) atomicAdd(reinterpret_cast<unsigned long long*>(&lc->enabled), (unsigned long long)total_enabled);
+        if (total_probes) atomicAdd(reinterpret_cast<unsigned long long*>(&lc->probes), (unsigned long long)total_probes);
+        if (total_cas) atomicAdd(reinterpret_cast<unsigned long long*>(&lc->cas), (unsigned long long)total_cas);
     }
     __syncthreads();
     for (u32 i = threadIdx.x; i < n; i += blockDim.x) {

@@ -1,0 +1,176 @@
+"""The partitioned engine's MULTI-RANK code path (dist.hpp with a communicator: one rank-local
+partition per rank, every collective issued in its order by every rank) run with world = 2, 3 and
+8 on one MI355X. The ranks are threads of this process on the in-process transport
+(sr_dist_local_group), which keeps RCCL's contract: stream-ordered collectives that every rank
+issues in the same sequence; a rank that issues a different collective or size makes every rank
+fail (RCCL would hang). Counts must equal the oracle's, every rank reports the same global counts,
+and discovery paths are available from ANY single rank after join (gathered at join), replaying on
+the CPU oracle model. Plus the BASELINE configuration 4 at its full size: 2pc N=11 partitioned 8
+ways (virtual partitions) against the closed forms of BASELINE.md §3."""
+import pytest
+
+from oracle_lib import INCREMENT_LOCK, LINEAR_EQUATION, TWO_PHASE, OracleRun, replay
+
+pytestmark = pytest.mark.gpu
+sr = pytest.importorskip("stateright_amd")
+from stateright_amd.distributed import Communicator  # noqa: E402
+
+MODELS = {
+    LINEAR_EQUATION: lambda p: sr.LinearEquation(*p),
+    TWO_PHASE: lambda p: sr.TwoPhaseSys(*p),
+    INCREMENT_LOCK: lambda p: sr.IncrementLock(*p),
+}
+_cache = {}
+
+
+def oracle(model, params):
+    k = (model, tuple(params))
+    if k not in _cache:
+        _cache[k] = OracleRun(model, params)
+    return _cache[k]
+
+
+def run_ranks(model, params, world, hint=0, defer=False):
+    comms = Communicator.local_group(world)
+    checkers = []
+    for c in comms:
+        b = MODELS[model](params).checker().comm(c)
+        if hint:
+            b = b.capacity_hint(hint)
+        if defer:
+            b = b.defer_paths()
+        checkers.append(b.spawn_bfs())
+    for ch in checkers:
+        ch.join()
+    return comms, checkers
+
+
+def close(comms, checkers):
+    checkers.clear()
+    for c in comms:
+        c.close()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("case", [(TWO_PHASE, [3]), (TWO_PHASE, [5]), (TWO_PHASE, [7]), (INCREMENT_LOCK, [7]),
+                                  (LINEAR_EQUATION, [2, 4, 7])],
+                         ids=lambda c: f"{c[0]}-{'-'.join(map(str, c[1]))}")
+def test_ranks_match_oracle(case, world):
+    model, params = case
+    o = oracle(model, params)
+    comms, cs = run_ranks(model, params, world)
+    try:
+        assert all(c.kind() == "local" and c.nranks() == world for c in comms)
+        for ch in cs:  # every rank reports the global counts
+            assert (ch.unique_state_count(), ch.state_count(), ch.max_depth()) == \
+                (o.unique_state_count, o.state_count, o.max_depth)
+        # discovery paths from ONE rank alone (no collective after join), valid on the CPU model
+        last = cs[-1]
+        assert sorted(last.discoveries()) == o.discovery_names()
+        props = last.properties()
+        names = [n for n, _ in props]
+        for name, path in last.discoveries().items():
+            r = replay(model, params, path.action_ids, n_props=len(props))
+            assert r is not None
+            want = 1 if props[names.index(name)][1] == sr.Expectation.Sometimes else 0
+            assert r[1][names.index(name)] == want
+            assert len(path) == len(o.discovery_actions(name))
+        # every rank gathered the same paths
+        assert cs[0].discoveries() == last.discoveries()
+    finally:
+        close(comms, cs)
+
+
+@pytest.mark.parametrize("sync", [False, True])
+@pytest.mark.parametrize("head", ["0", "65536"])
+def test_ranks_protocol_modes(sync, head, monkeypatch):
+    # the pipelined loop (one all-to-all per level, plan from the rows every rank holds) and the
+    # synchronous one (all-gather of rows + grouped exact-size exchange), with and without the
+    # replicated head
+    if sync:
+        monkeypatch.setenv("SR_DIST_SYNC", "1")
+    else:
+        monkeypatch.delenv("SR_DIST_SYNC", raising=False)
+    monkeypatch.setenv("SR_HEAD_MAX", head)
+    o = oracle(TWO_PHASE, [6])
+    comms, cs = run_ranks(TWO_PHASE, [6], 2)
+    try:
+        for ch in cs:
+            assert (ch.unique_state_count(), ch.state_count(), ch.max_depth()) == \
+                (o.unique_state_count, o.state_count, o.max_depth)
+            assert ch.stats()["pipelined"] == (0 if sync else 1)
+        assert sorted(cs[1].discoveries()) == o.discovery_names()
+    finally:
+        close(comms, cs)
+
+
+def test_ranks_deferred_paths_are_collective():
+    # defer_paths(): nothing gathered at join; every rank must then ask for the same property in
+    # the same order (threads here, as separate processes would)
+    import threading
+    o = oracle(TWO_PHASE, [5])
+    comms, cs = run_ranks(TWO_PHASE, [5], 2, defer=True)
+    out = [None, None]
+    try:
+        ts = [threading.Thread(target=lambda i=i: out.__setitem__(i, cs[i].discoveries())) for i in range(2)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(120)
+        # the walk through the replicated head is rank-local (each rank's head arena orders a
+        # level differently), so deferred paths may differ between ranks: all valid and shortest
+        assert out[0] is not None and out[1] is not None
+        for res in out:
+            assert sorted(res) == o.discovery_names()
+            for name, path in res.items():
+                r = replay(TWO_PHASE, [5], path.action_ids, n_props=3)
+                assert r is not None and r[1][["abort agreement", "commit agreement", "consistent"].index(name)] == 1
+                assert len(path) == len(o.discovery_actions(name))
+    finally:
+        close(comms, cs)
+
+
+def test_ranks_overflow_restart_is_collective():
+    # A tiny capacity hint: buffers overflow, every rank sees it in the rows and all restart together.
+    import math
+    n = 8
+    comms, cs = run_ranks(INCREMENT_LOCK, [n], 2, hint=10)
+    try:
+        expect = 1 + 4 * sum(math.factorial(n) // math.factorial(n - k) for k in range(1, n + 1))
+        assert [ch.unique_state_count() for ch in cs] == [expect, expect]
+    finally:
+        close(comms, cs)
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_ranks_bench_config(world):
+    # BASELINE config 3 (2pc N=9) on `world` ranks: closed forms, pipelined, no restart
+    n = 9
+    want = 6 ** n + 4 ** n + 2 ** n
+    comms, cs = run_ranks(TWO_PHASE, [n], world, hint=want)
+    try:
+        for ch in cs:
+            assert ch.unique_state_count() == want
+            assert 3 * ch.state_count() == 4 * n * 6 ** n + 3 * (n + 1) * 4 ** n + 3 * n * 2 ** n + 6
+            assert ch.max_depth() == 3 * n + 1
+            st = ch.stats()
+            assert st["pipelined"] == 1 and st["restarts"] == 0, st
+        assert sorted(cs[0].discoveries()) == ["abort agreement", "commit agreement"]
+    finally:
+        close(comms, cs)
+
+
+def test_config4_2pc11_partitioned_8_full_size():
+    # BASELINE configs[3]: 2pc N=11 partitioned 8 ways, at its full size (366 993 408 unique /
+    # 5 371 377 666 generated states, depth 34; BASELINE.md §3 closed forms).
+    n = 11
+    want = 6 ** n + 4 ** n + 2 ** n
+    c = sr.TwoPhaseSys(n).checker().partitions(8).capacity_hint(want).spawn_bfs().join()
+    assert c.unique_state_count() == want == 366_993_408
+    assert c.state_count() == 5_371_377_666
+    assert 3 * c.state_count() == 4 * n * 6 ** n + 3 * (n + 1) * 4 ** n + 3 * n * 2 ** n + 6
+    assert c.max_depth() == 3 * n + 1
+    assert sorted(c.discoveries()) == ["abort agreement", "commit agreement"]
+    for name, path in c.discoveries().items():
+        r = replay(TWO_PHASE, [n], path.action_ids, n_props=3)
+        assert r is not None and r[1][["abort agreement", "commit agreement", "consistent"].index(name)] == 1

@@ -263,3 +263,20 @@ def test_bucketed_levels_parity(n, monkeypatch):
     assert 3 * c.state_count() == 4 * n * 6 ** n + 3 * (n + 1) * 4 ** n + 3 * n * 2 ** n + 6
     assert c.max_depth() == 3 * n + 1
     assert sorted(c.discoveries()) == ["abort agreement", "commit agreement"]
+
+
+@pytest.mark.parametrize("grid", ["1", "2"])
+@pytest.mark.parametrize("case", [(TWO_PHASE, [5]), (TWO_PHASE, [8]), (PAXOS, [2])], ids=ids)
+def test_small_grid_strides(case, grid, monkeypatch):
+    # A one- or two-block grid strides over every chunk of every level, with and without level
+    # pipelining (dev_n = 1 / 0): the LDS duplicate filter and the stage persist across chunks and
+    # the stage overflows into direct appends. Counts and discoveries must not change.
+    monkeypatch.setenv("SR_GRID_MAX", grid)
+    model, params = case
+    o = oracle(model, params)
+    for pipe in ("1", "0"):
+        monkeypatch.setenv("SR_PIPELINE", pipe)
+        c, _ = gpu(model, params, "fast")
+        assert (c.unique_state_count(), c.state_count(), c.max_depth()) == \
+            (o.unique_state_count, o.state_count, o.max_depth)
+        assert sorted(c.discoveries()) == o.discovery_names()
