@@ -60,6 +60,8 @@ def parse():
     ap.add_argument("--order", default="fast", choices=["fast", "fifo"])
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU restatement (rank 0, N=1)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="host threads for the CPU baseline (0 = usable CPUs)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="every rank prints its launch plan as JSON and exits before any GPU call")
     ap.add_argument("--mode", default="partitioned", choices=["partitioned", "replicas", "rccl1"],
                     help="N>1: one check partitioned over the GPUs, or one independent check per GPU; "
                          "rccl1: the partitioned RCCL path on a one-rank communicator (N=1 rehearsal)")
@@ -167,6 +169,11 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"rank {rank}: WORLD_SIZE={world} but --gpus {args.gpus}")
+    if args.dry_run:
+        print(json.dumps({"dry_run": True, "rank": rank, "world_size": world, "local_rank": local_rank,
+                          "device": local_rank if world > 1 else 0, "mode": args.mode,
+                          "master": f"{os.environ.get('MASTER_ADDR')}:{os.environ.get('MASTER_PORT')}"}), flush=True)
+        return
 
     import math
 

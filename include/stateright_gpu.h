@@ -214,6 +214,9 @@ void sr_dist_free(sr_dist* comm);
 int32_t sr_rccl_version(int32_t* runtime, int32_t* compiled);
 int32_t sr_hip_runtime_version(int32_t* runtime, int32_t* compiled);
 int32_t sr_device_synchronize(int32_t device);
+/* Host-only self-test of the visited set's quotient encoding (kernels.hpp): the key permutation is
+ * a bijection and slot values decode to their keys. SR_OK or SR_ERR_ARG (sr_last_error). */
+int32_t sr_selftest_tables(void);
 /* comm == NULL: `virtual_partitions` partitions in this process on opts->device (same protocol,
  * device-copy exchange). FAST order only. */
 sr_bfs* sr_gpu_bfs_spawn_partitioned(sr_dist* comm, int32_t virtual_partitions, int32_t model_id,

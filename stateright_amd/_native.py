@@ -107,6 +107,7 @@ SIGNATURES = [
     ("sr_rccl_version", ctypes.c_int32, [ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32)]),
     ("sr_hip_runtime_version", ctypes.c_int32, [ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32)]),
     ("sr_device_synchronize", ctypes.c_int32, [ctypes.c_int32]),
+    ("sr_selftest_tables", ctypes.c_int32, []),
     ("sr_gpu_bfs_spawn_partitioned", _P, [_P, ctypes.c_int32, ctypes.c_int32, _I64P, ctypes.c_int32,
                                           ctypes.POINTER(sr_opts)]),
 ]

@@ -359,7 +359,8 @@ class DistEngine final : public EngineBase {
         u64 n_hi = 0, n_est = 0;         // upper bound / estimate of the next frontier size
         u64 local_prev = 0, nrec_prev = 0;
         u64 uniq = 0;                    // states claimed in this partition's visited set
-        TableView view() const { return TableView{keys.p, nullptr, cap - 1}; }
+        const M* model = nullptr;
+        TableView view() const { return make_table_view(*model, keys.p, nullptr, cap); }
     };
 
   public:
@@ -372,7 +373,16 @@ class DistEngine final : public EngineBase {
         if (T_ > (u32)MAX_PARTS) throw Error(SR_ERR_ARG, "at most 64 partitions");
         const u32 L = comm_ ? 1 : T_;
         parts_.resize(L);
-        for (u32 i = 0; i < L; ++i) parts_[i].id = comm_ ? (u32)comm_->rank : i;
+        for (u32 i = 0; i < L; ++i) {
+            parts_[i].id = comm_ ? (u32)comm_->rank : i;
+            parts_[i].model = &m_;
+        }
+        if (make_table_view(m_, nullptr, nullptr, min_table_cap(m_)).qbits) {
+            // exact quotient-mode tables: the LDS filter and the sent cache compare fingerprints,
+            // which are not exact for multi-word states
+            filt_log2_ = 0;
+            send_cache_max_parts_ = 0;
+        }
     }
     ~DistEngine() override {
         if (ctx_) {
@@ -601,7 +611,7 @@ class DistEngine final : public EngineBase {
         p.cap *= 2;
         p.keys.alloc(o_.device, p.cap);
         SR_HIP(hipMemsetAsync(p.keys.p, 0, p.cap * 8, stream_));
-        rehash<<<blocks_for(old_cap, 256), 256, 0, stream_>>>(TableView{ok.p, nullptr, old_cap - 1}, old_cap, p.view(), p.lc);
+        rehash<<<blocks_for(old_cap, 256), 256, 0, stream_>>>(make_table_view(m_, ok.p, nullptr, old_cap), old_cap, p.view(), p.lc);
         SR_HIP(hipGetLastError());
         SR_HIP(hipStreamSynchronize(stream_));
         stats.rehashes++;
@@ -649,7 +659,7 @@ class DistEngine final : public EngineBase {
         rows_all_.alloc(o_.device, RW * T_);
         if (comm_) rows_mine_.alloc(o_.device, RW);
         for (auto& p : parts_) {
-            u64 cap = (u64)(1u << 16) * grow_factor_;
+            u64 cap = std::max<u64>((u64)(1u << 16) * grow_factor_, min_table_cap(m_));
             while ((double)cap * 0.5 < (double)per_part * grow_factor_) cap <<= 1;
             p.uniq = 0;
             p.cap = cap;
@@ -673,7 +683,7 @@ class DistEngine final : public EngineBase {
             }
             init_counters(p);
             if (use_head) continue;  // the replicated head seeds the partitions (run_head)
-            insert_roots_part<M><<<1, 64, 0, stream_>>>(p.view(), dinit.p, (u32)k, p.id, T_, p.arena.p, p.apar.p, dn.p, p.lc);
+            insert_roots_part<M><<<1, 64, 0, stream_>>>(m_, p.view(), dinit.p, (u32)k, p.id, T_, p.arena.p, p.apar.p, dn.p, p.lc);
             u32 n0 = 0;
             SR_HIP(hipMemcpyAsync(&n0, dn.p, 4, hipMemcpyDeviceToHost, stream_));
             SR_HIP(hipStreamSynchronize(stream_));
@@ -897,7 +907,7 @@ class DistEngine final : public EngineBase {
     void run_head(const std::vector<u64>& rev, int k, u64& unique_total) {
         Part& p0 = parts_[0];
         const u64 cap_states = head_max_ * (u64)(D_ + 4) * 2 + 4096;
-        u64 hcap = 1u << 12;
+        u64 hcap = std::max<u64>(1u << 12, min_table_cap(m_));
         while ((double)hcap * 0.5 < (double)cap_states) hcap <<= 1;
         if (hkeys_.n < hcap) hkeys_.alloc(o_.device, hcap);
         if (harena_.n < cap_states * W) {
@@ -905,12 +915,12 @@ class DistEngine final : public EngineBase {
             hpar_.alloc(o_.device, cap_states);
         }
         SR_HIP(hipMemsetAsync(hkeys_.p, 0, hcap * 8, stream_));
-        const TableView hv{hkeys_.p, nullptr, hcap - 1};
+        const TableView hv = make_table_view(m_, hkeys_.p, nullptr, hcap);
         hlstart_.assign(1, 0);
         SR_HIP(hipMemcpyAsync(harena_.p, rev.data(), rev.size() * 8, hipMemcpyHostToDevice, stream_));
         SR_HIP(hipMemsetAsync(hpar_.p, 0xff, (size_t)k * 4, stream_));
         init_counters(p0);
-        insert_roots<M><<<blocks_for(k, 64), 64, 0, stream_>>>(hv, harena_.p, (u32)k, p0.lc);
+        insert_roots<M><<<blocks_for(k, 64), 64, 0, stream_>>>(m_, hv, harena_.p, (u32)k, p0.lc);
         u32 und = (1u << M::NPROPS) - 1;
         eval_roots<M><<<blocks_for(k, 64), 64, 0, stream_>>>(m_, harena_.p, (u32)k, p0.lc, und);
         p0.seq++;
@@ -993,7 +1003,7 @@ class DistEngine final : public EngineBase {
             while ((double)total > 0.5 * (double)p.cap) grow_table(p);
             ensure_arena(p, n + n / 4 + 4096, 0);
             SR_HIP(hipMemsetAsync(cnt.p, 0, 8, stream_));
-            take_owned<M><<<blocks_for(total, 256), 256, 0, stream_>>>(harena_.p, (u32)total, (u32)hlstart_[level], p.id, T_,
+            take_owned<M><<<blocks_for(total, 256), 256, 0, stream_>>>(m_, harena_.p, (u32)total, (u32)hlstart_[level], p.id, T_,
                                                                       p.view(), p.arena.p, p.apar.p, (u32)p.arena_cap, cnt.p,
                                                                       p.lc);
             SR_HIP(hipGetLastError());

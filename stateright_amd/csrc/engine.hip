@@ -19,7 +19,6 @@
 #include "../../include/stateright_gpu.h"
 #include "device.hpp"
 #include "kernels.hpp"
-#include "kernels_bucket.hpp"
 #include "dgraph.hpp"
 #include "paxos.hpp"
 
@@ -92,10 +91,13 @@ class Engine final : public EngineBase {
         // Internal tuning knobs (not part of the ABI): successors per lane per probe round and
         // the visited-set load factor the capacity hint is sized for.
         if (const char* e = std::getenv("SR_PROBE_BATCH")) probe_batch_ = std::atoi(e);
-        if (const char* e = std::getenv("SR_TABLE_LOAD")) table_load_ = std::atof(e);
+        if (const char* e = std::getenv("SR_TABLE_LOAD")) table_load_ = std::atof(e), load_env_ = true;
         if (const char* e = std::getenv("SR_PROBE_LOAD")) probe_load_ = std::atoi(e);
         if (const char* e = std::getenv("SR_PPW_LOG2")) ppw_env_ = std::atoi(e);
         if (const char* e = std::getenv("SR_FILTER_LOG2")) filt_log2_ = (u32)std::atoi(e);
+        // The LDS duplicate filter compares fingerprints: exact only in fingerprint mode (one-word
+        // states); an exact quotient-mode table (multi-word states with a key) runs without it.
+        if (make_table_view(m_, nullptr, nullptr, min_table_cap(m_)).qbits) filt_log2_ = 0;
         if (const char* e = std::getenv("SR_PIPELINE")) pipeline_ = std::atoi(e) != 0;
         if (const char* e = std::getenv("SR_QUERY_LOG2")) query_mask_ = (1ull << std::atoi(e)) - 1;
         if (const char* e = std::getenv("SR_GRID_MAX")) grid_max_ = (u32)std::max(0, std::atoi(e));  // <= 0: unset
@@ -317,7 +319,7 @@ class Engine final : public EngineBase {
     }
 
   private:
-    TableView view() const { return TableView{keys_.p, fifo_ ? meta_.p : nullptr, cap_ - 1}; }
+    TableView view() const { return make_table_view(m_, keys_.p, fifo_ ? meta_.p : nullptr, cap_); }
 
     void alloc_table(u64 cap) {
         cap_ = cap;
@@ -335,13 +337,13 @@ class Engine final : public EngineBase {
         DBuf<u64> ok, om;
         ok.swap(keys_);
         if (fifo_) om.swap(meta_);
-        TableView from{ok.p, fifo_ ? om.p : nullptr, cap_ - 1};
+        TableView from = make_table_view(m_, ok.p, fifo_ ? om.p : nullptr, cap_);
         u64 old_cap = cap_;
         alloc_table(cap_ * 2);
         rehash<<<blocks_for(old_cap, 256), 256, 0, stream_>>>(from, old_cap, view(), lc_d_);
         SR_HIP(hipGetLastError());
         if (cand && cand_n) {
-            remap_slots<<<blocks_for(cand_n, 256), 256, 0, stream_>>>(cand, cand_n, ok.p, view());
+            remap_slots<<<blocks_for(cand_n, 256), 256, 0, stream_>>>(cand, cand_n, from, view());
             SR_HIP(hipGetLastError());
         }
         SR_HIP(hipStreamSynchronize(stream_));
@@ -452,8 +454,12 @@ class Engine final : public EngineBase {
         launch_frontier.clear();
 
         // Visited set sized for <= table_load_ load at the hinted unique count.
-        u64 cap = (u64)(1u << 20) * grow_factor_;
-        if (o_.capacity_hint) while ((double)cap * table_load_ < (double)o_.capacity_hint * grow_factor_) cap <<= 1;
+        u64 cap = std::max<u64>((u64)(1u << 20) * grow_factor_, min_table_cap(m_));
+        // Hints beyond 2^31 states (increment_lock N=12: 5.2e9) size the table for <= 0.75 load and
+        // the arena with 30% slack, so that table + arena fit one MI355X's 288 GB.
+        const bool huge = o_.capacity_hint > (1ull << 31);
+        const double load = huge && !load_env_ ? 0.75 : table_load_;
+        if (o_.capacity_hint) while ((double)cap * load < (double)o_.capacity_hint * grow_factor_) cap <<= 1;
         ratio_ = (double)D_;
         en_ratio_ = std::max(1.0, (double)D_ / 2.0);
         alloc_table(cap);
@@ -469,13 +475,14 @@ class Engine final : public EngineBase {
         arena_cap_ = 0;
         // hinted: room for every state plus one level's worth of planning slack (a regrowth copies
         // the whole arena mid-run)
-        ensure_arena(std::max<u64>(1u << 16, (o_.capacity_hint + o_.capacity_hint / 2 + 1024) * grow_factor_), 0);
+        const u64 slack = huge ? o_.capacity_hint / 10 * 3 : o_.capacity_hint / 2;
+        ensure_arena(std::max<u64>(1u << 16, (o_.capacity_hint + slack + 1024) * grow_factor_), 0);
         lstart_.assign({0, (u64)k});
         lvisited_.clear();
         SR_HIP(hipMemcpyAsync(arena_.p, rev.data(), rev.size() * sizeof(u64), hipMemcpyHostToDevice, stream_));
         SR_HIP(hipMemsetAsync(apar_.p, 0xff, (size_t)k * sizeof(u32), stream_));
         init_counters();
-        insert_roots<M><<<blocks_for(k, 64), 64, 0, stream_>>>(view(), arena_.p, (u32)k, lc_d_);
+        insert_roots<M><<<blocks_for(k, 64), 64, 0, stream_>>>(m_, view(), arena_.p, (u32)k, lc_d_);
         eval_roots<M><<<blocks_for(k, 64), 64, 0, stream_>>>(m_, arena_.p, (u32)k, lc_d_, ((1u << M::NPROPS) - 1) & ~emask_);
         if (emask_) fill_u32<<<blocks_for(k, 64), 64, 0, stream_>>>(aeb_.p, (u32)k, emask_);  // bfs.rs:52-60
         u32 sq = next_seq();
@@ -758,9 +765,6 @@ class Engine final : public EngineBase {
         const u32 sq = next_seq();
         const u64 nbase = fbase + (dev_n ? 0 : n);  // start of the next level (dev_n: + n on the device)
         const u32 ncap = (u32)std::min<u64>(arena_cap_ - nbase, 0xffffffffu);
-        if constexpr (W == 1) {
-            if (bucket_min_ && shape >= bucket_min_) return launch_bucketed(fbase, n, dev_n, shape, undiscovered, sq, nbase, ncap);
-        }
         const u32 ppw_log2 = ppw_env_ >= 0 ? (u32)ppw_env_ : ppw_for(shape);
         const u32 grid = std::min(expand_grid_cap(), std::max<u32>(1, blocks_for((shape + (1u << ppw_log2) - 1) >> ppw_log2, 4)));
         timed([&] {
@@ -776,44 +780,6 @@ class Engine final : public EngineBase {
             }
         }, n);
         return sq;
-    }
-
-    // A big level (one-word states, FAST order) as expand_bucket + bucket_insert (kernels_bucket.hpp):
-    // B buckets sized so that a bucket's distinct states fit its LDS set (~1/3 load), regions sized
-    // from the successor estimate (a record that finds no room takes the direct path).
-    u32 launch_bucketed(u64 fbase, u32 n, bool dev_n, u64 shape, u32 undiscovered, u32 sq, u64 nbase, u32 ncap) {
-        const double est_new = (double)shape * std::max(ratio_, 0.5) * 1.15 + 1024.0;
-        u32 blog2 = 8;
-        while ((1u << blog2) < BK_MAXB && est_new / (double)(1u << blog2) > (double)BK_QS * 0.85) ++blog2;
-        const u32 B = 1u << blog2;
-        const double est_rec = (double)shape * en_ratio_ * 1.25 + 4096.0;  // an upper estimate (self-loops included)
-        const u32 nb = bk_blocks_;  // persistent grid: each block flushes thousands of records at a time
-        const u32 rcap = (u32)std::min<double>(est_rec / (double)(B * nb) * 1.5 + 32.0, 1u << 30);
-        ensure_buckets((u64)B * nb * rcap);
-        BucketView bk{bst_.p, bpar_.p, bcur_.p, rcap, blog2, nb};
-        const u32 ppw_log2 = 5;
-        const u32 grid = nb;
-        timed([&] {
-            expand_bucket<M><<<grid, 256, 0, stream_>>>(m_, arena_.p + fbase * W, 0u, n, view(), bk, arena_.p + nbase * W,
-                                                        apar_.p + nbase, ncap, lc_d_, undiscovered, ppw_log2, dev_n ? 1u : 0u);
-            SR_HIP(hipGetLastError());
-            bucket_insert<M><<<B, 1024, 0, stream_>>>(m_, view(), bk, arena_.p + nbase * W, apar_.p + nbase, ncap, lc_d_,
-                                                      undiscovered, hcd(sq), sq, 1u, dev_n ? 1u : 0u);
-        });
-        stats.bucketed_levels++;
-        return sq;
-    }
-
-    // Bucket regions for `records` records; grown only between levels (a stream synchronisation:
-    // launched levels may still read the old buffers).
-    void ensure_buckets(u64 records) {
-        if (!bcur_.p) bcur_.alloc(o_.device, (size_t)BK_MAXB * BK_MAXNB);
-        if (bcap_ >= records) return;
-        SR_HIP(hipStreamSynchronize(stream_));
-        const u64 cap = std::max<u64>(records, bcap_ * 2);
-        bst_.alloc(o_.device, cap);
-        bpar_.alloc(o_.device, cap);
-        bcap_ = cap;
     }
 
     // disc[p].fp from the discovering state in the arena (after the level loop).
@@ -978,18 +944,12 @@ class Engine final : public EngineBase {
     double ratio_ = 1.0;        // new states per expanded parent in the last level
     double en_ratio_ = 8.0;     // enabled action slots per expanded parent in the last level
     double table_load_ = 0.5;
+    bool load_env_ = false;
     Ctx* ctx_ = nullptr;
     hipStream_t stream_ = nullptr;
     HostCounters lc_{};  // host copy of the last published counters
     LevelCounters* lc_d_ = nullptr;
     u64 cap_ = 0;
-    DBuf<u64> bst_;              // bucketed levels: bucket regions (states, parent ranks, cursors)
-    DBuf<u32> bpar_, bcur_;
-    u64 bcap_ = 0;
-    u32 bk_blocks_ = std::getenv("SR_BK_BLOCKS") ? (u32)std::atoi(std::getenv("SR_BK_BLOCKS")) : 512;
-    // Bucketed big levels are OPT-IN (SR_BUCKET_MIN = frontier size from which a level is bucketed):
-    // measured slower than expand_fast on 2pc N=9/10 ("bucketed levels").
-    u64 bucket_min_ = std::getenv("SR_BUCKET_MIN") ? std::strtoull(std::getenv("SR_BUCKET_MIN"), nullptr, 10) : 0;
     DBuf<u64> keys_, meta_;      // visited set
     DBuf<u64> arena_;            // BFS tree: every level's states in visit order
     DBuf<u32> apar_;             // parent rank (in the previous level) of each arena state
@@ -1360,6 +1320,41 @@ int32_t sr_hip_runtime_version(int32_t* runtime, int32_t* compiled) {
     if (hipRuntimeGetVersion(&v) != hipSuccess) return SR_ERR_HIP;
     if (runtime) *runtime = v;
     if (compiled) *compiled = HIP_VERSION;
+    return SR_OK;
+}
+
+int32_t sr_selftest_tables(void) {
+    // qperm is a bijection on B bits (exhaustive for small B)
+    for (u32 B = 1; B <= 18; ++B) {
+        std::vector<u8> seen(1u << B, 0);
+        for (u64 x = 0; x < (1ull << B); ++x) {
+            const u64 y = (u64)qperm(x, B);
+            if (y >> B || seen[y]) {
+                set_error("qperm is not a bijection on " + std::to_string(B) + " bits");
+                return SR_ERR_ARG;
+            }
+            seen[y] = 1;
+        }
+    }
+    // quotient slot values decode to the key at every displacement (B = 89, k = 33: increment_lock
+    // N=12's table; B = 68, k = 20)
+    const u32 cases[][2] = {{89, 33}, {68, 20}, {82, 26}, {120, 64}};
+    u64 r = 0x243F6A8885A308D3ull;
+    for (auto& c : cases) {
+        TableView t{nullptr, nullptr, (c[1] >= 64 ? ~0ull : (1ull << c[1]) - 1), c[0] - c[1], 64 - (c[0] - c[1]), c[0]};
+        for (int i = 0; i < 100000; ++i) {
+            r = fmix64(r + 0x9E3779B97F4A7C15ull);
+            const u64 r2 = fmix64(r ^ 0xABCDEFull);
+            const u128 key = ((u128)r2 << 64 | r) & (((u128)1 << c[0]) - 1);
+            const u128 h = qperm(key, c[0]);
+            const ProbeKey pk = quot_probe(t, h);
+            const u64 d = r2 % 200;
+            if (quot_decode(t, (pk.home + d) & t.mask, pk.tag + d) != h || pk.home > t.mask || (pk.tag & ((1ull << t.dbits) - 1)) != 1) {
+                set_error("quotient slot encode/decode mismatch at B=" + std::to_string(c[0]));
+                return SR_ERR_ARG;
+            }
+        }
+    }
     return SR_OK;
 }
 

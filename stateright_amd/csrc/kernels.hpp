@@ -36,11 +36,97 @@ constexpr int MAX_PARTS = 64;  // visited-set partitions (one per GPU, or virtua
 
 enum ErrBits { ERR_TABLE_FULL = 1, ERR_FRONTIER_OVERFLOW = 2 };
 
+// Two slot encodings ("Visited set"):
+//  * fingerprint mode (qbits == 0): a slot holds the 64-bit fingerprint. Exact for one-word states
+//    (fingerprint<1> is a bijection); a 64-bit hash for wider states, like the reference's own
+//    visited set (DashMap keyed by a 64-bit ahash fingerprint, src/checker/bfs.rs:26,245-247).
+//  * quotient mode (qbits > 0, models with a packed key of B = bbits <= 120 bits, `qkey`): the key
+//    goes through a bijection on B bits (qperm); its top k = log2(cap) bits are the HOME slot and
+//    the slot stores the other qbits = B - k bits (the remainder) above dbits = 64 - qbits bits
+//    holding 1 + the linear-probe displacement from home. A slot value determines the key exactly,
+//    so the visited set is exact at 8 bytes per slot, for states far wider than 64 bits.
 struct TableView {
     u64* keys;
     u64* meta;
     u64 mask;
+    u32 qbits = 0;  // quotient mode: remainder bits per slot (0: fingerprint mode)
+    u32 dbits = 0;  // quotient mode: displacement bits (64 - qbits)
+    u32 bbits = 0;  // quotient mode: key bits B
 };
+
+// Where a key's probe sequence starts, and the value its slot holds at displacement 0; at
+// displacement d the slot is (home + d) & mask and the value tag + d * step (step = 1 in quotient
+// mode, 0 in fingerprint mode).
+struct ProbeKey {
+    u64 home;
+    u64 tag;
+};
+
+using u128 = unsigned __int128;
+
+// A bijection on B-bit integers (B <= 128): a 4-round unbalanced Feistel network over the top
+// B - B/2 and the low B/2 bits (every round is invertible whatever its round function).
+SR_HD u128 qperm(u128 x, u32 B) {
+    const u32 hb = B / 2, ab = B - hb;
+    const u64 mb = hb >= 64 ? ~0ull : (1ull << hb) - 1, ma = ab >= 64 ? ~0ull : (1ull << ab) - 1;
+    u64 b = (u64)x & mb, a = (u64)(x >> hb) & ma;
+    b ^= fmix64(a * 0x9E3779B97F4A7C15ull + 0x2545F4914F6CDD1Dull) & mb;
+    a ^= fmix64(b * 0xC2B2AE3D27D4EB4Full + 0x165667B19E3779F9ull) & ma;
+    b ^= fmix64(a * 0xD6E8FEB86659FD93ull + 0x94D049BB133111EBull) & mb;
+    a ^= fmix64(b * 0xBF58476D1CE4E5B9ull + 0x7F4A7C159E3779B9ull) & ma;
+    return ((u128)a << hb) | b;
+}
+
+SR_HD u64 probe_step(const TableView& t) { return t.qbits ? 1ull : 0ull; }
+SR_HD ProbeKey fp_probe(const TableView& t, u64 fp) { return ProbeKey{fp & t.mask, fp}; }
+SR_HD ProbeKey quot_probe(const TableView& t, u128 h) {
+    return ProbeKey{(u64)(h >> t.qbits), (((u64)h & ((1ull << t.qbits) - 1)) << t.dbits) | 1ull};
+}
+// Quotient mode: the permuted key held by slot i with value v.
+SR_HD u128 quot_decode(const TableView& t, u64 i, u64 v) {
+    const u64 d = (v & ((1ull << t.dbits) - 1)) - 1;
+    return ((u128)((i - d) & t.mask) << t.qbits) | (v >> t.dbits);
+}
+// Slot value of a key in `from` re-expressed for `to` (rehash into a larger table).
+SR_HD ProbeKey reprobe(const TableView& from, const TableView& to, u64 i, u64 v) {
+    return from.qbits ? quot_probe(to, quot_decode(from, i, v)) : fp_probe(to, v);
+}
+
+// Host: the view of a table of `cap` (a power of two) slots for model M. Quotient mode whenever
+// the model packs its states into a key (qkey) whose remainder fits a slot with >= 8 displacement
+// bits; min_table_cap keeps every table of such a model in that mode from the start (a
+// fingerprint cannot be turned back into a key when the table grows).
+template <class M>
+inline TableView make_table_view(const M& m, u64* keys, u64* meta, u64 cap) {
+    TableView v{keys, meta, cap - 1};
+    if constexpr (has_qkey<M>::value && M::W >= 2) {
+        const u32 B = (u32)m.qkey_bits();
+        u32 k = 0;
+        while ((1ull << k) < cap) ++k;
+        if (B <= 120 && B > k && B - k <= 56) {
+            v.qbits = B - k;
+            v.dbits = 64 - v.qbits;
+            v.bbits = B;
+        }
+    }
+    return v;
+}
+template <class M>
+inline u64 min_table_cap(const M& m) {
+    if constexpr (has_qkey<M>::value && M::W >= 2) {
+        const int B = m.qkey_bits();
+        if (B > 56 && B <= 96) return 1ull << (B - 56);
+    }
+    return 1;
+}
+
+template <class M>
+SR_HD ProbeKey probe_key(const M& m, const TableView& t, const u64* s) {
+    if constexpr (has_qkey<M>::value && M::W >= 2) {
+        if (t.qbits) return quot_probe(t, qperm(m.qkey(s), t.bbits));
+    }
+    return fp_probe(t, fingerprint<M::W>(s));
+}
 
 constexpr u32 NO_PARENT = 0xffffffffu;
 
@@ -182,13 +268,16 @@ __device__ __forceinline__ u64 probe_load(const u64* p) {
     else return *p;
 }
 
-// Find `key` or claim a vacant slot for it, starting at slot i whose key `cur` was already loaded.
-// Returns the slot; *is_new tells whether we claimed it.
+// Find key k or claim a vacant slot for it, starting at its home slot whose value `cur` was
+// already loaded. Returns the slot; *is_new tells whether we claimed it.
 // *probes / *cas (optional) count the further slot loads and the CAS attempts.
 template <int POL = 0>
-__device__ __forceinline__ u64 find_or_claim_from(const TableView& t, u64 key, u64 i, u64 cur, bool* is_new, u32* err,
-                                                  u32* probes = nullptr, u32* cas = nullptr) {
-    for (int probe = 0; probe < MAX_PROBE; ++probe) {
+__device__ __forceinline__ u64 find_or_claim_from(const TableView& t, const ProbeKey& k, u64 cur, bool* is_new,
+                                                  u32* err, u32* probes = nullptr, u32* cas = nullptr) {
+    const u64 step = probe_step(t);
+    const int limit = step && t.dbits < 17 ? (int)((1u << t.dbits) - 2) : MAX_PROBE;
+    u64 i = k.home, key = k.tag;
+    for (int probe = 0; probe < limit; ++probe) {
         if (cur == key) {
             *is_new = false;
             return i;
@@ -207,6 +296,7 @@ __device__ __forceinline__ u64 find_or_claim_from(const TableView& t, u64 key, u
             }
         }
         i = (i + 1) & t.mask;
+        key += step;
         cur = probe_load<POL>(&t.keys[i]);
         if (probes) ++*probes;
     }
@@ -215,19 +305,20 @@ __device__ __forceinline__ u64 find_or_claim_from(const TableView& t, u64 key, u
     return ~0ull;
 }
 
-__device__ __forceinline__ u64 find_or_claim(const TableView& t, u64 key, bool* is_new, u32* err) {
-    u64 i = key & t.mask;
-    return find_or_claim_from(t, key, i, t.keys[i], is_new, err);
+__device__ __forceinline__ u64 find_or_claim(const TableView& t, const ProbeKey& k, bool* is_new, u32* err) {
+    return find_or_claim_from(t, k, t.keys[k.home], is_new, err);
 }
 
-// Lookup only (path reconstruction).
-__device__ __forceinline__ u64 find_slot(const TableView& t, u64 key) {
-    u64 i = key & t.mask;
+// Lookup only.
+__device__ __forceinline__ u64 find_slot(const TableView& t, const ProbeKey& k) {
+    const u64 step = probe_step(t);
+    u64 i = k.home, key = k.tag;
     for (int probe = 0; probe < MAX_PROBE; ++probe) {
         u64 cur = t.keys[i];
         if (cur == key) return i;
         if (cur == 0) return ~0ull;
         i = (i + 1) & t.mask;
+        key += step;
     }
     return ~0ull;
 }
@@ -279,13 +370,13 @@ __device__ __forceinline__ bool same_state(const u64* a, const u64* b) {
 
 // Insert the (distinct) init states with parent None (`generated.insert(fp, None)`, bfs.rs:47-51).
 template <class M>
-__global__ void insert_roots(TableView t, const u64* states, u32 n, LevelCounters* lc) {
+__global__ void insert_roots(M m, TableView t, const u64* states, u32 n, LevelCounters* lc) {
     u32 r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= n) return;
     u64 s[M::W];
     load_state<M::W>(states, r, s);
     bool is_new;
-    u64 slot = find_or_claim(t, fingerprint<M::W>(s), &is_new, &lc->err);
+    u64 slot = find_or_claim(t, probe_key(m, t, s), &is_new, &lc->err);
     if (is_new) {
         if (t.meta) t.meta[slot] = 0;  // level 0
         atomicAdd(&lc->claims, 1u);
@@ -412,7 +503,8 @@ __global__ void __launch_bounds__(256) expand_fast(M m, const u64* __restrict__ 
         __syncthreads();
 
         for (u32 it = 0; it < total; it += 64 * PB) {
-            u64 ns[PB][W], key[PB], idx[PB], cur[PB];
+            u64 ns[PB][W], cur[PB];
+            ProbeKey pk[PB];
             u32 par[PB];
             bool ok[PB];
 #pragma unroll
@@ -449,17 +541,17 @@ __global__ void __launch_bounds__(256) expand_fast(M m, const u64* __restrict__ 
                         ok[j] = false;
                     }
                 }
-                key[j] = ok[j] ? fingerprint<W>(ns[j]) : 0;
-                idx[j] = key[j] & t.mask;
+                pk[j] = ok[j] ? probe_key(m, t, ns[j]) : ProbeKey{0, 0};
                 // Block-local duplicate filter: a direct-mapped LDS cache of the fingerprints this
                 // workgroup already sent to the visited set. Siblings' successors coincide often
                 // (commuting actions), and a hit is a duplicate of a state whose probe another lane
                 // of this block owns — counted, never probed again. A miss (or an eviction) only
                 // costs the ordinary probe, so the filter never changes which states are new.
+                // (Fingerprint mode only: the host turns it off for a quotient-mode table.)
                 if (fmask && ok[j]) {
-                    const u64 old = atomicExch(reinterpret_cast<unsigned long long*>(&filt[(u32)(key[j] >> 40) & fmask]),
-                                               (unsigned long long)key[j]);
-                    if (old == key[j]) {
+                    const u64 old = atomicExch(reinterpret_cast<unsigned long long*>(&filt[(u32)(pk[j].tag >> 40) & fmask]),
+                                               (unsigned long long)pk[j].tag);
+                    if (old == pk[j].tag) {
                         ++succ;
                         ok[j] = false;
                     }
@@ -467,7 +559,7 @@ __global__ void __launch_bounds__(256) expand_fast(M m, const u64* __restrict__ 
             }
 #pragma unroll
             for (int j = 0; j < PB; ++j) {
-                cur[j] = ok[j] ? probe_load<POL>(&t.keys[idx[j]]) : 0;
+                cur[j] = ok[j] ? probe_load<POL>(&t.keys[pk[j].home]) : 0;
                 if constexpr (STATS) probes += ok[j];
             }
             bool nw[PB];
@@ -476,8 +568,8 @@ __global__ void __launch_bounds__(256) expand_fast(M m, const u64* __restrict__ 
                 nw[j] = false;
                 if (!ok[j]) continue;
                 ++succ;
-                if (cur[j] == key[j]) continue;  // the common case: an already visited state
-                find_or_claim_from<POL>(t, key[j], idx[j], cur[j], &nw[j], &lc->err, STATS ? &probes : nullptr,
+                if (cur[j] == pk[j].tag) continue;  // the common case: an already visited state
+                find_or_claim_from<POL>(t, pk[j], cur[j], &nw[j], &lc->err, STATS ? &probes : nullptr,
                                         STATS ? &cas : nullptr);
             }
             // Append the new states of this round, aggregated per wave: one LDS atomic reserves the
@@ -566,7 +658,7 @@ __global__ void __launch_bounds__(256) expand_fifo(M m, const u64* __restrict__ 
             ++succ;
             if (same_state<M::W>(ns, s)) return;  // self-loop: the parent is visited already
             bool is_new;
-            u64 slot = find_or_claim(t, fingerprint<M::W>(ns), &is_new, &lc->err);
+            u64 slot = find_or_claim(t, probe_key(m, t, ns), &is_new, &lc->err);
             if (slot == ~0ull) return;
             claims += is_new;
             const u64 tag = lvl | ((u64)r * A + (u64)a);
@@ -728,18 +820,18 @@ __global__ void rehash(TableView from, u64 from_cap, TableView to, LevelCounters
     u64 k = from.keys[i];
     if (!k) return;
     bool is_new;
-    u64 slot = find_or_claim(to, k, &is_new, &lc->err);
+    u64 slot = find_or_claim(to, reprobe(from, to, i, k), &is_new, &lc->err);
     if (slot == ~0ull) return;
     if (to.meta) to.meta[slot] = from.meta[i];
 }
 
 // After a rehash: candidate slot indices of the old table -> slots of the new one.
-__global__ void remap_slots(u32* cand, u64 n, const u64* old_keys, TableView to) {
+__global__ void remap_slots(u32* cand, u64 n, TableView from, TableView to) {
     u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     u32 s = cand[i];
     if (s == CAND_NONE) return;
-    cand[i] = (u32)find_slot(to, old_keys[s]);
+    cand[i] = (u32)find_slot(to, reprobe(from, to, s, from.keys[s]));
 }
 
 // ---- exclusive scan of u32 counts (3-phase: tile sums, scan of sums, tile scan + carry) ----

@@ -146,7 +146,8 @@ __global__ void __launch_bounds__(256) expand_route(M m, u64* __restrict__ arena
         __syncthreads();
 
         for (u32 it = 0; it < total; it += 64 * PB) {
-            u64 ns[PB][W], key[PB], idx[PB], cur[PB];
+            u64 ns[PB][W], key[PB], cur[PB];
+            ProbeKey pk[PB];
             u32 par[PB], own[PB];
             bool ok[PB], rem[PB];
 #pragma unroll
@@ -181,8 +182,11 @@ __global__ void __launch_bounds__(256) expand_route(M m, u64* __restrict__ arena
                         ok[j] = false;
                     }
                 }
-                key[j] = ok[j] ? fingerprint<W>(ns[j]) : 0;
-                idx[j] = key[j] & t.mask;
+                // key = the fingerprint (owner, filter, sent cache); pk = the visited-set probe
+                // (the same value in fingerprint mode; the host turns the filter and the sent
+                // cache off for a quotient-mode table)
+                pk[j] = ok[j] ? probe_key(m, t, ns[j]) : ProbeKey{0, 0};
+                key[j] = !ok[j] ? 0 : t.qbits ? fingerprint<W>(ns[j]) : pk[j].tag;
                 if (fmask && ok[j]) {  // block-local duplicate filter (see expand_fast)
                     const u64 old = atomicExch(reinterpret_cast<unsigned long long*>(&filt[(u32)(key[j] >> 40) & fmask]),
                                                (unsigned long long)key[j]);
@@ -208,15 +212,15 @@ __global__ void __launch_bounds__(256) expand_route(M m, u64* __restrict__ arena
                 }
             }
 #pragma unroll
-            for (int j = 0; j < PB; ++j) cur[j] = (ok[j] && !rem[j]) ? probe_load<0>(&t.keys[idx[j]]) : 0;
+            for (int j = 0; j < PB; ++j) cur[j] = (ok[j] && !rem[j]) ? probe_load<0>(&t.keys[pk[j].home]) : 0;
             bool nw[PB];
 #pragma unroll
             for (int j = 0; j < PB; ++j) {
                 nw[j] = false;
                 if (!ok[j]) continue;
                 ++succ;
-                if (rem[j] || cur[j] == key[j]) continue;
-                find_or_claim_from<0>(t, key[j], idx[j], cur[j], &nw[j], &lc->err);
+                if (rem[j] || cur[j] == pk[j].tag) continue;
+                find_or_claim_from<0>(t, pk[j], cur[j], &nw[j], &lc->err);
             }
 #pragma unroll
             for (int j = 0; j < PB; ++j) {
@@ -378,7 +382,7 @@ __global__ void __launch_bounds__(256) insert_recv(M m, const u64* __restrict__ 
         for (int x = 0; x < W; ++x) ns[x] = recv[(u64)i * REC + x];
         const u64 pgid = PAR_SEARCH;
         bool is_new;
-        find_or_claim(t, fingerprint<W>(ns), &is_new, &lc->err);
+        find_or_claim(t, probe_key(m, t, ns), &is_new, &lc->err);
         if (is_new) {
             u32 kk = atomicAdd(&stage_n, 1u);
             if (kk < (u32)STAGE) {
@@ -481,7 +485,7 @@ __global__ void __launch_bounds__(256) insert_recv_lag(M m, const u64* __restric
                 for (int x = 0; x < W; ++x) ns[x] = rec[x];
                 const u64 pgid = PAR_SEARCH;
                 bool is_new;
-                find_or_claim(t, fingerprint<W>(ns), &is_new, &lc->err);
+                find_or_claim(t, probe_key(m, t, ns), &is_new, &lc->err);
                 if (is_new) {
                     const u32 kk = atomicAdd(&stage_n, 1u);  // < STAGE: one slot per thread
 #pragma unroll
@@ -547,7 +551,7 @@ __global__ void rows_publish(const u64* rows, u64* host_rows, u32 words, u32* ho
 
 // Init states owned by this partition (insert + level-0 properties), in visit order.
 template <class M>
-__global__ void insert_roots_part(TableView t, const u64* states, u32 n, u32 my_part, u32 nparts, u64* out, u64* out_par,
+__global__ void insert_roots_part(M m, TableView t, const u64* states, u32 n, u32 my_part, u32 nparts, u64* out, u64* out_par,
                                   u32* out_n, LevelCounters* lc) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;  // a handful of states: serial keeps init order
     u32 k = 0;
@@ -557,7 +561,7 @@ __global__ void insert_roots_part(TableView t, const u64* states, u32 n, u32 my_
         u64 key = fingerprint<M::W>(s);
         if (owner_of(key, nparts) != my_part) continue;
         bool is_new;
-        find_or_claim(t, key, &is_new, &lc->err);
+        find_or_claim(t, probe_key(m, t, s), &is_new, &lc->err);
         if (is_new) lc->claims += 1;
         store_state<M::W>(out, k, s);  // duplicates are queued too (bfs.rs:61-66)
         out_par[k] = ~0ull;
@@ -570,7 +574,7 @@ __global__ void insert_roots_part(TableView t, const u64* states, u32 n, u32 my_
 // visited set (cnt[1] = claims) and its share of the last head level [first_front, total) becomes
 // its first frontier (cnt[0] = size; parent PAR_SEARCH). Wave-aggregated counters.
 template <class M>
-__global__ void take_owned(const u64* __restrict__ hstates, u32 total, u32 first_front, u32 my_part, u32 nparts,
+__global__ void take_owned(M m, const u64* __restrict__ hstates, u32 total, u32 first_front, u32 my_part, u32 nparts,
                            TableView t, u64* __restrict__ arena, u64* __restrict__ apar, u32 arena_cap, u32* cnt,
                            LevelCounters* lc) {
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -581,7 +585,7 @@ __global__ void take_owned(const u64* __restrict__ hstates, u32 total, u32 first
         load_state<M::W>(hstates, i, s);
         const u64 fp = fingerprint<M::W>(s);
         mine = owner_of(fp, nparts) == my_part;
-        if (mine) find_or_claim(t, fp, &nw, &lc->err);
+        if (mine) find_or_claim(t, probe_key(m, t, s), &nw, &lc->err);
     }
     const u64 cm = __ballot(nw);
     if (cm && lane == __builtin_ctzll(cm)) atomicAdd(&cnt[1], (u32)__popcll(cm));

@@ -39,6 +39,14 @@ inline u32 model_emask(const M& m) {
     else return 0;
 }
 
+// Models whose states pack into a key of at most 120 bits (`qkey_bits()` and `qkey(s)`: an
+// injective packing of the state into an integer below 2^qkey_bits) can use the exact quotient
+// visited set (kernels.hpp TableView).
+template <class M, class = void>
+struct has_qkey : std::false_type {};
+template <class M>
+struct has_qkey<M, std::void_t<decltype(std::declval<const M&>().qkey_bits())>> : std::true_type {};
+
 // murmur3 fmix64: a bijection on u64 with fmix64(0) == 0.
 SR_HD u64 fmix64(u64 k) {
     k ^= k >> 33;
@@ -278,6 +286,13 @@ struct Increment {
     }
     int expectation(int) const { return ALWAYS; }
     const char* prop_name(int) const { return "fin"; }
+    // Exact key (quotient visited set) of the two-word layout: word 0 is full (4 + 6*10 = 64 bits),
+    // word 1 holds threads 10.. : the state is an integer below 2^(4 + 6n).
+    int qkey_bits() const { return 4 + 6 * n; }
+    SR_HD unsigned __int128 qkey(const u64* s) const {
+        if constexpr (W_ == 1) return s[0];
+        else return (unsigned __int128)s[0] | ((unsigned __int128)s[W_ - 1] << 64);
+    }
     int describe_width() const { return 1 + 2 * n; }
     void describe(const u64* s, i64* d) const {
         d[0] = (i64)getb(s, 0, 4);
@@ -343,6 +358,13 @@ struct IncrementLock {
     }
     int expectation(int) const { return ALWAYS; }
     const char* prop_name(int p) const { return p == 0 ? "fin" : "mutex"; }
+    // Exact key (quotient visited set): word 0 holds i, lock and threads 0..7 in its low 61 bits,
+    // word 1 threads 8.. : the state is the integer w0 | w1 << 61 below 2^(5 + 7n).
+    int qkey_bits() const { return 5 + 7 * n; }
+    SR_HD unsigned __int128 qkey(const u64* s) const {
+        if constexpr (W_ == 1) return s[0];
+        else return (unsigned __int128)s[0] | ((unsigned __int128)s[W_ - 1] << 61);
+    }
     int describe_width() const { return 2 + 2 * n; }
     void describe(const u64* s, i64* d) const {
         d[0] = (i64)getb(s, 0, 4);

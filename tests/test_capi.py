@@ -79,3 +79,11 @@ def test_paxos_action_codes_match_golden_encoding():
     assert ours == PAXOS_VALUE_CHOSEN_PATH
     with pytest.raises(ValueError):
         Paxos(2, server_count=5)
+
+
+def test_quotient_table_encoding_selftest():
+    # The exact visited set for multi-word states (quotient mode): the key permutation is a
+    # bijection (exhaustive up to 18 bits) and slot values decode to their keys (host-side check).
+    from stateright_amd import _native
+    lib = _native.load()
+    assert lib.sr_selftest_tables() == 0, _native.last_error()

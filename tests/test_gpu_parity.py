@@ -206,6 +206,33 @@ def test_increment_lock_large_closed_form(n):
     assert c.discoveries() == {}
 
 
+def test_increment_lock_12_exact_on_one_gpu():
+    # BASELINE.json configs[1] at its top (increment_lock, 12 threads): 5 208 245 377 states, depth
+    # 48, on ONE MI355X. An 89-bit state: a 64-bit fingerprint would expect ~0.74 colliding pairs
+    # at this size (n^2 / 2^65); the quotient visited set is exact (kernels.hpp TableView). Sized
+    # for 288 GB: 2^33 slots x 8 B = 64 GiB of table + ~6.8e9 x 20 B of BFS-tree arena.
+    n = 12
+    expect = 1 + 4 * sum(math.factorial(n) // math.factorial(n - k) for k in range(1, n + 1))
+    assert expect == 5_208_245_377
+    c = sr.IncrementLock(n).checker().capacity_hint(expect).spawn_bfs().join()
+    assert c.unique_state_count() == c.state_count() == expect
+    assert c.max_depth() == 4 * n
+    assert c.discoveries() == {}
+    assert c.stats()["table_capacity"] == 1 << 33
+
+
+@pytest.mark.parametrize("order", ["fifo", "fast"])
+def test_increment_lock_quotient_table_grows(order):
+    # A two-word state in a quotient-mode table that starts small (no hint) and doubles: the rehash
+    # decodes every slot back to its key (exact counts in both orders; FIFO also remaps the level's
+    # candidate slots).
+    n = 9
+    o = oracle(INCREMENT_LOCK, [n])
+    c = sr.IncrementLock(n).checker().order(order).spawn_bfs().join()
+    assert (c.unique_state_count(), c.state_count(), c.max_depth()) == (o.unique_state_count, o.state_count, o.max_depth)
+    assert c.stats()["rehashes"] > 0
+
+
 def test_2pc_10_fifo_matches_fast():
     # The exact-order pipeline at a BASELINE size: same counts as FAST, same closed forms.
     n = 10
@@ -250,19 +277,6 @@ def test_paxos_3_clients_matches_oracle(order):
     assert sorted(c.discoveries()) == ["value chosen"]
     if order == "fifo":
         assert c.discovery("value chosen").action_ids == o.discovery_actions("value chosen")
-
-
-@pytest.mark.parametrize("n", [6, 8, 9])
-def test_bucketed_levels_parity(n, monkeypatch):
-    # The opt-in bucketed path (kernels_bucket.hpp: expand into fingerprint buckets, LDS dedup per
-    # bucket, one probe per distinct state) on every level from 64 states up: counts are exact.
-    monkeypatch.setenv("SR_BUCKET_MIN", "64")
-    c = sr.TwoPhaseSys(n).checker().capacity_hint(6 ** n + 4 ** n + 2 ** n).spawn_bfs().join()
-    assert c.stats()["bucketed_levels"] > 0
-    assert c.unique_state_count() == 6 ** n + 4 ** n + 2 ** n
-    assert 3 * c.state_count() == 4 * n * 6 ** n + 3 * (n + 1) * 4 ** n + 3 * n * 2 ** n + 6
-    assert c.max_depth() == 3 * n + 1
-    assert sorted(c.discoveries()) == ["abort agreement", "commit agreement"]
 
 
 @pytest.mark.parametrize("grid", ["1", "2"])
