@@ -222,6 +222,37 @@ int32_t sr_selftest_tables(void);
 sr_bfs* sr_gpu_bfs_spawn_partitioned(sr_dist* comm, int32_t virtual_partitions, int32_t model_id,
                                      const int64_t* params, int32_t nparams, const sr_opts* opts);
 
+/* ---- GpuModel plugins: `impl Model` outside the registry (src/lib.rs:155-237) ----
+ * A user writes a GpuModel (the encoding concept of stateright_amd/csrc/models.hpp) and builds it
+ * with hipcc into its own shared library, instantiating the engine from
+ * include/stateright_gpu_model.hpp; the macro SR_GPU_PLUGIN(name, Model, make) there exports
+ * `const sr_plugin* sr_plugin_<name>(void)`. The engine library then runs it like a registered
+ * model. The plugin must be built from the same headers (abi). */
+#define SR_PLUGIN_ABI 2
+typedef struct sr_plugin {
+    uint32_t abi;         /* SR_PLUGIN_ABI of the headers the plugin was built with */
+    uint32_t opts_size;   /* sizeof(sr_opts) in that build */
+    const char* name;
+    /* Creates an engine object (comm = NULL and virtual_parts <= 1: one GPU; else partitioned). */
+    void* (*create)(const int64_t* params, int32_t nparams, const sr_opts* opts, void* comm, int32_t virtual_parts,
+                    char* err, int32_t errcap);
+    /* Fingerprint of a state given by its canonical description (needs the model's `undescribe`). */
+    int32_t (*fingerprint)(const int64_t* params, int32_t nparams, const int64_t* described, int32_t width,
+                           uint64_t* fp_out);
+} sr_plugin;
+
+sr_bfs* sr_gpu_bfs_spawn_plugin(const sr_plugin* plugin, const int64_t* params, int32_t nparams, const sr_opts* opts);
+sr_bfs* sr_gpu_bfs_spawn_plugin_partitioned(const sr_plugin* plugin, sr_dist* comm, int32_t virtual_partitions,
+                                            const int64_t* params, int32_t nparams, const sr_opts* opts);
+
+/* The engine's fingerprint of a state of a registered model, given by its canonical description
+ * (the integers sr_gpu_bfs_discovery_path / sr_gpu_bfs_visits return, describe_width of them):
+ * what a host-side `Path::from_fingerprints` (src/checker/path.rs:20-86) compares with the chain of
+ * sr_gpu_bfs_discovery. Host-only (no device needed). SR_ERR_UNSUPPORTED for models whose
+ * description does not determine the state (paxos: its history index is not described). */
+int32_t sr_model_fingerprint(int32_t model_id, const int64_t* params, int32_t nparams, const int64_t* described,
+                             int32_t width, uint64_t* fp_out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,25 +1,41 @@
-"""Builds the in-tree HIP engine library for gfx950 (no JIT cache: the .so travels with the repo)."""
+"""Builds the in-tree HIP engine library for gfx950 (no JIT cache: the .so travels with the repo),
+and the example GpuModel plugin (examples/plugins), which instantiates the same engine headers."""
 import os
 import subprocess
 
 HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
 SRC = os.path.join(HERE, "csrc", "engine.hip")
-DEPS = [os.path.join(HERE, "csrc", f) for f in ("engine.hip", "kernels.hpp", "kernels_dist.hpp", "dist.hpp",
-                                                "models.hpp", "device.hpp", "paxos.hpp", "dgraph.hpp")] + [
-    os.path.join(os.path.dirname(HERE), "include", "stateright_gpu.h")]
+CSRC = [os.path.join(HERE, "csrc", f) for f in ("engine.hip", "engine.hpp", "kernels.hpp", "kernels_dist.hpp",
+                                                 "dist.hpp", "models.hpp", "device.hpp", "paxos.hpp", "dgraph.hpp")]
+HEADERS = [os.path.join(ROOT, "include", f) for f in ("stateright_gpu.h", "stateright_gpu_model.hpp")]
 OUT = os.path.join(HERE, "libstateright_gpu.so")
+PLUGINS = {"sliding_puzzle": os.path.join(ROOT, "examples", "plugins", "sliding_puzzle.hip")}
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 
 
-def build(force=False, verbose=False):
-    if not force and os.path.exists(OUT) and all(os.path.getmtime(OUT) >= os.path.getmtime(d) for d in DEPS):
-        return OUT
+def plugin_path(name):
+    return os.path.join(ROOT, "examples", "plugins", f"lib{name}.so")
+
+
+def _hipcc(src, out, deps, force, verbose):
+    if not force and os.path.exists(out) and all(os.path.getmtime(out) >= os.path.getmtime(d) for d in deps):
+        return out
     cmd = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
-           "-o", OUT + ".tmp", SRC, "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
+           "-I", os.path.join(ROOT, "include"), "-o", out + ".tmp", src,
+           "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
     if verbose:
         print(" ".join(cmd))
     subprocess.check_call(cmd)
-    os.replace(OUT + ".tmp", OUT)
+    os.replace(out + ".tmp", out)
+    return out
+
+
+def build(force=False, verbose=False, plugins=True):
+    _hipcc(SRC, OUT, CSRC + HEADERS, force, verbose)
+    if plugins:
+        for name, src in PLUGINS.items():
+            _hipcc(src, plugin_path(name), CSRC + HEADERS + [src], force, verbose)
     return OUT
 
 

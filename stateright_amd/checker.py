@@ -232,7 +232,14 @@ class GpuBfsChecker:
         self._comm = comm
         params = list(model.params())
         arr = (ctypes.c_int64 * max(1, len(params)))(*params)
-        if comm is not None or partitions > 1:
+        plugin = getattr(model, "plugin", None)
+        if plugin is not None:  # a GpuModel compiled into its own library (stateright_amd.plugin)
+            if comm is not None or partitions > 1:
+                self._h = lib.sr_gpu_bfs_spawn_plugin_partitioned(plugin.handle, comm.handle if comm is not None else None,
+                                                                  partitions, arr, len(params), ctypes.byref(opts))
+            else:
+                self._h = lib.sr_gpu_bfs_spawn_plugin(plugin.handle, arr, len(params), ctypes.byref(opts))
+        elif comm is not None or partitions > 1:
             self._h = lib.sr_gpu_bfs_spawn_partitioned(comm.handle if comm is not None else None, partitions,
                                                        model.MODEL_ID, arr, len(params), ctypes.byref(opts))
         else:

@@ -1,0 +1,1022 @@
+// MI355X breadth-first model-checking engine: the host level loop over the HIP kernels, as a
+// header of templates over a GpuModel M (models.hpp), so that the engine library (engine.hip: the
+// compiled-in registry + the C ABI) and a user's own plugin build (include/stateright_gpu_model.hpp)
+// instantiate the same code.
+//
+// Replaces `BfsChecker` (src/checker/bfs.rs). The reference's T worker threads, job market and
+// 1500-state blocks (bfs.rs:75-152) become one host driver thread per GPU that runs the search
+// level by level; each level is one pass of HIP kernels over the frontier held in HBM (kernels.hpp).
+#pragma once
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <immintrin.h>
+#include <memory>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/stateright_gpu.h"
+#include "device.hpp"
+#include "kernels.hpp"
+
+namespace sr {
+
+
+using Clock = std::chrono::steady_clock;
+static double secs(Clock::time_point a, Clock::time_point b) { return std::chrono::duration<double>(b - a).count(); }
+
+static inline u32 blocks_for(u64 n, u32 bs) { return (u32)((n + bs - 1) / bs); }
+
+using Ctx = DeviceContext<LevelCounters, HostCounters>;
+using CtxPool = ContextPool<Ctx>;
+
+// Holds a pooled device context for the duration of a scope.
+struct CtxLease {
+    Ctx* c;
+    explicit CtxLease(int dev) : c(CtxPool::get().acquire(dev)) {}
+    ~CtxLease() { CtxPool::get().release(c); }
+};
+
+struct DiscoveryRec {
+    bool found = false;
+    u32 level = 0, rank = 0;
+    u64 fp = 0;
+};
+
+class EngineBase {
+  public:
+    virtual ~EngineBase() = default;
+    virtual void run() = 0;
+    virtual int nprops() const = 0;
+    virtual const char* prop_name(int p) const = 0;
+    virtual int expectation(int p) const = 0;
+    virtual int width() const = 0;
+    virtual std::string action_name(i64 id) const = 0;
+    virtual int chain(int p, std::vector<u64>& out) = 0;
+    virtual int path(int p, std::vector<i64>& actions, std::vector<i64>& states) = 0;
+    virtual std::vector<i64> visits() const = 0;
+    // Per visit (visit order): the visit index of its BFS-tree parent (-1 for an init state) and
+    // the canonical id of the first action leading there (-1 for an init state). Returns false if
+    // the engine keeps no visit record.
+    virtual bool visit_tree(std::vector<i64>&, std::vector<i64>&) const { return false; }
+    virtual i64 action_id_bound() const = 0;
+    virtual int init_count() const = 0;
+    virtual int replay(int init, const i64* ids, int n, std::vector<i64>& states, std::vector<int>& conds) const = 0;
+
+    std::atomic<u64> state_count{0}, unique{0};
+    std::atomic<u32> max_depth{0};
+    std::atomic<bool> finished{false};
+    bool reference_done = false;  // `is_done` (bfs.rs:307-311): explored all or discovered all
+    int status = SR_OK;
+    std::string error;
+    sr_stats stats{};
+    std::vector<DiscoveryRec> disc;
+    std::vector<double> launch_ms;    // per timed launch (profile=1), in launch order
+    std::vector<u64> launch_frontier; // the frontier each launch expanded (0 if unknown)
+};
+
+template <class M>
+class Engine final : public EngineBase {
+    static constexpr int W = M::W;
+
+  public:
+    Engine(M m, const sr_opts& o)
+        : m_(m), o_(o), A_((u32)m.max_actions()), D_((u32)m.max_out_degree()), emask_(model_emask(m)) {
+        disc.resize(M::NPROPS);
+        // Internal tuning knobs (not part of the ABI): successors per lane per probe round and
+        // the visited-set load factor the capacity hint is sized for.
+        if (const char* e = std::getenv("SR_PROBE_BATCH")) probe_batch_ = std::atoi(e);
+        if (const char* e = std::getenv("SR_TABLE_LOAD")) table_load_ = std::atof(e), load_env_ = true;
+        if (const char* e = std::getenv("SR_PROBE_LOAD")) probe_load_ = std::atoi(e);
+        if (const char* e = std::getenv("SR_PPW_LOG2")) ppw_env_ = std::atoi(e);
+        if (const char* e = std::getenv("SR_FILTER_LOG2")) filt_log2_ = (u32)std::atoi(e);
+        // The LDS duplicate filter compares fingerprints: exact only in fingerprint mode (one-word
+        // states); an exact quotient-mode table (multi-word states with a key) runs without it.
+        if (make_table_view(m_, nullptr, nullptr, min_table_cap(m_)).qbits) filt_log2_ = 0;
+        if (const char* e = std::getenv("SR_PIPELINE")) pipeline_ = std::atoi(e) != 0;
+        if (const char* e = std::getenv("SR_QUERY_LOG2")) query_mask_ = (1ull << std::atoi(e)) - 1;
+        if (const char* e = std::getenv("SR_GRID_MAX")) grid_max_ = (u32)std::max(0, std::atoi(e));  // <= 0: unset
+    }
+    ~Engine() override = default;
+
+    int nprops() const override { return M::NPROPS; }
+    const char* prop_name(int p) const override { return m_.prop_name(p); }
+    int expectation(int p) const override { return m_.expectation(p); }
+    int width() const override { return m_.describe_width(); }
+    std::string action_name(i64 id) const override { return m_.action_name(id); }
+
+    void run() override {
+        SR_HIP(hipSetDevice(o_.device));
+        CtxLease lease(o_.device);
+        bind(lease.c);
+        int order = o_.order;
+        if (order == SR_ORDER_AUTO) order = o_.target_state_count ? SR_ORDER_FIFO : SR_ORDER_FAST;
+        // `eventually` discoveries depend on the visit order (terminal-state overwrites), so such
+        // models always run in the reference's FIFO order.
+        if (emask_) order = SR_ORDER_FIFO;
+        bool order_dependent = run_with_restart(order);
+        if (order_dependent && o_.order == SR_ORDER_AUTO && order == SR_ORDER_FAST) {
+            // An early exit inside a level makes counts depend on the visit order: redo the
+            // check in the reference's exact FIFO order.
+            if (o_.verbose) std::fprintf(stderr, "[sr] early exit in FAST order; re-running in FIFO order\n");
+            run_with_restart(SR_ORDER_FIFO);
+        }
+        bind(nullptr);
+    }
+
+    // Capacity planning is optimistic (a chunk is sized for twice the previous level's growth, not
+    // for every successor being new). If a level ever outgrows it, the device reports a full table
+    // or arena and the check restarts from scratch in the pessimistic mode with larger buffers.
+    bool run_with_restart(int order) {
+        for (int attempt = 0;; ++attempt) {
+            try {
+                return run_order(order);
+            } catch (const Error& e) {
+                if (e.code != SR_ERR_CAPACITY || attempt >= 3) throw;
+                if (o_.verbose) std::fprintf(stderr, "[sr] %s; restarting with larger buffers\n", e.what());
+                pessimistic_ = true;
+                grow_factor_ *= 4;
+                (void)hipStreamSynchronize(stream_);
+                init_counters();
+            }
+        }
+    }
+
+    // `reconstruct_path` (src/checker/bfs.rs:314-342): the discovery's fingerprint chain, found by
+    // walking parent ranks back through the BFS-tree arena.
+    int chain(int p, std::vector<u64>& out) override {
+        out.clear();
+        if (p < 0 || p >= M::NPROPS || !disc[p].found) return 0;
+        SR_HIP(hipSetDevice(o_.device));
+        std::vector<u64> st;
+        tree_path(disc[p].level, disc[p].rank, st);
+        for (size_t i = 0; i < st.size() / W; ++i) out.push_back(fingerprint<W>(&st[i * W]));
+        return (int)out.size();
+    }
+
+    // States (W words each) from the init state down to (level, rank).
+    void tree_path(u32 level, u32 rank, std::vector<u64>& st) {
+        std::vector<u64> idx;
+        u64 r = rank;
+        for (int d = (int)level;; --d) {
+            u64 a = lstart_[d] + r;
+            idx.push_back(a);
+            if (d == 0) break;
+            u32 pr = 0;
+            SR_HIP(hipMemcpy(&pr, apar_.p + a, sizeof(u32), hipMemcpyDeviceToHost));
+            r = pr;
+        }
+        std::reverse(idx.begin(), idx.end());
+        st.resize(idx.size() * W);
+        for (size_t i = 0; i < idx.size(); ++i)
+            SR_HIP(hipMemcpy(&st[i * W], arena_.p + idx[i] * W, W * sizeof(u64), hipMemcpyDeviceToHost));
+    }
+
+    // `Path::from_fingerprints` (src/checker/path.rs:20-86) on the host copy of the GpuModel.
+    int path(int p, std::vector<i64>& actions, std::vector<i64>& states) override {
+        std::vector<u64> fps;
+        if (chain(p, fps) == 0) return -1;
+        const int wd = m_.describe_width();
+        u64 inits[8 * W];
+        int k = m_.init_states(inits);
+        std::vector<u64> cur;
+        for (int i = 0; i < k && cur.empty(); ++i)
+            if (fingerprint<W>(&inits[i * W]) == fps[0]) cur.assign(&inits[i * W], &inits[i * W] + W);
+        if (cur.empty()) throw Error(SR_ERR_NONDETERMINISM, "Unable to reconstruct a `Path`: no init state has the expected fingerprint");
+        auto emit = [&](const u64* s) {
+            size_t o = states.size();
+            states.resize(o + wd);
+            m_.describe(s, &states[o]);
+        };
+        for (size_t i = 1; i < fps.size(); ++i) {
+            u64 mask[M::MW];
+            m_.enabled(cur.data(), mask);
+            bool found = false;
+            for (int w = 0; w < M::MW && !found; ++w)
+                for (u64 bits = mask[w]; bits && !found; bits &= bits - 1) {
+                    int a = w * 64 + __builtin_ctzll(bits);
+                    u64 ns[W];
+                    if (!m_.apply(cur.data(), a, ns)) continue;
+                    if (fingerprint<W>(ns) == fps[i]) {
+                        emit(cur.data());
+                        actions.push_back(m_.action_id(cur.data(), a));
+                        cur.assign(ns, ns + W);
+                        found = true;
+                    }
+                }
+            if (!found)
+                throw Error(SR_ERR_NONDETERMINISM, "Unable to reconstruct a `Path`: " + std::to_string(i) +
+                                                       " previous state(s) reconstructed but no successor has the next fingerprint");
+        }
+        emit(cur.data());
+        return (int)actions.size();
+    }
+
+    i64 action_id_bound() const override { return m_.action_id_bound(); }
+    int init_count() const override {
+        u64 inits[8 * W];
+        return m_.init_states(inits);
+    }
+    int replay(int init, const i64* ids, int n, std::vector<i64>& states, std::vector<int>& conds) const override {
+        u64 inits[8 * W];
+        int k = m_.init_states(inits);
+        if (init < 0 || init >= k) return -1;
+        const int wd = m_.describe_width();
+        std::vector<u64> cur(&inits[init * W], &inits[init * W] + W);
+        auto emit = [&](const u64* s) {
+            size_t o = states.size();
+            states.resize(o + wd);
+            m_.describe(s, &states[o]);
+        };
+        for (int i = 0; i < n; ++i) {
+            u64 mask[M::MW];
+            m_.enabled(cur.data(), mask);
+            bool found = false;
+            for (int w = 0; w < M::MW && !found; ++w)
+                for (u64 bits = mask[w]; bits && !found; bits &= bits - 1) {
+                    int a = w * 64 + __builtin_ctzll(bits);
+                    if (m_.action_id(cur.data(), a) != ids[i]) continue;
+                    u64 ns[W];
+                    if (!m_.apply(cur.data(), a, ns)) continue;
+                    emit(cur.data());
+                    cur.assign(ns, ns + W);
+                    found = true;
+                }
+            if (!found) return -1;
+        }
+        emit(cur.data());
+        conds.assign(M::NPROPS, 0);
+        for (int p = 0; p < M::NPROPS; ++p) {
+            bool d = m_.discovers(p, cur.data());
+            conds[p] = m_.expectation(p) == SOMETIMES ? d : !d;
+        }
+        return n;
+    }
+
+    // The visitor's paths (src/checker/bfs.rs:187-189 builds `Path::from_fingerprints` of every
+    // popped state): each visited state's BFS-tree parent and the FIRST action, in `actions()`
+    // order, that leads from the parent to it (src/checker/path.rs:55-79).
+    bool visit_tree(std::vector<i64>& parent, std::vector<i64>& action) const override {
+        parent.clear();
+        action.clear();
+        std::vector<u64> prev_states;
+        i64 prev_base = 0;  // visit index of the previous level's first state
+        for (size_t d = 0; d < lvisited_.size(); ++d) {
+            const u64 nv = lvisited_[d];
+            std::vector<u64> st(nv * W);
+            std::vector<u32> par(nv);
+            if (nv) {
+                SR_HIP(hipMemcpy(st.data(), arena_.p + lstart_[d] * W, nv * W * sizeof(u64), hipMemcpyDeviceToHost));
+                SR_HIP(hipMemcpy(par.data(), apar_.p + lstart_[d], nv * sizeof(u32), hipMemcpyDeviceToHost));
+            }
+            const i64 base = (i64)parent.size();
+            for (u64 i = 0; i < nv; ++i) {
+                if (d == 0) {
+                    parent.push_back(-1);
+                    action.push_back(-1);
+                    continue;
+                }
+                const u64 pr = par[i];
+                if (pr >= prev_states.size() / W) throw Error(SR_ERR_NONDETERMINISM, "visit parent outside the visited prefix");
+                const u64* ps = &prev_states[pr * W];
+                const u64 want = fingerprint<W>(&st[i * W]);
+                u64 mask[M::MW];
+                m_.enabled(ps, mask);
+                i64 id = -1;
+                for (int w = 0; w < M::MW && id < 0; ++w)
+                    for (u64 bits = mask[w]; bits && id < 0; bits &= bits - 1) {
+                        const int a = w * 64 + __builtin_ctzll(bits);
+                        u64 ns[W];
+                        if (m_.apply(ps, a, ns) && fingerprint<W>(ns) == want) id = m_.action_id(ps, a);
+                    }
+                if (id < 0) throw Error(SR_ERR_NONDETERMINISM, "Unable to reconstruct a `Path` for a visited state");
+                parent.push_back(prev_base + (i64)pr);
+                action.push_back(id);
+            }
+            prev_states.swap(st);
+            prev_base = base;
+        }
+        return true;
+    }
+
+    std::vector<i64> visits() const override {
+        const int wd = m_.describe_width();
+        std::vector<u64> st;
+        for (size_t d = 0; d < lvisited_.size(); ++d) {
+            size_t o = st.size();
+            st.resize(o + lvisited_[d] * W);
+            if (lvisited_[d])
+                SR_HIP(hipMemcpy(&st[o], arena_.p + lstart_[d] * W, lvisited_[d] * W * sizeof(u64), hipMemcpyDeviceToHost));
+        }
+        std::vector<i64> out(st.size() / W * wd);
+        for (size_t i = 0; i < st.size() / W; ++i) m_.describe(&st[i * W], &out[i * wd]);
+        return out;
+    }
+
+  private:
+    TableView view() const { return make_table_view(m_, keys_.p, fifo_ ? meta_.p : nullptr, cap_); }
+
+    void alloc_table(u64 cap) {
+        cap_ = cap;
+        keys_.alloc(o_.device, cap);
+        SR_HIP(hipMemsetAsync(keys_.p, 0, cap * sizeof(u64), stream_));
+        if (fifo_) {
+            meta_.alloc(o_.device, cap);
+            SR_HIP(hipMemsetAsync(meta_.p, 0xff, cap * sizeof(u64), stream_));
+        }
+    }
+
+    // Doubles the visited set. In FIFO order the level's candidate slots (cand) are remapped to
+    // the new table, since the rehash moves every entry.
+    void grow_table(u32* cand = nullptr, u64 cand_n = 0) {
+        DBuf<u64> ok, om;
+        ok.swap(keys_);
+        if (fifo_) om.swap(meta_);
+        TableView from = make_table_view(m_, ok.p, fifo_ ? om.p : nullptr, cap_);
+        u64 old_cap = cap_;
+        alloc_table(cap_ * 2);
+        rehash<<<blocks_for(old_cap, 256), 256, 0, stream_>>>(from, old_cap, view(), lc_d_);
+        SR_HIP(hipGetLastError());
+        if (cand && cand_n) {
+            remap_slots<<<blocks_for(cand_n, 256), 256, 0, stream_>>>(cand, cand_n, from, view());
+            SR_HIP(hipGetLastError());
+        }
+        SR_HIP(hipStreamSynchronize(stream_));
+        stats.rehashes++;
+    }
+
+    // The BFS-tree arena holds every level's states (visit order) and their parent ranks; grows
+    // by copying the used prefix.
+    void ensure_arena(u64 states, u64 used) {
+        if (arena_cap_ >= states) return;
+        u64 cap = std::max<u64>(states, arena_cap_ * 2);
+        DBuf<u64> na;
+        DBuf<u32> np, ne;
+        na.alloc(o_.device, cap * W);
+        np.alloc(o_.device, cap);
+        if (emask_) ne.alloc(o_.device, cap);
+        if (used) {
+            SR_HIP(hipMemcpyAsync(na.p, arena_.p, used * W * sizeof(u64), hipMemcpyDeviceToDevice, stream_));
+            SR_HIP(hipMemcpyAsync(np.p, apar_.p, used * sizeof(u32), hipMemcpyDeviceToDevice, stream_));
+            if (emask_) SR_HIP(hipMemcpyAsync(ne.p, aeb_.p, used * sizeof(u32), hipMemcpyDeviceToDevice, stream_));
+        }
+        arena_.swap(na);
+        apar_.swap(np);
+        if (emask_) aeb_.swap(ne);
+        arena_cap_ = cap;
+        SR_HIP(hipStreamSynchronize(stream_));
+    }
+
+    void bind(Ctx* c) {
+        ctx_ = c;
+        stream_ = c ? c->stream : nullptr;
+        lc_d_ = c ? c->lc : nullptr;
+    }
+
+    // Device counters to their level-start values (once per run; afterwards the publishing
+    // workgroup of each level resets them).
+    void init_counters() {
+        LevelCounters z;
+        std::memset(&z, 0, sizeof(z));
+        for (auto& d : z.disc) d = ~0u;
+        SR_HIP(hipMemcpyAsync(lc_d_, &z, sizeof(z), hipMemcpyHostToDevice, stream_));
+        SR_HIP(hipStreamSynchronize(stream_));
+    }
+    u32 next_seq() { return ++ctx_->seq; }
+    HostCounters* hcd(u32 seq) const { return ctx_->hc_dev + (seq & 1); }  // device view of seq's mirror
+
+    // Waits until the launch tagged `seq` has published its counters to pinned host memory: a
+    // spin on one host word (no stream synchronisation, no copy), with a periodic stream query
+    // so that a failed launch cannot hang the host.
+    void wait_publish(u32 seq) {
+        volatile u32* flag = &ctx_->hc[seq & 1].seq;
+        for (u64 spin = 1;; ++spin) {
+            if (*flag == seq) break;
+            if ((spin & query_mask_) == 0) {
+                hipError_t e = hipStreamQuery(stream_);
+                if (e != hipSuccess && e != hipErrorNotReady) SR_HIP(e);
+                if (e == hipSuccess && *flag != seq) {
+                    if (*flag == seq) break;
+                    throw Error(SR_ERR_HIP, "launch finished without publishing its counters");
+                }
+            }
+            _mm_pause();
+        }
+        std::atomic_thread_fence(std::memory_order_acquire);
+        std::memcpy(&lc_, (const void*)&ctx_->hc[seq & 1], sizeof(lc_));
+        if (lc_.err & ERR_TABLE_FULL) throw Error(SR_ERR_CAPACITY, "visited set probe limit exceeded");
+        if (lc_.err & ERR_FRONTIER_OVERFLOW) throw Error(SR_ERR_CAPACITY, "frontier overflow");
+    }
+
+    // Launch bracketed by pooled events (profile=1); durations are summed once at the end of the
+    // run, so timing adds no synchronisation to the level loop.
+    template <class F>
+    void timed(F&& launch, u64 frontier = 0) {
+        size_t i = 2 * stats.expand_launches;
+        if (o_.profile) SR_HIP(hipEventRecord(ctx_->event(i), stream_));
+        launch();
+        SR_HIP(hipGetLastError());
+        if (o_.profile) SR_HIP(hipEventRecord(ctx_->event(i + 1), stream_));
+        stats.expand_launches++;
+        launch_frontier.push_back(frontier);
+    }
+    void collect_timing() {
+        if (!o_.profile || !stats.expand_launches) return;
+        SR_HIP(hipEventSynchronize(ctx_->event(2 * stats.expand_launches - 1)));
+        double ms = 0;
+        launch_ms.assign(stats.expand_launches, 0.0);
+        for (u64 i = 0; i < stats.expand_launches; ++i) {
+            float t = 0;
+            SR_HIP(hipEventElapsedTime(&t, ctx_->event(2 * i), ctx_->event(2 * i + 1)));
+            ms += t;
+            launch_ms[i] = t;
+        }
+        stats.expand_kernel_ms = ms;
+    }
+
+    // Returns true when the run stopped early inside a level in an order-dependent way.
+    bool run_order(int order) {
+        auto t_start = Clock::now();
+        fifo_ = order == SR_ORDER_FIFO;
+        state_count = 0;
+        unique = 0;
+        max_depth = 0;
+        for (auto& d : disc) d = DiscoveryRec{};
+        stats = sr_stats{};
+        stats.words_per_state = W;
+        stats.order_used = (u32)order;
+        launch_ms.clear();
+        launch_frontier.clear();
+
+        // Visited set sized for <= table_load_ load at the hinted unique count.
+        u64 cap = std::max<u64>((u64)(1u << 20) * grow_factor_, min_table_cap(m_));
+        // Hints beyond 2^31 states (increment_lock N=12: 5.2e9) size the table for <= 0.75 load and
+        // the arena with 30% slack, so that table + arena fit one MI355X's 288 GB.
+        const bool huge = o_.capacity_hint > (1ull << 31);
+        const double load = huge && !load_env_ ? 0.75 : table_load_;
+        if (o_.capacity_hint) while ((double)cap * load < (double)o_.capacity_hint * grow_factor_) cap <<= 1;
+        ratio_ = (double)D_;
+        en_ratio_ = std::max(1.0, (double)D_ / 2.0);
+        alloc_table(cap);
+
+        // Init states (bfs.rs:43-66): all of them are counted and queued (duplicates too), the
+        // visited set keeps distinct ones; `pending` pops from the back, so level 0 is visited in
+        // REVERSE init order.
+        std::vector<u64> inits(256 * W);
+        int k = m_.init_states(inits.data());
+        std::vector<u64> f0(inits.begin(), inits.begin() + k * W);
+        std::vector<u64> rev(k * W);
+        for (int i = 0; i < k; ++i) std::copy(&f0[i * W], &f0[i * W] + W, &rev[(k - 1 - i) * W]);
+        arena_cap_ = 0;
+        // hinted: room for every state plus one level's worth of planning slack (a regrowth copies
+        // the whole arena mid-run)
+        const u64 slack = huge ? o_.capacity_hint / 10 * 3 : o_.capacity_hint / 2;
+        ensure_arena(std::max<u64>(1u << 16, (o_.capacity_hint + slack + 1024) * grow_factor_), 0);
+        lstart_.assign({0, (u64)k});
+        lvisited_.clear();
+        SR_HIP(hipMemcpyAsync(arena_.p, rev.data(), rev.size() * sizeof(u64), hipMemcpyHostToDevice, stream_));
+        SR_HIP(hipMemsetAsync(apar_.p, 0xff, (size_t)k * sizeof(u32), stream_));
+        init_counters();
+        insert_roots<M><<<blocks_for(k, 64), 64, 0, stream_>>>(m_, view(), arena_.p, (u32)k, lc_d_);
+        eval_roots<M><<<blocks_for(k, 64), 64, 0, stream_>>>(m_, arena_.p, (u32)k, lc_d_, ((1u << M::NPROPS) - 1) & ~emask_);
+        if (emask_) fill_u32<<<blocks_for(k, 64), 64, 0, stream_>>>(aeb_.p, (u32)k, emask_);  // bfs.rs:52-60
+        u32 sq = next_seq();
+        publish_kernel<<<1, 64, 0, stream_>>>(lc_d_, hcd(sq), sq, 1, nullptr);
+        SR_HIP(hipGetLastError());
+        // FAST pipelined order: level 0 is enqueued before the host reads the roots' outcome (it is
+        // ignored if the roots already discover every property)
+        const bool pipelined = !fifo_ && !emask_ && !o_.target_state_count && M::NPROPS > 0 && pipeline_;
+        const u32 sq_level0 = pipelined ? launch_sync((u64)k, (1u << M::NPROPS) - 1) : 0u;
+        wait_publish(sq);
+        state_count = (u64)k;
+        unique = lc_.claims;
+
+        u32 undiscovered = (1u << M::NPROPS) - 1;
+        u64 n = (u64)k, popped_before = 0;
+        u32 level = 0;
+        bool order_dependent = false;
+        auto t_loop = Clock::now();
+        if (pipelined) order_dependent = pipeline_levels(n, sq_level0);
+        else for (;;) {
+            // 1. Discoveries among this level's states (evaluated when they were produced).
+            u32 newly = 0, max_rank = 0;
+            for (int p = 0; p < M::NPROPS; ++p)
+                if ((undiscovered >> p & 1) && lc_.disc[p] != ~0u) {
+                    newly |= 1u << p;
+                    max_rank = std::max(max_rank, lc_.disc[p]);
+                    disc[p].found = true;
+                    disc[p].level = level;
+                    disc[p].rank = lc_.disc[p];
+                    u64 s[W];
+                    SR_HIP(hipMemcpy(s, arena_.p + (lstart_[level] + lc_.disc[p]) * W, W * sizeof(u64), hipMemcpyDeviceToHost));
+                    disc[p].fp = fingerprint<W>(s);
+                }
+            // `eventually` properties: the first terminal candidate of each undiscovered one.
+            const u32 eund = undiscovered & emask_;
+            std::vector<u32> evf(M::NPROPS, ~0u);
+            DBuf<u32> tsat, evd;
+            if (emask_ && n) {
+                tsat.alloc(o_.device, n);
+                evd.alloc(o_.device, 2 * M::NPROPS);  // [first terminal candidate | last terminal + 1]
+                SR_HIP(hipMemsetAsync(evd.p, 0xff, M::NPROPS * sizeof(u32), stream_));
+                SR_HIP(hipMemsetAsync(evd.p + M::NPROPS, 0, M::NPROPS * sizeof(u32), stream_));
+                ev_scan<M><<<blocks_for(n, 256), 256, 0, stream_>>>(m_, cur(), aeb_.p + lstart_[level], (u32)n, eund,
+                                                                    emask_, tsat.p, evd.p);
+                SR_HIP(hipGetLastError());
+                SR_HIP(hipMemcpyAsync(evf.data(), evd.p, M::NPROPS * sizeof(u32), hipMemcpyDeviceToHost, stream_));
+                SR_HIP(hipStreamSynchronize(stream_));
+            }
+            u64 limit = n, visited = n;
+            bool stop = false;
+            if (M::NPROPS == 0) {
+                limit = 0;
+                visited = std::min<u64>(1, n);
+                stop = true;
+            } else if (undiscovered == 0) {
+                // Every property was discovered at a terminal state of the previous level: the next
+                // pop finds nothing to await and returns (bfs.rs:226).
+                limit = 0;
+                visited = std::min<u64>(1, n);
+                stop = true;
+                order_dependent = true;
+            } else {
+                // The first pop at which every property is discovered: always/sometimes ones at the
+                // pop of their discovering state, eventually ones right after their terminal state.
+                const u32 pop_und = undiscovered & ~emask_;
+                bool all = (newly & pop_und) == pop_und;
+                u64 at = newly ? (u64)max_rank : 0;
+                for (u32 e = eund; e; e &= e - 1) {
+                    const int p = __builtin_ctz(e);
+                    if (evf[p] == ~0u) all = false;
+                    else at = std::max<u64>(at, (u64)evf[p] + 1);
+                }
+                if (all && at < n) {
+                    // The pop of rank `at` finds every property discovered: check_block returns
+                    // without expanding it (bfs.rs:226) and the worker shuts down (bfs.rs:121-128).
+                    limit = at;
+                    visited = at + 1;
+                    stop = true;
+                    order_dependent = true;
+                }
+            }
+            undiscovered &= ~newly;
+
+            // 2. target_state_count: the reference checks it after each 1500-pop block (bfs.rs:113-135).
+            bool target_stop = false;
+            if (o_.target_state_count && state_count + limit * D_ >= o_.target_state_count) {
+                u64 lt = target_limit(n, popped_before, limit);
+                if (lt != ~0ull) {
+                    limit = lt;
+                    visited = lt;
+                    target_stop = true;
+                    stop = true;
+                    order_dependent = true;
+                }
+            }
+
+            lvisited_.push_back(visited);
+
+            // 3. Expand ranks [0, limit) (eventually: the bits passed on, terminal discoveries).
+            u64 produced = 0;
+            DBuf<u32> peb;
+            std::vector<u32> evl(M::NPROPS, 0);
+            if (emask_ && limit) {
+                peb.alloc(o_.device, limit);
+                ev_resolve<<<blocks_for(limit, 256), 256, 0, stream_>>>(tsat.p, aeb_.p + lstart_[level], (u32)limit, eund,
+                                                                       evd.p, peb.p, evd.p + M::NPROPS);
+                SR_HIP(hipGetLastError());
+                SR_HIP(hipMemcpyAsync(evl.data(), evd.p + M::NPROPS, M::NPROPS * sizeof(u32), hipMemcpyDeviceToHost, stream_));
+                SR_HIP(hipStreamSynchronize(stream_));
+            }
+            if (limit) {
+                produced = expand_level(level, n, limit, undiscovered & ~emask_, peb.p);
+            } else {
+                std::memset(&lc_, 0, sizeof(lc_));
+            }
+            for (int p = 0; p < M::NPROPS; ++p) {
+                if (!evl[p]) continue;  // discoveries.insert at a terminal state (bfs.rs:265-272)
+                disc[p].found = true;
+                disc[p].level = level;
+                disc[p].rank = evl[p] - 1;
+                u64 s[W];
+                SR_HIP(hipMemcpy(s, arena_.p + (lstart_[level] + evl[p] - 1) * W, W * sizeof(u64), hipMemcpyDeviceToHost));
+                disc[p].fp = fingerprint<W>(s);
+                undiscovered &= ~(1u << p);
+            }
+            state_count += lc_.successors;
+            unique += lc_.claims;
+            stats.successors += lc_.successors;
+            stats.probes += lc_.probes;
+            stats.cas += lc_.cas;
+            stats.algorithmic_bytes += limit * 8 * W + lc_.successors * 8 + (u64)lc_.claims * (16 + 8 * W);
+            stats.levels++;
+            if (produced) max_depth = level + 1;
+            if (o_.verbose)
+                std::fprintf(stderr, "[sr] level %u: frontier %llu expanded %llu succ %llu new %llu unique %llu cap %llu\n",
+                             level, (unsigned long long)n, (unsigned long long)limit,
+                             (unsigned long long)lc_.successors, (unsigned long long)produced,
+                             (unsigned long long)unique.load(), (unsigned long long)cap_);
+            popped_before += visited;
+            if (stop || produced == 0) {
+                if (target_stop) reference_done = false;  // the worker returns without waiting
+                else if (stop) reference_done = true;     // all properties discovered
+                else  // exhausted: the last (partial) block still checks the target (bfs.rs:129-135)
+                    reference_done = !(o_.target_state_count && state_count >= o_.target_state_count);
+                break;
+            }
+            lstart_.push_back(lstart_.back() + produced);
+            n = produced;
+            ++level;
+        }
+        auto t_end = Clock::now();
+        collect_timing();
+        stats.level_loop_sec = secs(t_loop, t_end);
+        stats.total_sec = secs(t_start, t_end);
+        stats.table_capacity = cap_;
+        return order_dependent && !fifo_;
+    }
+
+    // FAST order without `eventually` properties or a target count: the expansion of level L+1 is
+    // enqueued while level L still runs (its frontier size is read on the device: the claims of the
+    // last resetting publish), so the GPU does not idle while the host digests a level. The host
+    // keeps one level in flight beyond the one it waits for. A speculative launch is skipped when
+    // the visited set or the arena might not hold it (that level is then launched after the wait,
+    // sized exactly). A speculative level launched past the end (an exhausted frontier or an early
+    // exit) is ignored. Returns whether the run stopped early inside a level.
+    bool pipeline_levels(u64 n, u32 sq_level0) {
+        u32 undiscovered = (1u << M::NPROPS) - 1;
+        u32 level = 0;
+        bool order_dependent = false;
+        auto discoveries_of = [&](u32 lvl, u32& max_rank) {
+            u32 newly = 0;
+            for (int p = 0; p < M::NPROPS; ++p)
+                if ((undiscovered >> p & 1) && lc_.disc[p] != ~0u) {
+                    newly |= 1u << p;
+                    max_rank = std::max(max_rank, lc_.disc[p]);
+                    disc[p].found = true;
+                    disc[p].level = lvl;
+                    disc[p].rank = lc_.disc[p];
+                }
+            return newly;
+        };
+        u32 max_rank = 0;
+        u32 newly = discoveries_of(0, max_rank);  // among the init states (roots publish)
+        undiscovered &= ~newly;
+        if (newly && undiscovered == 0) {
+            lvisited_.push_back(max_rank + 1);
+            reference_done = true;
+            SR_HIP(hipStreamSynchronize(stream_));  // the level-0 launch is not counted
+            fill_discovery_fps();
+            return true;
+        }
+        u32 sq = sq_level0;  // enqueued before the roots' outcome was read
+        for (;;) {
+            // enqueue the next level before waiting for this one
+            const double g = std::max(ratio_, 1.0) * 1.5;
+            const u64 est1 = (u64)((double)n * g) + 1024;     // the next frontier
+            const u64 est2 = (u64)((double)est1 * g) + 1024;  // the states it will claim
+            const u64 nb_next = lstart_.back();
+            const bool spec = !pessimistic_ && (double)(unique + est1 + est2) < 0.8 * (double)cap_ &&
+                              nb_next + est1 + est2 <= arena_cap_;
+            // launch shape: a tight estimate (the grid strides over any excess)
+            const u64 shape = (u64)((double)n * std::max(ratio_, 0.05) * 1.1) + 64;
+            u32 sq_next = spec ? launch_expand(nb_next, 0, true, shape, undiscovered) : 0;
+
+            wait_publish(sq);  // lc_ = this level's counters
+            const u64 produced = lc_.claims;
+            state_count += lc_.successors;
+            unique += produced;
+            stats.successors += lc_.successors;
+            stats.probes += lc_.probes;
+            stats.cas += lc_.cas;
+            if (level < launch_frontier.size()) launch_frontier[level] = n;  // one launch per level
+            stats.algorithmic_bytes += n * 8 * W + lc_.successors * 8 + produced * (16 + 8 * W);
+            stats.levels++;
+            ratio_ = (double)produced / (double)n;
+            en_ratio_ = std::max(1.0, (double)lc_.enabled / (double)n);
+            lvisited_.push_back(n);
+            if (o_.verbose)
+                std::fprintf(stderr, "[sr] level %u: frontier %llu succ %llu new %llu unique %llu cap %llu%s\n", level,
+                             (unsigned long long)n, (unsigned long long)lc_.successors, (unsigned long long)produced,
+                             (unsigned long long)unique.load(), (unsigned long long)cap_, spec ? " (next enqueued)" : "");
+            if (produced == 0) {  // exhausted (a speculative launch saw an empty frontier)
+                reference_done = true;
+                break;
+            }
+            max_depth = level + 1;
+            lstart_.push_back(lstart_.back() + produced);
+            n = produced;
+            ++level;
+            max_rank = 0;
+            newly = discoveries_of(level, max_rank);
+            undiscovered &= ~newly;
+            if (newly && undiscovered == 0) {
+                // every property discovered inside this level: the reference stops at that pop
+                // (order-dependent in FAST order; AUTO re-runs FIFO). A speculative expansion of
+                // this level is not counted.
+                lvisited_.push_back(max_rank + 1);
+                reference_done = true;
+                order_dependent = true;
+                break;
+            }
+            sq = spec ? sq_next : launch_sync(n, undiscovered);
+        }
+        (void)hipStreamSynchronize(stream_);
+        fill_discovery_fps();
+        return order_dependent;
+    }
+
+    // Launch of the level whose frontier (n states) ends the arena, after the previous one is done:
+    // the visited set and the arena are grown first if the level might not fit.
+    u32 launch_sync(u64 n, u32 undiscovered) {
+        const u64 d_eff = pessimistic_ ? D_ : std::min<u64>(D_, (u64)std::ceil(2.0 * ratio_ + 1.0));
+        while ((double)(unique + n * d_eff) > 0.8 * (double)cap_) grow_table();
+        const u64 fbase = lstart_[lstart_.size() - 2];
+        ensure_arena(fbase + n + n * d_eff, fbase + n);
+        return launch_expand(fbase, (u32)n, false, n, undiscovered);
+    }
+
+    // expand_fast's grid is capped at two full residencies of the device (resident blocks per CU
+    // at its LDS footprint x CUs); the kernel strides over any further parents. Whole residencies
+    // avoid a partial last wave of workgroups. The measured gain is small and of the order of the
+    // ±3% run-to-run noise (`profiles/r01_grid_sweep.jsonl`, `r01_gridcap_default.jsonl`); the cap
+    // is printed with verbose=1. SR_GRID_MAX > 0 overrides it (<= 0 or unparsable: the default).
+    u32 expand_grid_cap() {
+        if (grid_max_) return grid_max_;
+        int per_cu = 0, cus = 0;
+        const size_t dyn = filt_log2_ ? (8u << filt_log2_) : 0u;
+        const void* k = probe_batch_ == 2 ? (const void*)expand_fast<M, 2, 0> : (const void*)expand_fast<M, 1, 0>;
+        SR_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 256, dyn));
+        SR_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, o_.device));
+        grid_max_ = per_cu > 0 && cus > 0 ? (u32)(2 * per_cu * cus) : ~0u;
+        if (o_.verbose) std::fprintf(stderr, "[sr] expand grid cap %u blocks (%d per CU x %d CUs x 2)\n", grid_max_, per_cu, cus);
+        return grid_max_;
+    }
+
+    // One expand_fast launch over a whole level whose frontier starts at arena offset `fbase`:
+    // n states (dev_n = 0), or the previous level's claims read on the device (dev_n = 1, `shape`
+    // is then an estimate used only for the launch shape; the grid strides over any excess).
+    u32 launch_expand(u64 fbase, u32 n, bool dev_n, u64 shape, u32 undiscovered) {
+        const u32 sq = next_seq();
+        const u64 nbase = fbase + (dev_n ? 0 : n);  // start of the next level (dev_n: + n on the device)
+        const u32 ncap = (u32)std::min<u64>(arena_cap_ - nbase, 0xffffffffu);
+        const u32 ppw_log2 = ppw_env_ >= 0 ? (u32)ppw_env_ : ppw_for(shape);
+        const u32 grid = std::min(expand_grid_cap(), std::max<u32>(1, blocks_for((shape + (1u << ppw_log2) - 1) >> ppw_log2, 4)));
+        timed([&] {
+            auto launch = [&](auto kern) {
+                kern<<<grid, 256, filt_log2_ ? (8u << filt_log2_) : 0u, stream_>>>(
+                    m_, arena_.p + fbase * W, 0u, n, view(), arena_.p + nbase * W, apar_.p + nbase, ncap, lc_d_,
+                    undiscovered, hcd(sq), sq, 1u, ppw_log2, filt_log2_, dev_n ? 1u : 0u);
+            };
+            if (o_.counters) launch(expand_fast<M, 1, 0, true>);
+            else switch (probe_batch_ * 10 + probe_load_) {
+                case 20: launch(expand_fast<M, 2, 0>); break;
+                default: launch(expand_fast<M, 1, 0>); break;
+            }
+        }, n);
+        return sq;
+    }
+
+    // disc[p].fp from the discovering state in the arena (after the level loop).
+    // The copies are queued together into pinned memory and waited for once (one round trip, not
+    // one blocking copy per property).
+    void fill_discovery_fps() {
+        static_assert((size_t)M::NPROPS * W <= Ctx::STAGE_WORDS, "discovery staging");
+        bool any = false;
+        for (int p = 0; p < M::NPROPS; ++p) {
+            if (!disc[p].found) continue;
+            SR_HIP(hipMemcpyAsync(ctx_->stage + (size_t)p * W, arena_.p + (lstart_[disc[p].level] + disc[p].rank) * W,
+                                  W * sizeof(u64), hipMemcpyDeviceToHost, stream_));
+            any = true;
+        }
+        if (!any) return;
+        SR_HIP(hipStreamSynchronize(stream_));
+        for (int p = 0; p < M::NPROPS; ++p)
+            if (disc[p].found) disc[p].fp = fingerprint<W>(ctx_->stage + (size_t)p * W);
+    }
+
+    // Smallest 1500-pop block boundary inside this level at which state_count >= target.
+    u64 target_limit(u64 n, u64 popped_before, u64 limit) {
+        DBuf<u32> counts;
+        counts.alloc(o_.device, n);
+        count_successors<M><<<blocks_for(n, 256), 256, 0, stream_>>>(m_, cur(), (u32)n, counts.p);
+        SR_HIP(hipGetLastError());
+        std::vector<u32> h(n);
+        SR_HIP(hipMemcpyAsync(h.data(), counts.p, n * sizeof(u32), hipMemcpyDeviceToHost, stream_));
+        SR_HIP(hipStreamSynchronize(stream_));
+        u64 sc = state_count;
+        u64 r = 0;
+        for (u64 k = popped_before / 1500 + 1;; ++k) {
+            u64 b = k * 1500 - popped_before;  // pops of this level at the block boundary
+            if (b > n || b > limit) return ~0ull;
+            for (; r < b; ++r) sc += h[r];
+            if (sc >= o_.target_state_count) return b;
+        }
+    }
+
+    // Expands frontier ranks [0, limit) of `level` into next_; returns the next frontier size.
+    u64 expand_level(u32 level, u64 n, u64 limit, u32 undiscovered, const u32* peb = nullptr) {
+        const u32 A = A_;  // action slots (FIFO candidate layout)
+        u64 claims = 0;
+        DBuf<u32> cand;
+        if (fifo_) {
+            cand.alloc(o_.device, limit * A);
+            SR_HIP(hipMemsetAsync(cand.p, 0xff, limit * A * sizeof(u32), stream_));
+        }
+        const u64 nbase = lstart_.back();  // arena offset of the next level
+        // New states per parent assumed when sizing a chunk: twice the last level's growth (the
+        // model's max out-degree D in pessimistic mode); see run_with_restart.
+        const u64 d_eff = pessimistic_ ? D_ : std::min<u64>(D_, (u64)std::ceil(2.0 * ratio_ + 1.0));
+        for (u64 lo = 0; lo < limit;) {
+            // Chunk so the visited set stays under 80% load.
+            u64 head = (u64)(0.8 * (double)cap_) - std::min<u64>((u64)(0.8 * (double)cap_), unique + claims);
+            u64 c = std::min<u64>(limit - lo, head / std::max<u64>(d_eff, 1));
+            if (c < std::min<u64>(limit - lo, 1u << 16)) {
+                grow_table(fifo_ ? cand.p : nullptr, fifo_ ? limit * A : 0);
+                continue;
+            }
+            if (!fifo_) ensure_arena(nbase + claims + c * d_eff, nbase + claims);
+            const u32 ulo = (u32)lo, uhi = (u32)(lo + c);
+            const bool last = lo + c == limit;
+            const u32 sq = next_seq();
+            if (fifo_) {
+                timed([&] {
+                    expand_fifo<M><<<blocks_for(c, 256), 256, 0, stream_>>>(m_, cur(), ulo, uhi, (u32)limit, view(), cand.p,
+                                                                            A, level, lc_d_, hcd(sq), sq);
+                });
+            } else {
+                const u32 ncap = (u32)std::min<u64>(arena_cap_ - nbase, 0xffffffffu);
+                u64* next = arena_.p + nbase * W;
+                u32* npar = apar_.p + nbase;
+                const u32 ppw_log2 = ppw_env_ >= 0 ? (u32)ppw_env_ : ppw_for(c);
+                const u32 grid = std::min(expand_grid_cap(), blocks_for((c + (1u << ppw_log2) - 1) >> ppw_log2, 4));
+                timed([&] {
+                    auto launch = [&](auto kern) {
+                        kern<<<grid, 256, filt_log2_ ? (8u << filt_log2_) : 0u, stream_>>>(
+                            m_, cur(), ulo, uhi, view(), next, npar, ncap, lc_d_, undiscovered, hcd(sq), sq,
+                            last ? 1u : 0u, ppw_log2, filt_log2_, 0u);
+                    };
+                    if (o_.counters) launch(expand_fast<M, 1, 0, true>);
+                    else switch (probe_batch_ * 10 + probe_load_) {
+                        case 11: launch(expand_fast<M, 1, 1>); break;
+                        case 12: launch(expand_fast<M, 1, 2>); break;
+                        case 13: launch(expand_fast<M, 1, 3>); break;
+                        case 20: launch(expand_fast<M, 2, 0>); break;
+                        case 21: launch(expand_fast<M, 2, 1>); break;
+                        default: launch(expand_fast<M, 1, 0>); break;
+                    }
+                });
+            }
+            wait_publish(sq);
+            claims = lc_.claims;
+            lo += c;
+        }
+        ratio_ = (double)claims / (double)limit;
+        if (!fifo_) {
+            en_ratio_ = std::max(1.0, (double)lc_.enabled / (double)limit);
+            return claims;
+        }
+
+        // FIFO passes 2-3: owners per parent, exclusive scan, ordered scatter.
+        ensure_arena(nbase + claims, nbase);
+        DBuf<u32> counts, offs, sums, total;
+        counts.alloc(o_.device, limit);
+        offs.alloc(o_.device, limit);
+        u32 tiles = blocks_for(limit, SCAN_TILE);
+        sums.alloc(o_.device, tiles);
+        total.alloc(o_.device, 1);
+        timed([&] { own_count<M><<<blocks_for(limit, 256), 256, 0, stream_>>>(cand.p, (u32)limit, A, level, view(), counts.p); });
+        scan_tile_sums<<<tiles, SCAN_BLOCK, 0, stream_>>>(counts.p, (u32)limit, sums.p);
+        scan_sums<<<1, SCAN_BLOCK, 0, stream_>>>(sums.p, tiles, total.p);
+        scan_tiles<<<tiles, SCAN_BLOCK, 0, stream_>>>(counts.p, (u32)limit, sums.p, offs.p);
+        SR_HIP(hipGetLastError());
+        const u32 sq = next_seq();
+        timed([&] {
+            scatter_fifo<M><<<blocks_for(limit, 256), 256, 0, stream_>>>(m_, cur(), cand.p, offs.p, (u32)limit, A, level,
+                                                                         view(), arena_.p + nbase * W, apar_.p + nbase, lc_d_,
+                                                                         undiscovered, hcd(sq), sq, total.p, peb,
+                                                                         emask_ ? aeb_.p + nbase : nullptr);
+        });
+        wait_publish(sq);
+        const u32 owners = lc_.aux;
+        if (owners != claims) throw Error(SR_ERR_CAPACITY, "FIFO ownership mismatch: owners " + std::to_string(owners) + " claims " + std::to_string(claims));
+        return owners;
+    }
+
+    // Parents per wave (log2) of the FAST kernel for a chunk of c parents. A wave walks the
+    // enabled action slots of its parents 64 at a time. Light models (a few ALU ops per successor)
+    // amortise the wave's setup over ~16 such rounds; heavy ones (paxos: ~1.3K VALU ops per
+    // successor) want ~4 rounds per wave and more waves to hide the probe latency. Small levels
+    // use fewer parents per wave until ~1K waves are in flight (minimum 4 parents per wave).
+    // Measured per level with SR_PPW_LOG2 sweeps (profiles/r01_ppw_levels.txt).
+    u32 ppw_for(u64 c) const {
+        const double rounds = W >= 4 ? 4.0 : 16.0;
+        const double ppw = 64.0 * rounds / en_ratio_;
+        u32 l = 2;
+        while (l < 6 && (double)(2u << l) <= ppw) ++l;
+        while (l > 2 && ((c + (1u << l) - 1) >> l) < 1024) --l;
+        return l;
+    }
+
+    // The frontier being expanded: the arena's second-to-last level.
+    const u64* cur() const { return arena_.p + lstart_[lstart_.size() - 2] * W; }
+
+    M m_;
+    sr_opts o_;
+    u32 A_;  // action slots
+    u32 D_;  // max successors of one state (bounds the new states a chunk can create)
+    u32 emask_;  // the model's `eventually` properties
+    bool fifo_ = false;
+    int probe_batch_ = 1;
+    int probe_load_ = 0;
+    int ppw_env_ = -1;
+    u32 grid_max_ = 0;       // cap on expand_fast's grid, 0 = two device residencies (SR_GRID_MAX)
+    u64 query_mask_ = 4095;  // spins between hipStreamQuery calls in wait_publish (SR_QUERY_LOG2)
+    bool pipeline_ = true;  // FAST-order level pipelining (SR_PIPELINE=0 disables, for A/B runs)
+    u32 filt_log2_ = W >= 4 ? 10 : 9;  // block-local duplicate filter (SR_FILTER_LOG2 sweep in profiles/)
+    bool pessimistic_ = false;  // size chunks for max out-degree new states per parent
+    u64 grow_factor_ = 1;       // initial-capacity multiplier after a capacity restart
+    double ratio_ = 1.0;        // new states per expanded parent in the last level
+    double en_ratio_ = 8.0;     // enabled action slots per expanded parent in the last level
+    double table_load_ = 0.5;
+    bool load_env_ = false;
+    Ctx* ctx_ = nullptr;
+    hipStream_t stream_ = nullptr;
+    HostCounters lc_{};  // host copy of the last published counters
+    LevelCounters* lc_d_ = nullptr;
+    u64 cap_ = 0;
+    DBuf<u64> keys_, meta_;      // visited set
+    DBuf<u64> arena_;            // BFS tree: every level's states in visit order
+    DBuf<u32> apar_;             // parent rank (in the previous level) of each arena state
+    DBuf<u32> aeb_;              // EventuallyBits of each arena state (models with eventually properties)
+    u64 arena_cap_ = 0;          // states
+    std::vector<u64> lstart_;    // arena offset of each level (+ one past the newest)
+    std::vector<u64> lvisited_;  // states of each level that the reference would pop
+};
+
+}  // namespace sr
+
+#include "dist.hpp"
+
+namespace sr {
+
+// The fingerprint of a state given by its canonical description (the integers of
+// sr_gpu_bfs_discovery_path / `describe`): what a host that holds the state compares with a
+// discovery's fingerprint chain (`Path::from_fingerprints`, src/checker/path.rs:20-86).
+template <class M>
+int described_fingerprint(const M& m, const i64* d, int width, u64* fp) {
+    if constexpr (has_undescribe<M>::value) {
+        if (!d || !fp || width != m.describe_width()) return SR_ERR_ARG;
+        u64 s[M::W];
+        m.undescribe(d, s);
+        *fp = fingerprint<M::W>(s);
+        return SR_OK;
+    } else {
+        (void)m, (void)d, (void)width, (void)fp;
+        return SR_ERR_UNSUPPORTED;
+    }
+}
+
+// ---- plugins: a GpuModel compiled into its own shared library (include/stateright_gpu_model.hpp) ----
+// MAKE(params, nparams, device) builds the model (device < 0: host-only use); it may throw Error.
+inline sr_opts normalized_opts(const sr_opts* opts) {
+    sr_opts o;
+    std::memset(&o, 0, sizeof(o));
+    o.struct_size = sizeof(sr_opts);
+    if (opts) std::memcpy(&o, opts, std::min<size_t>(sizeof(o), opts->struct_size ? opts->struct_size : sizeof(o)));
+    return o;
+}
+
+template <class M, class Make>
+void* plugin_create(Make make, const int64_t* p, int32_t np, const sr_opts* opts, void* comm, int32_t vparts, char* err,
+                    int32_t errcap) {
+    try {
+        const sr_opts o = normalized_opts(opts);
+        M m = make(p, np, o.device);
+        EngineBase* e;
+        if (comm || vparts > 1) e = new DistEngine<M>(m, o, static_cast<Comm*>(comm), (int)vparts);
+        else e = new Engine<M>(m, o);
+        return e;
+    } catch (const std::exception& x) {
+        if (err && errcap > 0) std::snprintf(err, (size_t)errcap, "%s", x.what());
+        return nullptr;
+    }
+}
+
+template <class M, class Make>
+int32_t plugin_fingerprint(Make make, const int64_t* p, int32_t np, const int64_t* d, int32_t width, uint64_t* fp) {
+    try {
+        return described_fingerprint(make(p, np, -1), d, width, fp);
+    } catch (const Error& x) {
+        return x.code;
+    } catch (const std::exception&) {
+        return SR_ERR_ARG;
+    }
+}
+
+}  // namespace sr

@@ -47,6 +47,14 @@ struct has_qkey : std::false_type {};
 template <class M>
 struct has_qkey<M, std::void_t<decltype(std::declval<const M&>().qkey_bits())>> : std::true_type {};
 
+// Models that can rebuild a state from its canonical description (`undescribe`, the inverse of
+// `describe`) expose their fingerprint to a host that holds the state (sr_model_fingerprint).
+template <class M, class = void>
+struct has_undescribe : std::false_type {};
+template <class M>
+struct has_undescribe<M, std::void_t<decltype(std::declval<const M&>().undescribe((const i64*)nullptr, (u64*)nullptr))>>
+    : std::true_type {};
+
 // murmur3 fmix64: a bijection on u64 with fmix64(0) == 0.
 SR_HD u64 fmix64(u64 k) {
     k ^= k >> 33;
@@ -107,6 +115,7 @@ struct LinearEquation {
     const char* prop_name(int) const { return "solvable"; }
     int describe_width() const { return 2; }
     void describe(const u64* s, i64* d) const { d[0] = (i64)(s[0] & 0xff); d[1] = (i64)((s[0] >> 8) & 0xff); }
+    void undescribe(const i64* d, u64* s) const { s[0] = ((u64)d[0] & 0xff) | ((u64)d[1] & 0xff) << 8; }
     i64 action_id(const u64*, int a_) const { return a_; }
     std::string action_name(i64 id) const { return id == 0 ? "IncreaseX" : "IncreaseY"; }
     i64 action_id_bound() const { return 2; }
@@ -130,6 +139,7 @@ struct BinaryClock {
     const char* prop_name(int) const { return "in [0, 1]"; }
     int describe_width() const { return 1; }
     void describe(const u64* s, i64* d) const { d[0] = (int8_t)(s[0] & 0xff); }
+    void undescribe(const i64* d, u64* s) const { s[0] = (u64)(u8)d[0]; }
     i64 action_id(const u64* s, int) const { return (s[0] & 0xff) == 0 ? 1 : 0; }  // GoLow=0, GoHigh=1
     std::string action_name(i64 id) const { return id == 0 ? "GoLow" : "GoHigh"; }
     i64 action_id_bound() const { return 2; }
@@ -231,6 +241,17 @@ struct TwoPhase {
         d[k++] = (i64)((s >> (4 * n + 2)) & 1);
         d[k++] = (i64)((s >> (4 * n + 3)) & 1);
     }
+    void undescribe(const i64* d, u64* sp) const {
+        u64 s = 0;
+        int k = 0;
+        for (int rm = 0; rm < n; ++rm) s |= ((u64)d[k++] & 3) << (2 * rm);
+        s |= ((u64)d[k++] & 3) << (2 * n);
+        for (int rm = 0; rm < n; ++rm) s |= ((u64)d[k++] & 1) << (2 * n + 2 + rm);
+        for (int rm = 0; rm < n; ++rm) s |= ((u64)d[k++] & 1) << (3 * n + 2 + rm);
+        s |= ((u64)d[k++] & 1) << (4 * n + 2);
+        s |= ((u64)d[k++] & 1) << (4 * n + 3);
+        sp[0] = s;
+    }
     i64 action_id(const u64*, int a) const { return a; }
     i64 action_id_bound() const { return 2 + 5 * n; }
     std::string action_name(i64 id) const {
@@ -299,6 +320,14 @@ struct Increment {
         for (int t = 0; t < n; ++t) {
             d[1 + 2 * t] = (i64)getb(s, toff(t), 4);
             d[2 + 2 * t] = (i64)getb(s, toff(t) + 4, 2);
+        }
+    }
+    void undescribe(const i64* d, u64* s) const {
+        for (int i = 0; i < W; ++i) s[i] = 0;
+        setb(s, 0, 4, (u64)d[0]);
+        for (int t = 0; t < n; ++t) {
+            setb(s, toff(t), 4, (u64)d[1 + 2 * t]);
+            setb(s, toff(t) + 4, 2, (u64)d[2 + 2 * t]);
         }
     }
     i64 action_id(const u64* s, int t) const { return 2 * t + (getb(s, toff(t) + 4, 2) == 2 ? 1 : 0); }
@@ -372,6 +401,15 @@ struct IncrementLock {
         for (int t = 0; t < n; ++t) {
             d[2 + 2 * t] = (i64)getb(s, toff(t), 4);
             d[3 + 2 * t] = (i64)getb(s, toff(t) + 4, 3);
+        }
+    }
+    void undescribe(const i64* d, u64* s) const {
+        for (int i = 0; i < W; ++i) s[i] = 0;
+        setb(s, 0, 4, (u64)d[0]);
+        setb(s, 4, 1, (u64)d[1]);
+        for (int t = 0; t < n; ++t) {
+            setb(s, toff(t), 4, (u64)d[2 + 2 * t]);
+            setb(s, toff(t) + 4, 3, (u64)d[3 + 2 * t]);
         }
     }
     i64 action_id(const u64* s, int t) const { return 4 * t + (i64)getb(s, toff(t) + 4, 3); }
