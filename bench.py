@@ -27,6 +27,8 @@ timed on the engine's stream) and, at N=1, `cpu_baseline` (the CPU restatement o
 `spawn_bfs`, oracle/bfs_cli, on the same 2pc N=9 check, host threads and 1 thread).
 """
 import argparse
+import contextlib
+import ctypes
 import json
 import os
 import re
@@ -60,12 +62,31 @@ def parse():
     ap.add_argument("--order", default="fast", choices=["fast", "fifo"])
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU restatement (rank 0, N=1)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="host threads for the CPU baseline (0 = usable CPUs)")
+    ap.add_argument("--config4-steps", type=int, default=3,
+                    help="also time BASELINE configs[3] (2pc N=11, partitioned over the N GPUs; one GPU at N=1) "
+                         "for this many checks after one warmup (0 = skip); reported as `config4`, not `value`")
     ap.add_argument("--dry-run", action="store_true",
                     help="every rank prints its launch plan as JSON and exits before any GPU call")
     ap.add_argument("--mode", default="partitioned", choices=["partitioned", "replicas", "rccl1"],
                     help="N>1: one check partitioned over the GPUs, or one independent check per GPU; "
                          "rccl1: the partitioned RCCL path on a one-rank communicator (N=1 rehearsal)")
     return ap.parse_args()
+
+
+@contextlib.contextmanager
+def stdout_to_stderr():
+    """fd 1 -> fd 2 for the duration (RCCL prints its init banner to stdout with C stdio; the
+    bench's stdout must carry only the JSON line)."""
+    sys.stdout.flush()
+    libc = ctypes.CDLL(None)
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        yield
+    finally:
+        libc.fflush(None)
+        os.dup2(saved, 1)
+        os.close(saved)
 
 
 def launch_ranks(args):
@@ -160,6 +181,38 @@ def pmc_traffic(n, world):
     return None, None
 
 
+def measure_config4(args, world, comm, dev, barrier):
+    """BASELINE.json configs[3]: 2pc N=11 (366 993 408 unique states, 34 levels) partitioned over
+    the `world` GPUs (one process each, RCCL all-to-all per level), or on the one GPU at N=1."""
+    from stateright_amd import TwoPhaseSys
+    n = 11
+    want = 6 ** n + 4 ** n + 2 ** n
+
+    def check():
+        b = TwoPhaseSys(n).checker().capacity_hint(want).device(dev)
+        b = b.comm(comm).defer_paths() if world > 1 else b.order("fast")
+        c = b.spawn_bfs().join()
+        if c.unique_state_count() != want:
+            raise SystemExit(f"config4: wrong unique count {c.unique_state_count()} != {want}")
+        return c
+
+    check()  # warmup: allocations
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.config4_steps):
+        c = check()
+    barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        el = comm.allreduce([el], "max")[0]
+    st = c.stats()
+    return {"workload": f"2pc N={n} spawn_bfs, full check per step ({want} unique states; BASELINE configs[3])",
+            "parallelism": f"partitioned{world} (RCCL all-to-all per level)" if world > 1 else "1 GPU",
+            "n_gpus": world, "steps": args.config4_steps, "ms_per_step": el / args.config4_steps * 1e3,
+            "value": want * args.config4_steps / el, "unit": "unique states/s",
+            "restarts": st["restarts"], "head_levels": st["head_levels"], "records_routed": st["records_routed"]}
+
+
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -204,12 +257,10 @@ def main():
         label = f"2pc N={n}"
     partitioned = (world > 1 and args.mode == "partitioned") or args.mode == "rccl1"
     comm = None
-    if world > 1:
+    if world > 1 or args.mode == "rccl1":
         from stateright_amd.distributed import Communicator
-        comm = Communicator.from_env(device=dev)
-    elif args.mode == "rccl1":
-        from stateright_amd.distributed import Communicator
-        comm = Communicator(0, 1, Communicator.unique_id(), dev)
+        with stdout_to_stderr():
+            comm = Communicator.from_env(device=dev) if world > 1 else Communicator(0, 1, Communicator.unique_id(), dev)
 
     def step(profile=False, counters=False):
         b = make().checker().capacity_hint(expect_unique).device(dev)
@@ -272,6 +323,10 @@ def main():
     if world > 1:
         elapsed = comm.allreduce([elapsed], "max")[0]
     unique_total = float(unique) if partitioned or world == 1 else float(unique) * world
+
+    config4 = None
+    if args.config4_steps > 0 and args.model == "2pc":
+        config4 = measure_config4(args, world, comm, dev, barrier)
 
     c, st = last
     if rank != 0:
@@ -363,6 +418,8 @@ def main():
                                       "restarts", "pipelined", "records_routed", "head_levels")},
         "runtime": {"hip": versions["hip"], "rccl": versions["rccl"], "libs": N.loaded_runtime_paths()},
     }
+    if config4 is not None:
+        res["config4"] = config4
     if args.cpu_baseline and world == 1:
         try:
             res["cpu_baseline"] = cpu_baseline(args, n)

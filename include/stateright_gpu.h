@@ -167,6 +167,12 @@ int32_t sr_gpu_bfs_init_count(const sr_bfs* bfs);
  * not enabled along the way (the reference returns None). */
 int32_t sr_gpu_bfs_replay(const sr_bfs* bfs, int32_t init_index, const int64_t* action_ids, int32_t n_actions,
                           int64_t* states, int64_t cap_states, int32_t* conditions, int32_t cap_conditions);
+/* `Path::from_actions` as above, reporting each property's condition on EVERY state of the path
+ * (conditions[i * property_count + p], i = 0..n) and whether the last state is terminal (its
+ * `actions()` list is empty): what `assert_discovery` needs for an `eventually` property
+ * (src/checker.rs:306-323). Returns n, or -1 if an action is not enabled along the way. */
+int32_t sr_gpu_bfs_replay_trace(const sr_bfs* bfs, int32_t init_index, const int64_t* action_ids, int32_t n_actions,
+                                int32_t* conditions, int64_t cap, int32_t* terminal);
 /* Visited states in visit order (record_visits=1), describe_width int64s each; returns count*width. */
 int64_t sr_gpu_bfs_visits(const sr_bfs* bfs, int64_t* out, int64_t cap);
 /* The visitor's paths (`CheckerVisitor::visit` gets `Path::from_fingerprints` of every popped

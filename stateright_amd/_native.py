@@ -91,6 +91,8 @@ SIGNATURES = [
     ("sr_gpu_bfs_init_count", ctypes.c_int32, [_P]),
     ("sr_gpu_bfs_replay", ctypes.c_int32, [_P, ctypes.c_int32, _I64P, ctypes.c_int32, _I64P, ctypes.c_int64,
                                            ctypes.POINTER(ctypes.c_int32), ctypes.c_int32]),
+    ("sr_gpu_bfs_replay_trace", ctypes.c_int32, [_P, ctypes.c_int32, _I64P, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32),
+                                                 ctypes.c_int64, ctypes.POINTER(ctypes.c_int32)]),
     ("sr_gpu_bfs_visits", ctypes.c_int64, [_P, _I64P, ctypes.c_int64]),
     ("sr_gpu_bfs_visit_tree", ctypes.c_int64, [_P, _I64P, _I64P, ctypes.c_int64]),
     ("sr_gpu_bfs_free", None, [_P]),

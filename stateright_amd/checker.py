@@ -453,18 +453,46 @@ class GpuBfsChecker:
         flat = list(states)
         return [tuple(flat[k:k + width]) for k in range(0, len(flat), width)], list(conds[:len(self.properties())])
 
+    def replay_trace(self, actions, init_index=0):
+        """`Path::from_actions`: (per-state conditions [[cond of property p] per state], last state
+        terminal?) or None if an action is not enabled along the way."""
+        ids = [self.action_id(a) for a in actions]
+        arr = (ctypes.c_int64 * max(1, len(ids)))(*ids)
+        n_props = len(self.properties())
+        conds = (ctypes.c_int32 * max(1, (len(ids) + 1) * n_props))()
+        term = ctypes.c_int32()
+        n = self._lib.sr_gpu_bfs_replay_trace(self._h, init_index, arr, len(ids), conds, len(conds), ctypes.byref(term))
+        if n < 0:
+            return None
+        flat = list(conds)
+        return [flat[k * n_props:(k + 1) * n_props] for k in range(len(ids) + 1)], bool(term.value)
+
     def assert_discovery(self, name, actions):
-        """`assert_discovery` (src/checker.rs:292-337) for always/sometimes properties."""
+        """`assert_discovery` (src/checker.rs:292-337): the actions, from some init state, lead to a
+        state violating an `always` / satisfying a `sometimes` property, or along a path on which
+        an `eventually` property never holds and that ends at a terminal state."""
         found = self.assert_any_discovery(name)
         i = self._prop_index(name)
         exp = self.properties()[i][1]
+        info = []
         for init in range(self._lib.sr_gpu_bfs_init_count(self._h)):
-            r = self.replay(actions, init)
+            r = self.replay_trace(actions, init)
             if r is None:
                 continue
-            holds = r[1][i]
-            if exp == Expectation.Always and not holds:
+            per_state, terminal = r
+            last = per_state[-1][i]
+            if exp == Expectation.Always and not last:
                 return
-            if exp == Expectation.Sometimes and holds:
+            if exp == Expectation.Sometimes and last:
                 return
-        raise AssertionError(f'Invalid discovery for "{name}", but a valid one was found. found={found.into_actions()}')
+            if exp == Expectation.Eventually:
+                satisfied = any(s[i] for s in per_state)
+                if not satisfied and terminal:
+                    return
+                if satisfied:
+                    info.append("incorrect counterexample satisfies eventually property")
+                if not terminal:
+                    info.append("incorrect counterexample is nonterminal")
+        extra = f" ({'; '.join(info)})" if info else ""
+        raise AssertionError(f'Invalid discovery for "{name}"{extra}, but a valid one was found. '
+                             f"found={found.into_actions()}")

@@ -402,7 +402,10 @@ class DistEngine final : public EngineBase {
         u64 inits[8 * W];
         return m_.init_states(inits);
     }
-    int replay(int, const i64*, int, std::vector<i64>&, std::vector<int>&) const override { return -1; }
+    int replay(int init, const i64* ids, int n, std::vector<i64>& states, std::vector<int>& conds,
+               std::vector<int>* all_conds, int* terminal) const override {
+        return replay_model(m_, init, ids, n, states, conds, all_conds, terminal);
+    }
     std::vector<i64> visits() const override { return {}; }
     int partitions() const { return (int)T_; }
     bool early_exit() const { return early_exit_; }

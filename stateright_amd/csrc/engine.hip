@@ -305,6 +305,19 @@ int64_t sr_gpu_bfs_visit_tree(const sr_bfs* b, int64_t* parent, int64_t* action,
 int64_t sr_gpu_bfs_action_id_bound(const sr_bfs* b) { return b ? b->e->action_id_bound() : 0; }
 int32_t sr_gpu_bfs_init_count(const sr_bfs* b) { return b ? b->e->init_count() : 0; }
 
+int32_t sr_gpu_bfs_replay_trace(const sr_bfs* b, int32_t init, const int64_t* ids, int32_t n, int32_t* conditions,
+                                int64_t cap, int32_t* terminal) {
+    if (!b) return SR_ERR_ARG;
+    std::vector<i64> s;
+    std::vector<int> c, all;
+    int term = 0;
+    int r = b->e->replay(init, ids, n, s, c, &all, &term);
+    if (r < 0) return -1;
+    for (int64_t i = 0; i < (int64_t)all.size() && i < cap; ++i) conditions[i] = all[i];
+    if (terminal) *terminal = term;
+    return r;
+}
+
 int32_t sr_gpu_bfs_replay(const sr_bfs* b, int32_t init, const int64_t* ids, int32_t n, int64_t* states, int64_t cap_states,
                           int32_t* conds, int32_t cap_conds) {
     if (!b) return SR_ERR_ARG;

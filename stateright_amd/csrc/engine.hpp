@@ -66,7 +66,11 @@ class EngineBase {
     virtual bool visit_tree(std::vector<i64>&, std::vector<i64>&) const { return false; }
     virtual i64 action_id_bound() const = 0;
     virtual int init_count() const = 0;
-    virtual int replay(int init, const i64* ids, int n, std::vector<i64>& states, std::vector<int>& conds) const = 0;
+    // `Path::from_actions` (src/checker/path.rs:90-112) from init state `init`: the states, each
+    // property's CONDITION on the last state, optionally on every state ((n + 1) x nprops), and
+    // whether the last state is terminal (`actions()` lists nothing). -1: an action is not enabled.
+    virtual int replay(int init, const i64* ids, int n, std::vector<i64>& states, std::vector<int>& conds,
+                       std::vector<int>* all_conds = nullptr, int* terminal = nullptr) const = 0;
 
     std::atomic<u64> state_count{0}, unique{0};
     std::atomic<u32> max_depth{0};
@@ -79,6 +83,54 @@ class EngineBase {
     std::vector<double> launch_ms;    // per timed launch (profile=1), in launch order
     std::vector<u64> launch_frontier; // the frontier each launch expanded (0 if unknown)
 };
+
+template <class M>
+int replay_model(const M& m, int init, const i64* ids, int n, std::vector<i64>& states, std::vector<int>& conds,
+                 std::vector<int>* all_conds, int* terminal) {
+    constexpr int W = M::W;
+    u64 inits[8 * W];
+    const int k = m.init_states(inits);
+    if (init < 0 || init >= k) return -1;
+    const int wd = m.describe_width();
+    std::vector<u64> cur(&inits[init * W], &inits[init * W] + W);
+    // the property's condition (discovers() is !condition for `always`, the condition otherwise)
+    auto cond = [&](int p, const u64* s) { return m.expectation(p) == ALWAYS ? !m.discovers(p, s) : m.discovers(p, s); };
+    auto emit = [&](const u64* s) {
+        size_t o = states.size();
+        states.resize(o + wd);
+        m.describe(s, &states[o]);
+        if (all_conds)
+            for (int p = 0; p < M::NPROPS; ++p) all_conds->push_back(cond(p, s) ? 1 : 0);
+    };
+    if (all_conds) all_conds->clear();
+    for (int i = 0; i < n; ++i) {
+        u64 mask[M::MW];
+        m.enabled(cur.data(), mask);
+        bool found = false;
+        for (int w = 0; w < M::MW && !found; ++w)
+            for (u64 bits = mask[w]; bits && !found; bits &= bits - 1) {
+                int a = w * 64 + __builtin_ctzll(bits);
+                if (m.action_id(cur.data(), a) != ids[i]) continue;
+                u64 ns[W];
+                if (!m.apply(cur.data(), a, ns)) continue;
+                emit(cur.data());
+                cur.assign(ns, ns + W);
+                found = true;
+            }
+        if (!found) return -1;
+    }
+    emit(cur.data());
+    conds.assign(M::NPROPS, 0);
+    for (int p = 0; p < M::NPROPS; ++p) conds[p] = cond(p, cur.data()) ? 1 : 0;
+    if (terminal) {
+        u64 mask[M::MW];
+        m.enabled(cur.data(), mask);
+        u64 any = 0;
+        for (int w = 0; w < M::MW; ++w) any |= mask[w];
+        *terminal = any == 0;
+    }
+    return n;
+}
 
 template <class M>
 class Engine final : public EngineBase {
@@ -222,40 +274,9 @@ class Engine final : public EngineBase {
         u64 inits[8 * W];
         return m_.init_states(inits);
     }
-    int replay(int init, const i64* ids, int n, std::vector<i64>& states, std::vector<int>& conds) const override {
-        u64 inits[8 * W];
-        int k = m_.init_states(inits);
-        if (init < 0 || init >= k) return -1;
-        const int wd = m_.describe_width();
-        std::vector<u64> cur(&inits[init * W], &inits[init * W] + W);
-        auto emit = [&](const u64* s) {
-            size_t o = states.size();
-            states.resize(o + wd);
-            m_.describe(s, &states[o]);
-        };
-        for (int i = 0; i < n; ++i) {
-            u64 mask[M::MW];
-            m_.enabled(cur.data(), mask);
-            bool found = false;
-            for (int w = 0; w < M::MW && !found; ++w)
-                for (u64 bits = mask[w]; bits && !found; bits &= bits - 1) {
-                    int a = w * 64 + __builtin_ctzll(bits);
-                    if (m_.action_id(cur.data(), a) != ids[i]) continue;
-                    u64 ns[W];
-                    if (!m_.apply(cur.data(), a, ns)) continue;
-                    emit(cur.data());
-                    cur.assign(ns, ns + W);
-                    found = true;
-                }
-            if (!found) return -1;
-        }
-        emit(cur.data());
-        conds.assign(M::NPROPS, 0);
-        for (int p = 0; p < M::NPROPS; ++p) {
-            bool d = m_.discovers(p, cur.data());
-            conds[p] = m_.expectation(p) == SOMETIMES ? d : !d;
-        }
-        return n;
+    int replay(int init, const i64* ids, int n, std::vector<i64>& states, std::vector<int>& conds,
+               std::vector<int>* all_conds, int* terminal) const override {
+        return replay_model(m_, init, ids, n, states, conds, all_conds, terminal);
     }
 
     // The visitor's paths (src/checker/bfs.rs:187-189 builds `Path::from_fingerprints` of every

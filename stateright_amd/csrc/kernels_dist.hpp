@@ -62,6 +62,16 @@ __device__ __forceinline__ bool last_workgroup(LevelCounters* lc) {
     return true;
 }
 
+// Pipelined mode: the last workgroup of a launch, told to every thread of that workgroup.
+__device__ __forceinline__ bool last_block(LevelCounters* lc) {
+    __shared__ u32 is_last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) is_last = atomicAdd(&lc->ticket, 1u) == gridDim.x - 1;
+    __syncthreads();
+    return is_last != 0;
+}
+
 // Expands the frontier of this partition (its size n is read from ctl). Same structure as
 // expand_fast (kernels.hpp): waves of ppw parents, successors load-balanced over the lanes, PB
 // successors per lane per round with their probes issued back to back, and the block-local LDS
@@ -338,27 +348,40 @@ __global__ void __launch_bounds__(256) expand_route(M m, u64* __restrict__ arena
         if (total_succ) atomicAdd(reinterpret_cast<unsigned long long*>(&lc->successors), (unsigned long long)total_succ);
         if (total_enabled) atomicAdd(reinterpret_cast<unsigned long long*>(&lc->enabled), (unsigned long long)total_enabled);
     }
-    if (!last_workgroup<M::NPROPS>(lc)) return;
-    for (u32 q = 0; q < nparts; ++q) {
-        row[q] = __hip_atomic_load(&send_counts[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        send_counts[q] = 0;  // for the next level
+    if (!last_block(lc)) return;
+    // The row, one word per thread (every source word is a round trip to the coherence point: one
+    // thread loading them in turn was the floor of a small level), staged in LDS for the headers.
+    __shared__ u64 srow[MAX_PARTS + 6 + MAX_PROPS];
+    const u32 rw = nparts + 6 + M::NPROPS;
+    for (u32 w = threadIdx.x; w < rw; w += blockDim.x) {
+        const u32 f = w - nparts;  // row fields after the per-destination counts
+        const u32* src = w < nparts ? send_counts + w
+                         : f == 1   ? reinterpret_cast<const u32*>(&lc->successors)
+                         : f == 2   ? &lc->claims
+                         : f == 3   ? &lc->err
+                         : f == 4   ? reinterpret_cast<const u32*>(&lc->enabled)
+                         : f == 5   ? &ctl->roots
+                         : f >= 6   ? &ctl->disc_prev[f - 6]
+                                    : &lc->claims;  // f == 0: the frontier size n (no load needed)
+        const bool wide = w >= nparts && (f == 1 || f == 4);
+        const u64 lo = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const u64 hi = __hip_atomic_load(src + (wide ? 1 : 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const u64 v = w >= nparts && f == 0 ? n : (wide ? lo | hi << 32 : lo);
+        srow[w] = v;
+        row[w] = v;
     }
-    row[nparts + 0] = n;
-    row[nparts + 1] = __hip_atomic_load(&lc->successors, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    row[nparts + 2] = __hip_atomic_load(&lc->claims, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    row[nparts + 3] = __hip_atomic_load(&lc->err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    row[nparts + 4] = __hip_atomic_load(&lc->enabled, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    row[nparts + 5] = ctl->roots;
-#pragma unroll
-    for (int p = 0; p < M::NPROPS; ++p) row[nparts + 6 + p] = ctl->disc_prev[p];
-    if (lag) {  // the row travels in the header of every bucket (and so reaches every rank)
-        const u32 rw = nparts + 6 + M::NPROPS;
-        for (u32 q = 0; q < nparts; ++q)
-            for (u32 w = 0; w < rw; ++w) send[(u64)q * bucket_stride - DIST_HDR + w] = row[w];
+    __syncthreads();
+    for (u32 q = threadIdx.x; q < nparts; q += blockDim.x) send_counts[q] = 0;  // for the next level
+    if (lag)  // the row travels in the header of every bucket (and so reaches every rank)
+        for (u32 i = threadIdx.x; i < nparts * rw; i += blockDim.x) {
+            const u32 q = i / rw, w = i - q * rw;
+            send[(u64)q * bucket_stride - DIST_HDR + w] = srow[w];
+        }
+    if (threadIdx.x == 0) {
+        lc->successors = 0;
+        lc->enabled = 0;
+        lc->ticket = 0;
     }
-    lc->successors = 0;
-    lc->enabled = 0;
-    lc->ticket = 0;
 }
 
 // Insert the records this partition received (state + parent gid); new states continue the next
@@ -429,16 +452,6 @@ __global__ void __launch_bounds__(256) insert_recv(M m, const u64* __restrict__ 
     ctl->roots = 0;
     lc->claims = 0;
     lc->ticket = 0;
-}
-
-// Pipelined mode: the last workgroup of a launch, told to every thread of that workgroup.
-__device__ __forceinline__ bool last_block(LevelCounters* lc) {
-    __shared__ u32 is_last;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) is_last = atomicAdd(&lc->ticket, 1u) == gridDim.x - 1;
-    __syncthreads();
-    return is_last != 0;
 }
 
 // Host-visible outcome of one pipelined level (pinned, two slots per partition): the rows of
@@ -522,23 +535,29 @@ __global__ void __launch_bounds__(256) insert_recv_lag(M m, const u64* __restric
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (threadIdx.x != 0) return;
-    const u32 claims = __hip_atomic_load(&lc->claims, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const u32 err = __hip_atomic_load(&lc->err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    pub->claims = claims;
-    pub->err = err;
-    ctl->nb = nb + n;
-    ctl->n = min(claims, next_cap);
-#pragma unroll
-    for (int p = 0; p < M::NPROPS; ++p) {
-        ctl->disc_prev[p] = __hip_atomic_load(&lc->disc[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        lc->disc[p] = ~0u;
+    if (threadIdx.x >= 64) return;
+    // the close, one counter per lane of wave 0: lane 0 claims, 1 err, 2 + p disc[p]
+    const u32 lane = threadIdx.x;
+    const bool live = lane < 2u + (u32)M::NPROPS;
+    const u32* src = lane == 0 ? &lc->claims : lane == 1 ? &lc->err : &lc->disc[live ? lane - 2 : 0];
+    const u32 v = live ? __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+    const u32 claims = __shfl(v, 0, 64), err = __shfl(v, 1, 64);
+    if (lane >= 2 && live) {
+        ctl->disc_prev[lane - 2] = v;
+        lc->disc[lane - 2] = ~0u;
     }
-    ctl->roots = 0;
-    lc->claims = 0;
-    lc->ticket = 0;
+    if (lane == 0) {
+        pub->claims = claims;
+        pub->err = err;
+        ctl->nb = nb + n;
+        ctl->n = min(claims, next_cap);
+        ctl->roots = 0;
+        lc->claims = 0;
+        lc->ticket = 0;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: host memory
-    __hip_atomic_store(&pub->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (lane == 0) __hip_atomic_store(&pub->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Copies the all-gathered rows to pinned host memory and then stores `seq` (the host spins on it).

@@ -80,3 +80,25 @@ def test_partitioned_rejects_eventually():
     g = sr.DGraph.with_property(EVENTUALLY).with_path([0, 1])
     with pytest.raises(sr.CheckerError):
         g.checker().partitions(2).spawn_bfs().join()
+
+
+def test_assert_discovery_eventually():
+    # src/checker.rs:306-323: an `eventually` counterexample is valid when the condition holds on
+    # no state of the path and the path ends at a terminal state (no actions)
+    c = odd([0, 1], [0, 2])
+    c.assert_discovery("odd", [2])
+    with pytest.raises(AssertionError, match="satisfies eventually property"):
+        c.assert_discovery("odd", [1])
+    c = odd([0, 1, 4, 6], [2, 4, 8])
+    c.assert_discovery("odd", [4, 6])       # 2 -> 4 -> 6, terminal, never odd
+    c.assert_discovery("odd", [4, 8])       # 2 -> 4 -> 8 as well
+    with pytest.raises(AssertionError, match="is nonterminal"):
+        c.assert_discovery("odd", [4])      # 2 -> 4 has successors
+    with pytest.raises(AssertionError, match="Invalid discovery"):
+        c.assert_discovery("odd", [7])      # not an action anywhere
+
+
+def test_replay_trace_conditions_every_state():
+    c = odd([0, 1, 4, 6], [2, 4, 8])
+    per_state, terminal = c.replay_trace([1, 4, 6], init_index=0)  # 0 -> 1 -> 4 -> 6
+    assert [s[0] for s in per_state] == [0, 1, 0, 0] and terminal
