@@ -173,6 +173,14 @@ int32_t sr_gpu_bfs_replay(const sr_bfs* bfs, int32_t init_index, const int64_t* 
  * (src/checker.rs:306-323). Returns n, or -1 if an action is not enabled along the way. */
 int32_t sr_gpu_bfs_replay_trace(const sr_bfs* bfs, int32_t init_index, const int64_t* action_ids, int32_t n_actions,
                                 int32_t* conditions, int64_t cap, int32_t* terminal);
+/* Explorer's `states` route (src/checker/explorer.rs:159-240), host-only: n == 0 lists the init
+ * states (action -1); otherwise the state reached by the fingerprint path (`Path::final_state`,
+ * src/checker/path.rs:115-136) and, per action its `actions()` lists (in order), the canonical
+ * action id, whether `next_state` is Some (has_state), the next state's fingerprint and its
+ * description (describe_width int64s per view). Returns the number of views (at most cap are
+ * written), or -1 if no state follows the fingerprints. */
+int32_t sr_gpu_bfs_explore(const sr_bfs* bfs, const uint64_t* fingerprints, int32_t n, int64_t* action_ids,
+                           int32_t* has_state, uint64_t* fingerprints_out, int64_t* states, int32_t cap);
 /* Visited states in visit order (record_visits=1), describe_width int64s each; returns count*width. */
 int64_t sr_gpu_bfs_visits(const sr_bfs* bfs, int64_t* out, int64_t cap);
 /* The visitor's paths (`CheckerVisitor::visit` gets `Path::from_fingerprints` of every popped

@@ -93,6 +93,9 @@ SIGNATURES = [
                                            ctypes.POINTER(ctypes.c_int32), ctypes.c_int32]),
     ("sr_gpu_bfs_replay_trace", ctypes.c_int32, [_P, ctypes.c_int32, _I64P, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32),
                                                  ctypes.c_int64, ctypes.POINTER(ctypes.c_int32)]),
+    ("sr_gpu_bfs_explore", ctypes.c_int32, [_P, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int32, _I64P,
+                                            ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_uint64), _I64P,
+                                            ctypes.c_int32]),
     ("sr_gpu_bfs_visits", ctypes.c_int64, [_P, _I64P, ctypes.c_int64]),
     ("sr_gpu_bfs_visit_tree", ctypes.c_int64, [_P, _I64P, _I64P, ctypes.c_int64]),
     ("sr_gpu_bfs_free", None, [_P]),

@@ -217,8 +217,20 @@ class CheckerBuilder:
         self._opts.order = N.SR_ORDER_FAST
         return self.spawn_bfs()
 
-    def serve(self, *_):
-        raise NotImplementedError("Explorer is out of scope for the GPU engine (SURVEY.md §2)")
+    def serve(self, address=("127.0.0.1", 3000), block=True):
+        """`serve` (src/checker.rs:107-113, src/checker/explorer.rs:71-129): spawns the GPU check and
+        serves the Explorer's JSON routes (`/.status`, `/.states/<fp>/<fp>/...`) and a small UI over
+        it. Blocks like the reference unless block=False, which returns the running
+        `stateright_amd.explorer.Explorer` (its `.checker`, `.url`, `.shutdown()`)."""
+        from .explorer import Explorer
+        ex = Explorer(self.spawn_bfs(), address)
+        if not block:
+            return ex.start()
+        try:
+            ex.serve_forever()
+        finally:
+            ex.shutdown()
+        return ex.checker
 
 
 class GpuBfsChecker:
@@ -359,6 +371,32 @@ class GpuBfsChecker:
         self._lib.sr_gpu_bfs_visits(self._h, buf, n)
         flat = list(buf[:n])
         return [tuple(flat[k:k + width]) for k in range(0, n, width)]
+
+    def explore(self, fingerprints):
+        """Explorer's `states` view (src/checker/explorer.rs:159-240): [(action name or None, state
+        description or None, fingerprint or None)] of the init states (no fingerprints) or of the
+        steps following the state the fingerprint path leads to; None if no state follows."""
+        n = len(fingerprints)
+        fps = (ctypes.c_uint64 * max(1, n))(*fingerprints)
+        width = self._lib.sr_gpu_bfs_describe_width(self._h)
+        cap = 4096
+        acts = (ctypes.c_int64 * cap)()
+        has = (ctypes.c_int32 * cap)()
+        fpo = (ctypes.c_uint64 * cap)()
+        st = (ctypes.c_int64 * (cap * max(1, width)))()
+        v = self._lib.sr_gpu_bfs_explore(self._h, fps, n, acts, has, fpo, st, cap)
+        if v == -1:
+            return None
+        if v < 0:
+            raise CheckerError("sr_gpu_bfs_explore", v)
+        out = []
+        for i in range(min(v, cap)):
+            name = None if acts[i] < 0 else self.action_name(acts[i])
+            if has[i]:
+                out.append((name, tuple(st[i * width:(i + 1) * width]), fpo[i]))
+            else:
+                out.append((name, None, None))
+        return out
 
     def visit_paths(self):
         """The path to every visited state, in visit order (what the reference hands to its

@@ -406,6 +406,10 @@ class DistEngine final : public EngineBase {
                std::vector<int>* all_conds, int* terminal) const override {
         return replay_model(m_, init, ids, n, states, conds, all_conds, terminal);
     }
+    int explore(const u64* fps, int n, std::vector<i64>& action, std::vector<int>& has, std::vector<u64>& fp,
+                std::vector<i64>& states) const override {
+        return explore_model(m_, fps, n, action, has, fp, states);
+    }
     std::vector<i64> visits() const override { return {}; }
     int partitions() const { return (int)T_; }
     bool early_exit() const { return early_exit_; }

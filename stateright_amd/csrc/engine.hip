@@ -318,6 +318,32 @@ int32_t sr_gpu_bfs_replay_trace(const sr_bfs* b, int32_t init, const int64_t* id
     return r;
 }
 
+int32_t sr_gpu_bfs_explore(const sr_bfs* b, const uint64_t* fps, int32_t n, int64_t* action_ids, int32_t* has_state,
+                           uint64_t* fp_out, int64_t* states, int32_t cap) {
+    try {
+        if (!b || (n > 0 && !fps)) return SR_ERR_ARG;
+        std::vector<i64> a, st;
+        std::vector<int> h;
+        std::vector<u64> f;
+        const int v = b->e->explore(fps, n, a, h, f, st);
+        if (v < 0) {
+            set_error("Unable to find state following fingerprints");
+            return -1;
+        }
+        const int wd = b->e->width();
+        for (int i = 0; i < v && i < cap; ++i) {
+            if (action_ids) action_ids[i] = a[i];
+            if (has_state) has_state[i] = h[i];
+            if (fp_out) fp_out[i] = f[i];
+            if (states) std::memcpy(states + (size_t)i * wd, st.data() + (size_t)i * wd, wd * sizeof(i64));
+        }
+        return v;
+    } catch (const Error& x) {
+        set_error(x.what());
+        return x.code;
+    }
+}
+
 int32_t sr_gpu_bfs_replay(const sr_bfs* b, int32_t init, const int64_t* ids, int32_t n, int64_t* states, int64_t cap_states,
                           int32_t* conds, int32_t cap_conds) {
     if (!b) return SR_ERR_ARG;

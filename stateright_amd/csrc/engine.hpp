@@ -71,6 +71,8 @@ class EngineBase {
     // whether the last state is terminal (`actions()` lists nothing). -1: an action is not enabled.
     virtual int replay(int init, const i64* ids, int n, std::vector<i64>& states, std::vector<int>& conds,
                        std::vector<int>* all_conds = nullptr, int* terminal = nullptr) const = 0;
+    virtual int explore(const u64* fps, int n, std::vector<i64>& action, std::vector<int>& has, std::vector<u64>& fp,
+                        std::vector<i64>& states) const = 0;
 
     std::atomic<u64> state_count{0}, unique{0};
     std::atomic<u32> max_depth{0};
@@ -130,6 +132,64 @@ int replay_model(const M& m, int init, const i64* ids, int n, std::vector<i64>& 
         *terminal = any == 0;
     }
     return n;
+}
+
+// Explorer's `states` route (src/checker/explorer.rs:159-240) on the host copy of the encoding:
+// with no fingerprints, the init states; otherwise `Path::final_state` (src/checker/path.rs:115-136:
+// the init state with the first fingerprint, then the first matching step per fingerprint) and,
+// for every action `actions()` lists there in order, the next state (has = 0: `next_state` is
+// None, the reference's "Action ignored" view). Returns the number of views, or -1 if no state
+// follows the fingerprints.
+template <class M>
+int explore_model(const M& m, const u64* fps, int n, std::vector<i64>& action, std::vector<int>& has,
+                  std::vector<u64>& fp_out, std::vector<i64>& states) {
+    constexpr int W = M::W;
+    const int wd = m.describe_width();
+    auto emit = [&](i64 a, const u64* s) {
+        action.push_back(a);
+        has.push_back(s ? 1 : 0);
+        fp_out.push_back(s ? fingerprint<W>(s) : 0);
+        const size_t o = states.size();
+        states.resize(o + wd, 0);
+        if (s) m.describe(s, &states[o]);
+    };
+    u64 inits[8 * W];
+    const int k = m.init_states(inits);
+    if (n == 0) {
+        for (int i = 0; i < k; ++i) emit(-1, &inits[i * W]);
+        return k;
+    }
+    std::vector<u64> cur;
+    for (int i = 0; i < k && cur.empty(); ++i)
+        if (fingerprint<W>(&inits[i * W]) == fps[0]) cur.assign(&inits[i * W], &inits[i * W] + W);
+    if (cur.empty()) return -1;
+    for (int j = 1; j < n; ++j) {
+        u64 mask[M::MW];
+        m.enabled(cur.data(), mask);
+        bool found = false;
+        for (int w = 0; w < M::MW && !found; ++w)
+            for (u64 bits = mask[w]; bits && !found; bits &= bits - 1) {
+                const int a = w * 64 + __builtin_ctzll(bits);
+                u64 ns[W];
+                if (m.apply(cur.data(), a, ns) && fingerprint<W>(ns) == fps[j]) {
+                    cur.assign(ns, ns + W);
+                    found = true;
+                }
+            }
+        if (!found) return -1;
+    }
+    u64 mask[M::MW];
+    m.enabled(cur.data(), mask);
+    int views = 0;
+    for (int w = 0; w < M::MW; ++w)
+        for (u64 bits = mask[w]; bits; bits &= bits - 1) {
+            const int a = w * 64 + __builtin_ctzll(bits);
+            u64 ns[W];
+            const bool ok = m.apply(cur.data(), a, ns);
+            emit(m.action_id(cur.data(), a), ok ? ns : nullptr);
+            ++views;
+        }
+    return views;
 }
 
 template <class M>
@@ -277,6 +337,10 @@ class Engine final : public EngineBase {
     int replay(int init, const i64* ids, int n, std::vector<i64>& states, std::vector<int>& conds,
                std::vector<int>* all_conds, int* terminal) const override {
         return replay_model(m_, init, ids, n, states, conds, all_conds, terminal);
+    }
+    int explore(const u64* fps, int n, std::vector<i64>& action, std::vector<int>& has, std::vector<u64>& fp,
+                std::vector<i64>& states) const override {
+        return explore_model(m_, fps, n, action, has, fp, states);
     }
 
     // The visitor's paths (src/checker/bfs.rs:187-189 builds `Path::from_fingerprints` of every
