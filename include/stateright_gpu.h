@@ -96,6 +96,10 @@ typedef struct sr_opts {
                                     sr_gpu_bfs_discovery* for the same property in the same order).
                                     The reference's join reconstructs nothing either
                                     (src/checker/bfs.rs:289-298 builds paths in discoveries()). */
+    int32_t symmetry;            /* 1 = canonical symmetry reduction (models with a canonical form:
+                                    2pc, plugins with `canonical`): one state per orbit, order-
+                                    independent counts; NOT the reference's DFS count, whose
+                                    representatives are not canonical (src/checker/dfs.rs:258-283) */
 } sr_opts;
 
 /* Timing/throughput counters of a finished run (sr_gpu_bfs_stats). */

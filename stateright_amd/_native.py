@@ -34,6 +34,7 @@ class sr_opts(ctypes.Structure):
         ("verbose", ctypes.c_int32),
         ("counters", ctypes.c_int32),
         ("defer_paths", ctypes.c_int32),
+        ("symmetry", ctypes.c_int32),
     ]
 
 

@@ -141,6 +141,16 @@ class CheckerBuilder:
         self._symmetry = True
         return self
 
+    def symmetry_canonical(self):
+        """Engine opt-in: canonical symmetry reduction. Visited states, frontier and BFS tree hold one
+        representative per orbit (2pc: RMs sorted by their full (rm_state, tm_prepared, Prepared msg)
+        tuple), so `unique_state_count` is the number of reachable orbits, the same in every visit
+        order; discovery paths are concrete paths of the original model. This is deliberately NOT the
+        reference's `symmetry().spawn_dfs()` count (665 for 2pc N=5), whose representatives sort by
+        rm_state alone and make the count depend on the DFS order (src/checker/dfs.rs:258-283)."""
+        self._opts.symmetry = 1
+        return self
+
     # --- engine-specific options ---------------------------------------------------------------
     def order(self, order):
         """"auto" (default), "fifo" (exact reference visit order) or "fast"."""
@@ -213,7 +223,8 @@ class CheckerBuilder:
         if self._symmetry:
             raise NotImplementedError(
                 "symmetry().spawn_dfs(): the symmetry-reduced count depends on the reference's "
-                "depth-first visit order (non-canonical representatives); not reproducible on the GPU")
+                "depth-first visit order (non-canonical representatives); not reproducible on the GPU. "
+                "symmetry_canonical() gives an order-independent reduction (one state per orbit)")
         self._opts.order = N.SR_ORDER_FAST
         return self.spawn_bfs()
 

@@ -510,32 +510,8 @@ class DistEngine final : public EngineBase {
     int path(int p, std::vector<i64>& actions, std::vector<i64>& states) override {
         std::vector<u64> st;
         if (!path_states(p, st)) return -1;
-        const int wd = m_.describe_width();
-        const size_t len = st.size() / W;
-        for (size_t i = 0; i < len; ++i) {
-            size_t o = states.size();
-            states.resize(o + wd);
-            m_.describe(&st[i * W], &states[o]);
-            if (i + 1 == len) break;
-            // the first action (in `actions()` order) leading to the next state
-            u64 mask[M::MW];
-            m_.enabled(&st[i * W], mask);
-            bool found = false;
-            const u64 want = fingerprint<W>(&st[(i + 1) * W]);
-            for (int w = 0; w < M::MW && !found; ++w)
-                for (u64 bits = mask[w]; bits && !found; bits &= bits - 1) {
-                    int a = w * 64 + __builtin_ctzll(bits);
-                    u64 ns[W];
-                    if (m_.apply(&st[i * W], a, ns) && fingerprint<W>(ns) == want) {
-                        actions.push_back(m_.action_id(&st[i * W], a));
-                        found = true;
-                    }
-                }
-            if (!found) throw Error(SR_ERR_NONDETERMINISM, "Unable to reconstruct a `Path` across partitions");
-        }
-        return (int)actions.size();
+        return concrete_path(m_, st, actions, states);
     }
-
   private:
     struct DiscAt {
         bool found = false;

@@ -20,6 +20,8 @@ static std::unique_ptr<EngineBase> make_model_engine(int model, const i64* p, in
     auto need = [&](int k) {
         if (np < k) throw Error(SR_ERR_ARG, "model " + std::to_string(model) + " needs " + std::to_string(k) + " params");
     };
+    if (o.symmetry && model != SR_MODEL_2PC)
+        throw Error(SR_ERR_UNSUPPORTED, "symmetry reduction: model " + std::to_string(model) + " has no canonical form");
     switch (model) {
         case SR_MODEL_LINEAR_EQUATION:
             need(3);
@@ -29,6 +31,7 @@ static std::unique_ptr<EngineBase> make_model_engine(int model, const i64* p, in
         case SR_MODEL_2PC:
             need(1);
             if (p[0] < 1 || p[0] > 14) throw Error(SR_ERR_UNSUPPORTED, "2pc: rm_count must be in 1..=14 (4n+4 <= 63 bits)");
+            if (o.symmetry) return std::make_unique<E<Canon<TwoPhase>>>(Canon<TwoPhase>(TwoPhase{(int)p[0]}), o, args...);
             return std::make_unique<E<TwoPhase>>(TwoPhase{(int)p[0]}, o, args...);
         case SR_MODEL_INCREMENT:
             need(1);

@@ -192,6 +192,61 @@ int explore_model(const M& m, const u64* fps, int n, std::vector<i64>& action, s
     return views;
 }
 
+// `Path::from_fingerprints` (src/checker/path.rs:20-86) over the states of a BFS-tree path (W words
+// each): from the init state, each step is the FIRST action in `actions()` order whose successor is
+// the next state. Under the canonical symmetry reduction (Canon<M>) the tree holds orbit
+// representatives; the path is then made concrete in the original model: an init state whose
+// representative is the first state, and at each step the first action whose successor's
+// representative is the next one. Returns the number of actions.
+template <class M>
+int concrete_path(const M& m, const std::vector<u64>& st, std::vector<i64>& actions, std::vector<i64>& states) {
+    constexpr int W = M::W;
+    const size_t len = st.size() / W;
+    if (!len) return -1;
+    const int wd = m.describe_width();
+    std::vector<u64> cur(st.begin(), st.begin() + W);
+    if constexpr (is_canon<M>::value) {
+        u64 inits[8 * W];
+        const int k = m.base().init_states(inits);
+        cur.clear();
+        for (int i = 0; i < k && cur.empty(); ++i) {
+            u64 c[W];
+            m.base().canonical(&inits[i * W], c);
+            if (std::equal(c, c + W, st.begin())) cur.assign(&inits[i * W], &inits[i * W] + W);
+        }
+        if (cur.empty()) throw Error(SR_ERR_NONDETERMINISM, "Unable to reconstruct a `Path`: no init state has the expected representative");
+    }
+    auto emit = [&](const u64* s) {
+        const size_t o = states.size();
+        states.resize(o + wd);
+        m.describe(s, &states[o]);
+    };
+    for (size_t i = 1; i < len; ++i) {
+        const u64* target = &st[i * W];
+        u64 mask[M::MW];
+        m.enabled(cur.data(), mask);
+        bool found = false;
+        for (int w = 0; w < M::MW && !found; ++w)
+            for (u64 bits = mask[w]; bits && !found; bits &= bits - 1) {
+                const int a = w * 64 + __builtin_ctzll(bits);
+                u64 ns[W];
+                if (!m.apply(cur.data(), a, ns) || !std::equal(ns, ns + W, target)) continue;
+                u64 next[W];
+                if constexpr (is_canon<M>::value) m.base().apply(cur.data(), a, next);
+                else std::copy(ns, ns + W, next);
+                emit(cur.data());
+                actions.push_back(m.action_id(cur.data(), a));
+                cur.assign(next, next + W);
+                found = true;
+            }
+        if (!found)
+            throw Error(SR_ERR_NONDETERMINISM, "Unable to reconstruct a `Path`: " + std::to_string(i) +
+                                                   " previous state(s) reconstructed but no successor is the next state");
+    }
+    emit(cur.data());
+    return (int)actions.size();
+}
+
 template <class M>
 class Engine final : public EngineBase {
     static constexpr int W = M::W;
@@ -291,42 +346,11 @@ class Engine final : public EngineBase {
 
     // `Path::from_fingerprints` (src/checker/path.rs:20-86) on the host copy of the GpuModel.
     int path(int p, std::vector<i64>& actions, std::vector<i64>& states) override {
-        std::vector<u64> fps;
-        if (chain(p, fps) == 0) return -1;
-        const int wd = m_.describe_width();
-        u64 inits[8 * W];
-        int k = m_.init_states(inits);
-        std::vector<u64> cur;
-        for (int i = 0; i < k && cur.empty(); ++i)
-            if (fingerprint<W>(&inits[i * W]) == fps[0]) cur.assign(&inits[i * W], &inits[i * W] + W);
-        if (cur.empty()) throw Error(SR_ERR_NONDETERMINISM, "Unable to reconstruct a `Path`: no init state has the expected fingerprint");
-        auto emit = [&](const u64* s) {
-            size_t o = states.size();
-            states.resize(o + wd);
-            m_.describe(s, &states[o]);
-        };
-        for (size_t i = 1; i < fps.size(); ++i) {
-            u64 mask[M::MW];
-            m_.enabled(cur.data(), mask);
-            bool found = false;
-            for (int w = 0; w < M::MW && !found; ++w)
-                for (u64 bits = mask[w]; bits && !found; bits &= bits - 1) {
-                    int a = w * 64 + __builtin_ctzll(bits);
-                    u64 ns[W];
-                    if (!m_.apply(cur.data(), a, ns)) continue;
-                    if (fingerprint<W>(ns) == fps[i]) {
-                        emit(cur.data());
-                        actions.push_back(m_.action_id(cur.data(), a));
-                        cur.assign(ns, ns + W);
-                        found = true;
-                    }
-                }
-            if (!found)
-                throw Error(SR_ERR_NONDETERMINISM, "Unable to reconstruct a `Path`: " + std::to_string(i) +
-                                                       " previous state(s) reconstructed but no successor has the next fingerprint");
-        }
-        emit(cur.data());
-        return (int)actions.size();
+        if (p < 0 || p >= M::NPROPS || !disc[p].found) return -1;
+        SR_HIP(hipSetDevice(o_.device));
+        std::vector<u64> st;
+        tree_path(disc[p].level, disc[p].rank, st);
+        return concrete_path(m_, st, actions, states);
     }
 
     i64 action_id_bound() const override { return m_.action_id_bound(); }
@@ -1083,9 +1107,19 @@ void* plugin_create(Make make, const int64_t* p, int32_t np, const sr_opts* opts
     try {
         const sr_opts o = normalized_opts(opts);
         M m = make(p, np, o.device);
-        EngineBase* e;
-        if (comm || vparts > 1) e = new DistEngine<M>(m, o, static_cast<Comm*>(comm), (int)vparts);
-        else e = new Engine<M>(m, o);
+        EngineBase* e = nullptr;
+        if (o.symmetry) {
+            if constexpr (has_canonical<M>::value) {
+                if (comm || vparts > 1) e = new DistEngine<Canon<M>>(Canon<M>(m), o, static_cast<Comm*>(comm), (int)vparts);
+                else e = new Engine<Canon<M>>(Canon<M>(m), o);
+            } else {
+                throw Error(SR_ERR_UNSUPPORTED, "symmetry reduction: the plugin model has no `canonical`");
+            }
+        } else if (comm || vparts > 1) {
+            e = new DistEngine<M>(m, o, static_cast<Comm*>(comm), (int)vparts);
+        } else {
+            e = new Engine<M>(m, o);
+        }
         return e;
     } catch (const std::exception& x) {
         if (err && errcap > 0) std::snprintf(err, (size_t)errcap, "%s", x.what());

@@ -55,6 +55,42 @@ template <class M>
 struct has_undescribe<M, std::void_t<decltype(std::declval<const M&>().undescribe((const i64*)nullptr, (u64*)nullptr))>>
     : std::true_type {};
 
+// Models with a canonical representative under their symmetry (`canonical(s, out)`).
+template <class M, class = void>
+struct has_canonical : std::false_type {};
+template <class M>
+struct has_canonical<M, std::void_t<decltype(std::declval<const M&>().canonical((const u64*)nullptr, (u64*)nullptr))>>
+    : std::true_type {};
+
+// The symmetry-reduced view of a model (the engine's opt-in canonical reduction): init states and
+// successors are replaced by their canonical representatives, so the visited set, the frontier and
+// the BFS tree hold one state per orbit. Everything else is the model's own.
+template <class M>
+struct Canon : M {
+    Canon() = default;
+    explicit Canon(const M& m) : M(m) {}
+    const M& base() const { return *this; }
+    SR_HD bool apply(const u64* s, int a, u64* o) const {
+        u64 t[M::W];
+        if (!M::apply(s, a, t)) return false;
+        M::canonical(t, o);
+        return true;
+    }
+    int init_states(u64* out) const {
+        const int k = M::init_states(out);
+        for (int i = 0; i < k; ++i) {
+            u64 t[M::W];
+            M::canonical(out + i * M::W, t);
+            for (int w = 0; w < M::W; ++w) out[i * M::W + w] = t[w];
+        }
+        return k;
+    }
+};
+template <class M>
+struct is_canon : std::false_type {};
+template <class M>
+struct is_canon<Canon<M>> : std::true_type {};
+
 // murmur3 fmix64: a bijection on u64 with fmix64(0) == 0.
 SR_HD u64 fmix64(u64 k) {
     k ^= k >> 33;
@@ -251,6 +287,28 @@ struct TwoPhase {
         s |= ((u64)d[k++] & 1) << (4 * n + 2);
         s |= ((u64)d[k++] & 1) << (4 * n + 3);
         sp[0] = s;
+    }
+    // Canonical representative under permutations of the resource managers (the symmetry the
+    // reference's `representative` exploits, examples/2pc.rs:156-187): the per-RM tuples
+    // (rm_state, tm_prepared, Prepared{rm} in msgs) sorted ascending by that 4-bit key. Unlike the
+    // reference's sort by rm_state alone (ties kept in index order), equal orbits always give equal
+    // words, so the reduced state count does not depend on the visit order.
+    SR_HD void canonical(const u64* sp, u64* o) const {
+        const u64 s = sp[0];
+        u32 cnt[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) cnt[k] = 0;
+        for (int rm = 0; rm < n; ++rm) {
+            const u32 key = (u32)((s >> (2 * rm)) & 3) | (u32)((s >> (2 * n + 2 + rm)) & 1) << 2 |
+                            (u32)((s >> (3 * n + 2 + rm)) & 1) << 3;
+            ++cnt[key];
+        }
+        u64 r = s & (3ull << (2 * n) | 3ull << (4 * n + 2));  // tm_state, Commit, Abort
+        int rm = 0;
+        for (u32 key = 0; key < 16; ++key)
+            for (u32 c = 0; c < cnt[key]; ++c, ++rm)
+                r |= (u64)(key & 3) << (2 * rm) | (u64)(key >> 2 & 1) << (2 * n + 2 + rm) | (u64)(key >> 3 & 1) << (3 * n + 2 + rm);
+        o[0] = r;
     }
     i64 action_id(const u64*, int a) const { return a; }
     i64 action_id_bound() const { return 2 + 5 * n; }
