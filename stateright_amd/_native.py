@@ -58,6 +58,7 @@ class sr_stats(ctypes.Structure):
         ("head_levels", ctypes.c_uint64),
         ("probes", ctypes.c_uint64),
         ("cas", ctypes.c_uint64),
+        ("multi_levels", ctypes.c_uint64),
     ]
 
     def as_dict(self):

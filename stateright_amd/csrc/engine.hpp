@@ -561,6 +561,7 @@ class Engine final : public EngineBase {
         stats.order_used = (u32)order;
         launch_ms.clear();
         launch_frontier.clear();
+        seq_launch_.clear();
 
         // Visited set sized for <= table_load_ load at the hinted unique count.
         u64 cap = std::max<u64>((u64)(1u << 20) * grow_factor_, min_table_cap(m_));
@@ -600,7 +601,8 @@ class Engine final : public EngineBase {
         // FAST pipelined order: level 0 is enqueued before the host reads the roots' outcome (it is
         // ignored if the roots already discover every property)
         const bool pipelined = !fifo_ && !emask_ && !o_.target_state_count && M::NPROPS > 0 && pipeline_;
-        const u32 sq_level0 = pipelined ? launch_sync((u64)k, (1u << M::NPROPS) - 1) : 0u;
+        bool multi0 = false;
+        const u32 sq_level0 = pipelined ? launch_next((u64)k, (1u << M::NPROPS) - 1, multi0) : 0u;
         wait_publish(sq);
         state_count = (u64)k;
         unique = lc_.claims;
@@ -610,7 +612,7 @@ class Engine final : public EngineBase {
         u32 level = 0;
         bool order_dependent = false;
         auto t_loop = Clock::now();
-        if (pipelined) order_dependent = pipeline_levels(n, sq_level0);
+        if (pipelined) order_dependent = pipeline_levels(n, sq_level0, multi0);
         else for (;;) {
             // 1. Discoveries among this level's states (evaluated when they were produced).
             u32 newly = 0, max_rank = 0;
@@ -757,24 +759,24 @@ class Engine final : public EngineBase {
     // the visited set or the arena might not hold it (that level is then launched after the wait,
     // sized exactly). A speculative level launched past the end (an exhausted frontier or an early
     // exit) is ignored. Returns whether the run stopped early inside a level.
-    bool pipeline_levels(u64 n, u32 sq_level0) {
+    bool pipeline_levels(u64 n, u32 sq_level0, bool multi) {
         u32 undiscovered = (1u << M::NPROPS) - 1;
         u32 level = 0;
         bool order_dependent = false;
-        auto discoveries_of = [&](u32 lvl, u32& max_rank) {
+        auto discoveries_of = [&](u32 lvl, const HostCounters& c, u32& max_rank) {
             u32 newly = 0;
             for (int p = 0; p < M::NPROPS; ++p)
-                if ((undiscovered >> p & 1) && lc_.disc[p] != ~0u) {
+                if ((undiscovered >> p & 1) && c.disc[p] != ~0u) {
                     newly |= 1u << p;
-                    max_rank = std::max(max_rank, lc_.disc[p]);
+                    max_rank = std::max(max_rank, c.disc[p]);
                     disc[p].found = true;
                     disc[p].level = lvl;
-                    disc[p].rank = lc_.disc[p];
+                    disc[p].rank = c.disc[p];
                 }
             return newly;
         };
         u32 max_rank = 0;
-        u32 newly = discoveries_of(0, max_rank);  // among the init states (roots publish)
+        u32 newly = discoveries_of(0, lc_, max_rank);  // among the init states (roots publish)
         undiscovered &= ~newly;
         if (newly && undiscovered == 0) {
             lvisited_.push_back(max_rank + 1);
@@ -783,46 +785,33 @@ class Engine final : public EngineBase {
             fill_discovery_fps();
             return true;
         }
-        u32 sq = sq_level0;  // enqueued before the roots' outcome was read
-        for (;;) {
-            // enqueue the next level before waiting for this one
-            const double g = std::max(ratio_, 1.0) * 1.5;
-            const u64 est1 = (u64)((double)n * g) + 1024;     // the next frontier
-            const u64 est2 = (u64)((double)est1 * g) + 1024;  // the states it will claim
-            const u64 nb_next = lstart_.back();
-            const bool spec = !pessimistic_ && (double)(unique + est1 + est2) < 0.8 * (double)cap_ &&
-                              nb_next + est1 + est2 <= arena_cap_;
-            // launch shape: a tight estimate (the grid strides over any excess)
-            const u64 shape = (u64)((double)n * std::max(ratio_, 0.05) * 1.1) + 64;
-            u32 sq_next = spec ? launch_expand(nb_next, 0, true, shape, undiscovered) : 0;
-
-            wait_publish(sq);  // lc_ = this level's counters
-            const u64 produced = lc_.claims;
-            state_count += lc_.successors;
+        // One level's outcome (counters c); false when the check is over.
+        auto account = [&](const HostCounters& c, const char* how) -> bool {
+            const u64 produced = c.claims;
+            state_count += c.successors;
             unique += produced;
-            stats.successors += lc_.successors;
-            stats.probes += lc_.probes;
-            stats.cas += lc_.cas;
-            if (level < launch_frontier.size()) launch_frontier[level] = n;  // one launch per level
-            stats.algorithmic_bytes += n * 8 * W + lc_.successors * 8 + produced * (16 + 8 * W);
+            stats.successors += c.successors;
+            stats.probes += c.probes;
+            stats.cas += c.cas;
+            stats.algorithmic_bytes += n * 8 * W + c.successors * 8 + produced * (16 + 8 * W);
             stats.levels++;
             ratio_ = (double)produced / (double)n;
-            en_ratio_ = std::max(1.0, (double)lc_.enabled / (double)n);
+            en_ratio_ = std::max(1.0, (double)c.enabled / (double)n);
             lvisited_.push_back(n);
             if (o_.verbose)
                 std::fprintf(stderr, "[sr] level %u: frontier %llu succ %llu new %llu unique %llu cap %llu%s\n", level,
-                             (unsigned long long)n, (unsigned long long)lc_.successors, (unsigned long long)produced,
-                             (unsigned long long)unique.load(), (unsigned long long)cap_, spec ? " (next enqueued)" : "");
+                             (unsigned long long)n, (unsigned long long)c.successors, (unsigned long long)produced,
+                             (unsigned long long)unique.load(), (unsigned long long)cap_, how);
             if (produced == 0) {  // exhausted (a speculative launch saw an empty frontier)
                 reference_done = true;
-                break;
+                return false;
             }
             max_depth = level + 1;
             lstart_.push_back(lstart_.back() + produced);
             n = produced;
             ++level;
             max_rank = 0;
-            newly = discoveries_of(level, max_rank);
+            newly = discoveries_of(level, c, max_rank);
             undiscovered &= ~newly;
             if (newly && undiscovered == 0) {
                 // every property discovered inside this level: the reference stops at that pop
@@ -831,13 +820,107 @@ class Engine final : public EngineBase {
                 lvisited_.push_back(max_rank + 1);
                 reference_done = true;
                 order_dependent = true;
-                break;
+                return false;
             }
-            sq = spec ? sq_next : launch_sync(n, undiscovered);
+            return true;
+        };
+        u32 sq = sq_level0;  // enqueued before the roots' outcome was read
+        for (;;) {
+            if (multi) {
+                // a multi-level launch: the per-level counters of every level it ran
+                wait_publish(sq);
+                const u32 k = lc_.aux;
+                if (k == 0 || k > (u32)MULTI_MAX_LEVELS) throw Error(SR_ERR_HIP, "multi-level launch: bad level count");
+                std::vector<LevelCounters> recs(k);
+                u32 merr = 0;
+                MultiCtl* mc = reinterpret_cast<MultiCtl*>(multi_.p);
+                SR_HIP(hipMemcpyAsync(recs.data(), mc->lcs, k * sizeof(LevelCounters), hipMemcpyDeviceToHost, stream_));
+                SR_HIP(hipMemcpyAsync(&merr, &mc->err, sizeof(u32), hipMemcpyDeviceToHost, stream_));
+                SR_HIP(hipStreamSynchronize(stream_));
+                if (merr) throw Error(SR_ERR_HIP, "multi-level launch: the device-wide barrier timed out");
+                stats.multi_levels += k;
+                bool go = true;
+                for (u32 i = 0; i < k && go; ++i) {
+                    HostCounters c{};
+                    c.successors = recs[i].successors;
+                    c.enabled = recs[i].enabled;
+                    c.probes = recs[i].probes;
+                    c.cas = recs[i].cas;
+                    c.claims = recs[i].claims;
+                    c.err = recs[i].err;
+                    for (int p = 0; p < M::NPROPS; ++p) c.disc[p] = recs[i].disc[p];
+                    if (c.err & ERR_TABLE_FULL) throw Error(SR_ERR_CAPACITY, "visited set probe limit exceeded");
+                    if (c.err & ERR_FRONTIER_OVERFLOW) throw Error(SR_ERR_CAPACITY, "frontier overflow");
+                    go = account(c, " (multi-level launch)");
+                }
+                if (!go) break;
+                sq = launch_next(n, undiscovered, multi);
+                continue;
+            }
+            // enqueue the next level before waiting for this one, unless it is predicted small:
+            // the multi-level form is then launched after the wait, sized exactly
+            const double g = std::max(ratio_, 1.0) * 1.5;
+            const u64 est1 = (u64)((double)n * g) + 1024;     // the next frontier
+            const u64 est2 = (u64)((double)est1 * g) + 1024;  // the states it will claim
+            const u64 nb_next = lstart_.back();
+            const bool small_next = multi_max_n_ && (double)n * ratio_ <= (double)multi_max_n_;
+            const bool spec = !pessimistic_ && !small_next && (double)(unique + est1 + est2) < 0.8 * (double)cap_ &&
+                              nb_next + est1 + est2 <= arena_cap_;
+            // launch shape: a tight estimate (the grid strides over any excess)
+            const u64 shape = (u64)((double)n * std::max(ratio_, 0.05) * 1.1) + 64;
+            u32 sq_next = spec ? launch_expand(nb_next, 0, true, shape, undiscovered) : 0;
+
+            wait_publish(sq);  // lc_ = this level's counters
+            auto it = seq_launch_.find(sq);
+            if (it != seq_launch_.end() && it->second < launch_frontier.size()) launch_frontier[it->second] = n;
+            if (!account(lc_, spec ? " (next enqueued)" : "")) break;
+            sq = spec ? sq_next : launch_next(n, undiscovered, multi);
         }
         (void)hipStreamSynchronize(stream_);
         fill_discovery_fps();
         return order_dependent;
+    }
+
+    // The next level after a host wait: the multi-level form when its frontier is small (and the
+    // visited set and arena leave room for it), otherwise one ordinary launch.
+    u32 launch_next(u64 n, u32 undiscovered, bool& multi) {
+        multi = false;
+        if (multi_max_n_ && n <= multi_max_n_) {
+            const u64 fbase = lstart_[lstart_.size() - 2];
+            const u64 d_eff = std::min<u64>(D_, (u64)std::ceil(2.0 * ratio_ + 1.0));
+            while ((double)(unique + n * d_eff) > 0.8 * (double)cap_) grow_table();
+            ensure_arena(fbase + n + std::max<u64>(n * D_, multi_arena_min_), fbase + n);
+            const u64 nbase = fbase + n;
+            const u64 room_t = (u64)(0.8 * (double)cap_) > unique.load() ? (u64)(0.8 * (double)cap_) - unique.load() : 0;
+            const u64 room_a = arena_cap_ > nbase ? arena_cap_ - nbase : 0;
+            const u64 budget = std::min(room_t, room_a);
+            if (budget >= n * D_) {
+                multi = true;
+                return launch_multi(fbase, (u32)n, undiscovered, budget);
+            }
+        }
+        return launch_sync(n, undiscovered);
+    }
+
+    u32 launch_multi(u64 fbase, u32 n, u32 undiscovered, u64 budget) {
+        if (!multi_.p) multi_.alloc(o_.device, (sizeof(MultiCtl) + 7) / 8);
+        if (!multi_grid_) {
+            int cus = 0;
+            SR_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, o_.device));
+            multi_grid_ = (u32)std::max(1, cus);  // one workgroup per CU: always resident
+        }
+        MultiCtl* mc = reinterpret_cast<MultiCtl*>(multi_.p);
+        multi_init<<<1, 256, 0, stream_>>>(mc, multi_max_n_, (u32)MULTI_MAX_LEVELS, D_, budget);
+        SR_HIP(hipGetLastError());
+        const u32 sq = next_seq();
+        const u64 nbase = fbase + n;
+        const u32 ncap = (u32)std::min<u64>(arena_cap_ - nbase, 0xffffffffu);
+        timed([&] {
+            expand_fast<M, 1, 0, false, true><<<multi_grid_, 256, filt_log2_ ? (8u << filt_log2_) : 0u, stream_>>>(
+                m_, arena_.p + fbase * W, 0u, n, view(), arena_.p + nbase * W, apar_.p + nbase, ncap, lc_d_, undiscovered,
+                hcd(sq), sq, 0u, 2u, filt_log2_, 0u, mc);
+        }, n);
+        return sq;
     }
 
     // Launch of the level whose frontier (n states) ends the arena, after the previous one is done:
@@ -876,11 +959,12 @@ class Engine final : public EngineBase {
         const u32 ncap = (u32)std::min<u64>(arena_cap_ - nbase, 0xffffffffu);
         const u32 ppw_log2 = ppw_env_ >= 0 ? (u32)ppw_env_ : ppw_for(shape);
         const u32 grid = std::min(expand_grid_cap(), std::max<u32>(1, blocks_for((shape + (1u << ppw_log2) - 1) >> ppw_log2, 4)));
+        seq_launch_[sq] = launch_frontier.size();
         timed([&] {
             auto launch = [&](auto kern) {
                 kern<<<grid, 256, filt_log2_ ? (8u << filt_log2_) : 0u, stream_>>>(
                     m_, arena_.p + fbase * W, 0u, n, view(), arena_.p + nbase * W, apar_.p + nbase, ncap, lc_d_,
-                    undiscovered, hcd(sq), sq, 1u, ppw_log2, filt_log2_, dev_n ? 1u : 0u);
+                    undiscovered, hcd(sq), sq, 1u, ppw_log2, filt_log2_, dev_n ? 1u : 0u, nullptr);
             };
             if (o_.counters) launch(expand_fast<M, 1, 0, true>);
             else switch (probe_batch_ * 10 + probe_load_) {
@@ -968,7 +1052,7 @@ class Engine final : public EngineBase {
                     auto launch = [&](auto kern) {
                         kern<<<grid, 256, filt_log2_ ? (8u << filt_log2_) : 0u, stream_>>>(
                             m_, cur(), ulo, uhi, view(), next, npar, ncap, lc_d_, undiscovered, hcd(sq), sq,
-                            last ? 1u : 0u, ppw_log2, filt_log2_, 0u);
+                            last ? 1u : 0u, ppw_log2, filt_log2_, 0u, nullptr);
                     };
                     if (o_.counters) launch(expand_fast<M, 1, 0, true>);
                     else switch (probe_batch_ * 10 + probe_load_) {
@@ -1047,6 +1131,14 @@ class Engine final : public EngineBase {
     u32 grid_max_ = 0;       // cap on expand_fast's grid, 0 = two device residencies (SR_GRID_MAX)
     u64 query_mask_ = 4095;  // spins between hipStreamQuery calls in wait_publish (SR_QUERY_LOG2)
     bool pipeline_ = true;  // FAST-order level pipelining (SR_PIPELINE=0 disables, for A/B runs)
+    // Multi-level launches for frontiers up to multi_max_n_ states (SR_MULTI_MAX_N; 0 = off, the
+    // default: measured no faster than pipelined single-level launches, a small level costs ~16 us
+    // either way, profiles/r02_multi_level_ab.txt).
+    u32 multi_max_n_ = std::getenv("SR_MULTI_MAX_N") ? (u32)std::atoi(std::getenv("SR_MULTI_MAX_N")) : 0;
+    u64 multi_arena_min_ = 1u << 20;  // arena room reserved ahead of a multi-level launch (states)
+    u32 multi_grid_ = 0;              // its workgroups: one per CU
+    DBuf<u64> multi_;                 // its MultiCtl
+    std::map<u32, size_t> seq_launch_;  // launch sequence number -> index in launch_frontier
     u32 filt_log2_ = W >= 4 ? 10 : 9;  // block-local duplicate filter (SR_FILTER_LOG2 sweep in profiles/)
     bool pessimistic_ = false;  // size chunks for max out-degree new states per parent
     u64 grow_factor_ = 1;       // initial-capacity multiplier after a capacity restart
