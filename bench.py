@@ -199,7 +199,9 @@ def measure_config4(args, world, comm, dev, barrier):
     check()  # warmup: allocations
     barrier()
     t0 = time.perf_counter()
+    c = None
     for _ in range(args.config4_steps):
+        c = None
         c = check()
     barrier()
     el = time.perf_counter() - t0
@@ -276,6 +278,8 @@ def main():
             raise SystemExit(f"wrong unique count {c.unique_state_count()} != {expect_unique}")
         return c
 
+    # A finished checker holds its visited set and arena until it is freed: drop the previous one
+    # before the next check allocates (increment_lock N=12 needs ~200 GB of the 288).
     for _ in range(args.warmup):
         step()
 
@@ -290,7 +294,9 @@ def main():
     barrier()
     t0 = time.perf_counter()
     unique = 0
+    c = None
     for _ in range(args.steps):
+        c = None
         c = step()
         unique += c.unique_state_count()
     barrier()
@@ -304,7 +310,9 @@ def main():
     last = None
     barrier()
     t1 = time.perf_counter()
+    c = None
     for _ in range(args.steps):
+        c = last = None
         c = step(profile=True)
         st = c.stats()
         kernel_ms += st["expand_kernel_ms"]
@@ -315,6 +323,11 @@ def main():
     profiled_elapsed = time.perf_counter() - t1
     # Counter pass (untimed): visited-set probes and CAS claims per check, from a counting variant
     # of the expand kernel; the rates divide them by the event-timed kernel time of the pass above.
+    c, st = last
+    last = None
+    prof = c.launch_profile() if not partitioned else []
+    final_state_count = c.state_count()
+    c = None
     probes = cas = 0
     for _ in range(args.steps):
         stc = step(counters=True).stats()
@@ -328,9 +341,7 @@ def main():
     if args.config4_steps > 0 and args.model == "2pc":
         config4 = measure_config4(args, world, comm, dev, barrier)
 
-    c, st = last
     if rank != 0:
-        del c
         comm.close()
         return
 
@@ -350,7 +361,6 @@ def main():
         fracs["cas_rate"] = cas_rate / RANDOM_CAS_PEAK
     # Per-level split of the last profiled check: big levels, small levels, and the span between
     # launches (level boundaries: dispatch, ramp/drain, host planning).
-    prof = c.launch_profile() if not partitioned else []
     big = sum(ms for ms, _ in prof if ms >= BIG_LEVEL_MS)
     small = sum(ms for ms, _ in prof if ms < BIG_LEVEL_MS)
     span_ms = st["level_loop_sec"] * 1e3
@@ -378,7 +388,7 @@ def main():
             "comm": comm.kind() if comm is not None else None,
             "rccl_nranks": comm.nranks() if comm is not None else None,
         },
-        "state_count_per_sec": float(c.state_count()) * (1 if partitioned else world) * args.steps / elapsed,
+        "state_count_per_sec": float(final_state_count) * (1 if partitioned else world) * args.steps / elapsed,
         "roofline": {
             "bound": "hbm",
             "limiter": max(fracs, key=fracs.get),
