@@ -566,9 +566,12 @@ __global__ void __launch_bounds__(256) expand_fast(M m, const u64* __restrict__ 
     extern __shared__ u64 filt[];       // 2^filt_log2 fingerprints (dynamic LDS; 0 = no filter)
     __shared__ u64 stage[STAGE * W];
     __shared__ u32 stage_par[STAGE];
-    __shared__ u64 pst[4][64 * W];      // parent states of each wave
-    __shared__ u64 pmask[4][64 * MW];   // their enabled-action masks
-    __shared__ u32 pexcl[4][64];        // exclusive prefix of their successor counts
+    // Parents per wave at most: wide states (paxos, W = 11) take few parents per wave (ppw_for), and
+    // staging 64 of them cost 22.5 KB of LDS per block, which capped residency at 3 blocks per CU.
+    constexpr u32 PPW_LOG2_MAX = W >= 4 ? 4 : 6;
+    __shared__ u64 pst[4][(1 << PPW_LOG2_MAX) * W];     // parent states of each wave
+    __shared__ u64 pmask[4][(1 << PPW_LOG2_MAX) * MW];  // their enabled-action masks
+    __shared__ u32 pexcl[4][64];                        // exclusive prefix of their successor counts
     __shared__ u32 stage_n, base, scratch[4];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     if (threadIdx.x == 0) stage_n = 0;
@@ -584,6 +587,7 @@ __global__ void __launch_bounds__(256) expand_fast(M m, const u64* __restrict__ 
     // Each wave takes ppw = 2^ppw_log2 <= 64 parents (small levels use fewer parents per wave so
     // that their successors spread over more waves: shorter per-lane probe chains). The grid
     // strides over chunks of 4 waves (a pipelined launch is sized from an estimate of the frontier).
+    ppw_log2 = min(ppw_log2, PPW_LOG2_MAX);
     const u32 ppw = 1u << ppw_log2;
     const u64 chunk = (u64)(blockDim.x >> 6) << ppw_log2;
     const u32 fmask = filt_log2 ? (1u << filt_log2) - 1 : 0;
