@@ -262,7 +262,9 @@ def main():
     if world > 1 or args.mode == "rccl1":
         from stateright_amd.distributed import Communicator
         with stdout_to_stderr():
-            comm = Communicator.from_env(device=dev) if world > 1 else Communicator(0, 1, Communicator.unique_id(), dev)
+            # under a launcher (RANK set) every rank bootstraps from its environment, also at N=1
+            comm = (Communicator.from_env(device=dev) if "RANK" in os.environ
+                    else Communicator(0, 1, Communicator.unique_id(), dev))
 
     def step(profile=False, counters=False):
         b = make().checker().capacity_hint(expect_unique).device(dev)
