@@ -9,7 +9,7 @@ set -e
 export TMPDIR=/tmp
 OUT=gpurun_out/pmc_traffic
 mkdir -p $OUT
-CMD="python3 bench.py --steps 2 --warmup 1 --cpu-baseline 0"
+CMD="python3 bench.py --steps 2 --warmup 1 --cpu-baseline 0 --config4-steps 0"
 timeout -k 10 180 rocprofv3 --pmc TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_ATOMIC_sum --kernel-trace --output-format csv -d $OUT/a -o a -- $CMD > $OUT/a.log 2>&1
 timeout -k 10 180 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $OUT/b -o b -- $CMD > $OUT/b.log 2>&1
 python3 - <<'PY'
