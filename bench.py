@@ -225,9 +225,11 @@ def main():
     if world != args.gpus:
         raise SystemExit(f"rank {rank}: WORLD_SIZE={world} but --gpus {args.gpus}")
     if args.dry_run:
-        print(json.dumps({"dry_run": True, "rank": rank, "world_size": world, "local_rank": local_rank,
-                          "device": local_rank if world > 1 else 0, "mode": args.mode,
-                          "master": f"{os.environ.get('MASTER_ADDR')}:{os.environ.get('MASTER_PORT')}"}), flush=True)
+        plan = json.dumps({"dry_run": True, "rank": rank, "world_size": world, "local_rank": local_rank,
+                           "device": local_rank if world > 1 else 0, "mode": args.mode,
+                           "master": f"{os.environ.get('MASTER_ADDR')}:{os.environ.get('MASTER_PORT')}"})
+        sys.stdout.flush()
+        os.write(1, (plan + "\n").encode())  # one write: the ranks share the launcher's stdout pipe
         return
 
     import math

@@ -1,36 +1,40 @@
-"""Partitioned-search timing (2pc N=9, one GPU) over route-kernel knobs: record stage words and the
-block filter. Virtual partitions and a one-rank RCCL communicator; best of 5 full checks."""
+"""Partitioned-search timing (2pc N=9, one GPU, T virtual partitions) over the route kernel's knobs:
+record-stage words (SR_RSTAGE_WORDS), parents per wave (SR_ROUTE_PPW_LOG2, -1 = the host rule)
+and the sent cache (SR_SEND_CACHE). Best of REPS full checks per point."""
+import itertools
 import os
 import sys
 import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from stateright_amd import TwoPhaseSys  # noqa: E402
-from stateright_amd.distributed import Communicator  # noqa: E402
 
-n = 9
+n = int(os.environ.get("N", "9"))
 want = 6 ** n + 4 ** n + 2 ** n
-comm = Communicator(0, 1, Communicator.unique_id(), 0)
+reps = int(os.environ.get("REPS", "3"))
 
 
-def best(make, reps=5):
+def best(parts):
     t = 1e9
     for _ in range(reps + 1):
         t0 = time.perf_counter()
-        c = make().spawn_bfs().join()
+        c = TwoPhaseSys(n).checker().partitions(parts).capacity_hint(want).defer_paths().spawn_bfs().join()
         t = min(t, time.perf_counter() - t0)
         assert c.unique_state_count() == want
-    return t * 1e3, c.stats()
+        st = c.stats()
+        del c
+    return t * 1e3, st
 
 
-for head in ["0", "65536"]:
-    os.environ["SR_HEAD_MAX"] = head
-    line = [f"head_max={head}:"]
-    for parts in (2, 4, 8):
-        ms, st = best(lambda: TwoPhaseSys(n).checker().partitions(parts).capacity_hint(want))
-        line.append(f"T{parts} {ms:.2f}ms rec={st['records_routed'] / 1e6:.1f}M head={st['head_levels']} "
-                    f"restarts={st['restarts']}")
-    ms, st = best(lambda: TwoPhaseSys(n).checker().comm(comm).capacity_hint(want))
-    line.append(f"rccl1 {ms:.2f}ms head={st['head_levels']} restarts={st['restarts']}")
-    print("  ".join(line), flush=True)
-comm.close()
+grid = itertools.product(os.environ.get("PARTS", "2,8").split(","), os.environ.get("RSTAGE", "1024,2048,4096").split(","),
+                         os.environ.get("PPW", "-1,5,6").split(","), os.environ.get("CACHE", "1,0").split(","))
+for parts, rs, ppw, cache in grid:
+    os.environ["SR_RSTAGE_WORDS"] = rs
+    os.environ["SR_SEND_CACHE"] = cache
+    if ppw == "-1":
+        os.environ.pop("SR_ROUTE_PPW_LOG2", None)
+    else:
+        os.environ["SR_ROUTE_PPW_LOG2"] = ppw
+    ms, st = best(int(parts))
+    print(f"T={parts} rstage={rs} ppw_log2={ppw} cache={cache}: {ms:.2f} ms  records={st['records_routed'] / 1e6:.1f}M "
+          f"restarts={st['restarts']}", flush=True)

@@ -1429,16 +1429,18 @@ class DistEngine final : public EngineBase {
         u32 l = 2;
         while (l < 6 && (double)(2u << l) <= ppw) ++l;
         while (l > 2 && ((c + (1u << l) - 1) >> l) < 1024) --l;
-        // a chunk (4 waves) must fit the LDS record stage
-        const double rstage = (double)std::max<u32>(rstage_recs(), 1);
-        while (l > 2 && 4.0 * (double)(1u << l) * rec_ratio_ * 1.3 > rstage) --l;
+        // a chunk (4 waves) must fit the LDS record stage (one partition stages no records: the
+        // clamp would force 4 parents per wave, one partly filled round each)
+        if (const u32 rs = rstage_recs())
+            while (l > 2 && 4.0 * (double)(1u << l) * rec_ratio_ * 1.3 > (double)rs) --l;
         return l;
     }
     double rec_ratio_ = 4.0;  // remote records per parent, last level
     // Records staged per chunk in LDS (none with one partition), and expand_route's dynamic LDS.
     u32 rstage_recs() const { return T_ > 1 ? rstage_words_ / REC : 0u; }
     size_t route_lds() const {
-        return (filt_log2_ ? (8u << filt_log2_) : 0u) + (size_t)rstage_recs() * (REC * 8 + 2 + 1);
+        return (filt_log2_ ? (8u << filt_log2_) : 0u) + (size_t)rstage_recs() * (REC * 8 + 2 + 1) +
+               (size_t)route_local_stage(T_, W) * (W * 8 + 4);
     }
     u32 rstage_words_ = std::getenv("SR_RSTAGE_WORDS") ? (u32)std::atoi(std::getenv("SR_RSTAGE_WORDS")) : 1024;
     int route_ppw_env_ = std::getenv("SR_ROUTE_PPW_LOG2") ? std::atoi(std::getenv("SR_ROUTE_PPW_LOG2")) : -1;

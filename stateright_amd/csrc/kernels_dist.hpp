@@ -72,6 +72,14 @@ __device__ __forceinline__ bool last_block(LevelCounters* lc) {
     return is_last != 0;
 }
 
+// Local new states expand_route stages per chunk (states of W words): a partition keeps ~1/T of its
+// new states (a growth level of 2pc makes ~3 per parent, 768 per 256-parent chunk), so the stage
+// shrinks with T and leaves its LDS to the record stage: LDS per block sets residency, and the
+// probes of this kernel are latency-bound.
+__host__ __device__ __forceinline__ u32 route_local_stage(u32 nparts, int W) {
+    return (nparts <= 1 ? 1024u : nparts == 2 ? 512u : 256u) / (u32)W;
+}
+
 // Expands the frontier of this partition (its size n is read from ctl). Same structure as
 // expand_fast (kernels.hpp): waves of ppw parents, successors load-balanced over the lanes, PB
 // successors per lane per round with their probes issued back to back, and the block-local LDS
@@ -93,18 +101,18 @@ __global__ void __launch_bounds__(256) expand_route(M m, u64* __restrict__ arena
                                                     u32 ppw_log2, u32 filt_log2, u64 bucket_stride, u32 lag,
                                                     u64* __restrict__ sent, u64 sent_mask, u32 rs) {
     constexpr int W = M::W, MW = M::MW, REC = W;
-    constexpr int STAGE = 512 / W;          // local new states staged per chunk
-    // Dynamic LDS: [filter: 2^filt_log2 fingerprints][record stage: rs x REC words][ranks: rs u16]
-    // [owners: rs u8]. rs (records staged per chunk, all owners) is chosen on the host: 0 with one
-    // partition, so the one-partition launch keeps expand_fast's occupancy.
+    // Dynamic LDS: [filter: 2^filt_log2 fingerprints][record stage: rs x REC words][local stage:
+    // ls x W words][its parents' frontier ranks: ls u32][record ranks: rs u16][record owners: rs u8].
+    // rs (records staged per chunk, all owners) is chosen on the host: 0 with one partition, so the
+    // one-partition launch keeps expand_fast's occupancy; ls = route_local_stage(nparts).
     extern __shared__ u64 dyn[];
-    const u32 RSTAGE = rs;
+    const u32 RSTAGE = rs, STAGE = route_local_stage(nparts, W);
     u64* filt = dyn;
     u64* rstage = dyn + (filt_log2 ? (1u << filt_log2) : 0u);
-    u16* rrank = reinterpret_cast<u16*>(rstage + (u64)rs * REC);
+    u64* stage = rstage + (u64)rs * REC;
+    u32* stage_par = reinterpret_cast<u32*>(stage + (u64)STAGE * W);  // the gid is formed at flush
+    u16* rrank = reinterpret_cast<u16*>(stage_par + STAGE);
     u8* rown = reinterpret_cast<u8*>(rrank + rs);
-    __shared__ u64 stage[STAGE * W];
-    __shared__ u64 stage_par[STAGE];
     __shared__ u32 ocnt[MAX_PARTS], obase[MAX_PARTS];
     __shared__ u64 pst[4][64 * W];
     __shared__ u64 pmask[4][64 * MW];
@@ -253,7 +261,7 @@ __global__ void __launch_bounds__(256) expand_route(M m, u64* __restrict__ arena
                             const u32 kk = sb + below;
 #pragma unroll
                             for (int x = 0; x < W; ++x) stage[kk * W + x] = ns[j][x];
-                            stage_par[kk] = pg;
+                            stage_par[kk] = (u32)(wave0 + par[j]);
                         } else {
                             const u32 pos = gb + (below - in_stage);
                             if (pos < next_cap) {
@@ -327,7 +335,7 @@ __global__ void __launch_bounds__(256) expand_route(M m, u64* __restrict__ arena
             for (int x = 0; x < W; ++x) ns[x] = stage[i * W + x];
             if (pos < next_cap) {
                 store_state<W>(next, pos, ns);
-                next_par[pos] = stage_par[i];
+                next_par[pos] = gid_base + stage_par[i];
             } else {
                 atomicOr(&lc->err, (u32)ERR_FRONTIER_OVERFLOW);
             }
