@@ -490,11 +490,45 @@ class Engine final : public EngineBase {
     // Device counters to their level-start values (once per run; afterwards the publishing
     // workgroup of each level resets them).
     void init_counters() {
-        LevelCounters z;
-        std::memset(&z, 0, sizeof(z));
-        for (auto& d : z.disc) d = ~0u;
-        SR_HIP(hipMemcpyAsync(lc_d_, &z, sizeof(z), hipMemcpyHostToDevice, stream_));
+        std::vector<LevelCounters> z(1 + SLOTS);
+        std::memset(z.data(), 0, z.size() * sizeof(LevelCounters));
+        for (auto& c : z)
+            for (auto& d : c.disc) d = ~0u;
+        SR_HIP(hipMemcpyAsync(lc_d_, z.data(), sizeof(LevelCounters), hipMemcpyHostToDevice, stream_));
+        if (!slots_.p) slots_.alloc(o_.device, (SLOTS * sizeof(LevelCounters) + 7) / 8);
+        SR_HIP(hipMemcpyAsync(slots_.p, z.data() + 1, SLOTS * sizeof(LevelCounters), hipMemcpyHostToDevice, stream_));
+        slot_k_ = 0;
+        slot_published_ = true;
         SR_HIP(hipStreamSynchronize(stream_));
+    }
+
+    // Per-level counter slots of the pipelined loop (SlotWork, kernels.hpp).
+    LevelCounters* slot(u32 k) const { return reinterpret_cast<LevelCounters*>(slots_.p) + (k % SLOTS); }
+    // The slot duties of the next slotted launch: its frontier size from the previous slot (dev_n),
+    // the previous slot's publish unless it is already done, and the reset of slot K-2.
+    SlotWork slot_work(bool dev_n) {
+        SlotWork sw{};
+        if (dev_n) sw.prev_n = slot_k_ ? &slot(slot_k_ - 1)->claims : &lc_d_->prev_claims;
+        if (slot_k_ && !slot_published_) {
+            sw.pub = slot(slot_k_ - 1);
+            sw.hc = hcd(slot_seq_);
+            sw.seq = slot_seq_;
+            slot_published_ = true;
+        }
+        if (slot_k_ >= 2) sw.zero = slot(slot_k_ - 2);
+        return sw;
+    }
+    // The last slotted level's publish, when no launch that would carry it is enqueued before the
+    // host waits for it.
+    void publish_pending_slot() {
+        if (slot_published_) return;
+        SlotWork sw{};
+        sw.pub = slot(slot_k_ - 1);
+        sw.hc = hcd(slot_seq_);
+        sw.seq = slot_seq_;
+        slot_publish_kernel<M::NPROPS><<<1, 64, 0, stream_>>>(sw);
+        SR_HIP(hipGetLastError());
+        slot_published_ = true;
     }
     u32 next_seq() { return ++ctx_->seq; }
     HostCounters* hcd(u32 seq) const { return ctx_->hc_dev + (seq & 1); }  // device view of seq's mirror
@@ -842,10 +876,12 @@ class Engine final : public EngineBase {
                 bool go = true;
                 for (u32 i = 0; i < k && go; ++i) {
                     HostCounters c{};
-                    c.successors = recs[i].successors;
-                    c.enabled = recs[i].enabled;
-                    c.probes = recs[i].probes;
-                    c.cas = recs[i].cas;
+                    for (const StatShard& sh : recs[i].stat) {  // summed over the shards
+                        c.successors += sh.successors;
+                        c.enabled += sh.enabled;
+                        c.probes += sh.probes;
+                        c.cas += sh.cas;
+                    }
                     c.claims = recs[i].claims;
                     c.err = recs[i].err;
                     for (int p = 0; p < M::NPROPS; ++p) c.disc[p] = recs[i].disc[p];
@@ -869,6 +905,7 @@ class Engine final : public EngineBase {
             // launch shape: a tight estimate (the grid strides over any excess)
             const u64 shape = (u64)((double)n * std::max(ratio_, 0.05) * 1.1) + 64;
             u32 sq_next = spec ? launch_expand(nb_next, 0, true, shape, undiscovered) : 0;
+            if (!spec) publish_pending_slot();  // otherwise the enqueued level publishes this one
 
             wait_publish(sq);  // lc_ = this level's counters
             auto it = seq_launch_.find(sq);
@@ -918,7 +955,7 @@ class Engine final : public EngineBase {
         timed([&] {
             expand_fast<M, 1, 0, false, true><<<multi_grid_, 256, filt_log2_ ? (8u << filt_log2_) : 0u, stream_>>>(
                 m_, arena_.p + fbase * W, 0u, n, view(), arena_.p + nbase * W, apar_.p + nbase, ncap, lc_d_, undiscovered,
-                hcd(sq), sq, 0u, 2u, filt_log2_, 0u, mc);
+                hcd(sq), sq, 0u, 2u, filt_log2_, SlotWork{}, mc);
         }, n);
         return sq;
     }
@@ -960,11 +997,14 @@ class Engine final : public EngineBase {
         const u32 ppw_log2 = ppw_env_ >= 0 ? (u32)ppw_env_ : ppw_for(shape);
         const u32 grid = std::min(expand_grid_cap(), std::max<u32>(1, blocks_for((shape + (1u << ppw_log2) - 1) >> ppw_log2, 4)));
         seq_launch_[sq] = launch_frontier.size();
+        // a slotted launch: it counts into its own slot and is published by its successor
+        const SlotWork sw = slot_work(dev_n);
+        LevelCounters* lc = slot(slot_k_);
         timed([&] {
             auto launch = [&](auto kern) {
                 kern<<<grid, 256, filt_log2_ ? (8u << filt_log2_) : 0u, stream_>>>(
-                    m_, arena_.p + fbase * W, 0u, n, view(), arena_.p + nbase * W, apar_.p + nbase, ncap, lc_d_,
-                    undiscovered, hcd(sq), sq, 1u, ppw_log2, filt_log2_, dev_n ? 1u : 0u, nullptr);
+                    m_, arena_.p + fbase * W, 0u, n, view(), arena_.p + nbase * W, apar_.p + nbase, ncap, lc,
+                    undiscovered, nullptr, sq, 0u, ppw_log2, filt_log2_, sw, nullptr);
             };
             if (o_.counters) launch(expand_fast<M, 1, 0, true>);
             else switch (probe_batch_ * 10 + probe_load_) {
@@ -972,6 +1012,9 @@ class Engine final : public EngineBase {
                 default: launch(expand_fast<M, 1, 0>); break;
             }
         }, n);
+        slot_seq_ = sq;
+        slot_published_ = false;
+        ++slot_k_;
         return sq;
     }
 
@@ -1052,7 +1095,7 @@ class Engine final : public EngineBase {
                     auto launch = [&](auto kern) {
                         kern<<<grid, 256, filt_log2_ ? (8u << filt_log2_) : 0u, stream_>>>(
                             m_, cur(), ulo, uhi, view(), next, npar, ncap, lc_d_, undiscovered, hcd(sq), sq,
-                            last ? 1u : 0u, ppw_log2, filt_log2_, 0u, nullptr);
+                            last ? 1u : 0u, ppw_log2, filt_log2_, SlotWork{}, nullptr);
                     };
                     if (o_.counters) launch(expand_fast<M, 1, 0, true>);
                     else switch (probe_batch_ * 10 + probe_load_) {
@@ -1139,6 +1182,10 @@ class Engine final : public EngineBase {
     u64 multi_arena_min_ = 1u << 20;  // arena room reserved ahead of a multi-level launch (states)
     u32 multi_grid_ = 0;              // its workgroups: one per CU
     DBuf<u64> multi_;                 // its MultiCtl
+    DBuf<u64> slots_;                 // SLOTS per-level counter slots (the pipelined loop)
+    u32 slot_k_ = 0;                  // slotted launches in this run
+    u32 slot_seq_ = 0;                // sequence number of the last one
+    bool slot_published_ = true;      // its publish is done or enqueued
     std::map<u32, size_t> seq_launch_;  // launch sequence number -> index in launch_frontier
     u32 filt_log2_ = W >= 4 ? 10 : 9;  // block-local duplicate filter (SR_FILTER_LOG2 sweep in profiles/)
     bool pessimistic_ = false;  // size chunks for max out-degree new states per parent

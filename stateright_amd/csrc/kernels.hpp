@@ -130,25 +130,73 @@ SR_HD ProbeKey probe_key(const M& m, const TableView& t, const u64* s) {
 
 constexpr u32 NO_PARENT = 0xffffffffu;
 
-// Per-level device counters. The hot counters sit on separate 128-byte lines (one returning
-// atomic per workgroup each). The last workgroup of a launch (ticket) publishes a snapshot to
-// pinned host memory, so the host learns the level's outcome without a copy or a stream sync.
-struct LevelCounters {
+// Per-level device counters. Atomics to one 128-byte line serialise at the coherence point at
+// ~11 ns each whatever the addresses inside it (scripts/microbench_atomics.hip: 12 288 atomics to
+// one line take 143 us; to 8 lines, 21 us), and the workgroups of a level finish together. So
+// every counter that each workgroup updates is spread: the statistics over NSHARD lines (by
+// blockIdx % NSHARD, summed by the publisher) and the ticket over NSHARD group tickets plus one
+// top ticket. claims (one or two reservations per workgroup) keeps its own line. The last
+// workgroup of a launch publishes a snapshot to pinned host memory, so the host learns the
+// level's outcome without a copy or a stream sync.
+constexpr u32 NSHARD = 16;
+struct StatShard {
     u64 successors;        // successors within boundary (state_count increments, bfs.rs:235)
     u64 enabled;           // enabled action slots of the expanded parents (launch-shape statistic)
     u64 probes;            // visited-set slots loaded (first probe + linear-probe steps)
     u64 cas;               // 64-bit atomicCAS claims attempted on the visited set
-    u64 pad0[12];
+    u64 pad[12];
+};
+struct LevelCounters {
+    StatShard stat[NSHARD];
     u32 claims;            // new states inserted into the visited set (= next-frontier cursor)
     u32 pad1[31];
-    u32 ticket;            // workgroups finished in this launch
+    u32 ticket;            // groups of workgroups finished in this launch
     u32 pad2[31];
+    u32 gticket[NSHARD][32];  // workgroups finished per group (blockIdx % NSHARD), one line each
     u32 err;               // ErrBits
     u32 disc[MAX_PROPS];   // min rank of a discovering state in the frontier being produced
     u32 pad3[32];
     u32 prev_claims;       // claims of the last level (set by a resetting publish): the size of the
                            // frontier a pipelined launch expands, read on the device
 };
+
+// A workgroup's statistics (one thread): into its shard.
+__device__ __forceinline__ void add_stats(LevelCounters* lc, u32 succ, u32 en, u32 probes = 0, u32 cas = 0) {
+    StatShard* sh = &lc->stat[blockIdx.x % NSHARD];
+    if (succ) atomicAdd(reinterpret_cast<unsigned long long*>(&sh->successors), (unsigned long long)succ);
+    if (en) atomicAdd(reinterpret_cast<unsigned long long*>(&sh->enabled), (unsigned long long)en);
+    if (probes) atomicAdd(reinterpret_cast<unsigned long long*>(&sh->probes), (unsigned long long)probes);
+    if (cas) atomicAdd(reinterpret_cast<unsigned long long*>(&sh->cas), (unsigned long long)cas);
+}
+
+// The workgroup's ticket (one thread, after its counter atomics have drained): true for the last
+// workgroup of the launch. The last arrival of each group takes the top ticket; the group
+// tickets chain the arrivals, so the last workgroup sees every counter update of the launch.
+__device__ __forceinline__ bool take_ticket(LevelCounters* lc) {
+    // a small grid (a small level) takes the top ticket directly: one round trip, not two
+    if (gridDim.x <= 128) return atomicAdd(&lc->ticket, 1u) == gridDim.x - 1;
+    const u32 g = blockIdx.x % NSHARD;
+    const u32 gsize = (gridDim.x - g + NSHARD - 1) / NSHARD;
+    if (atomicAdd(&lc->gticket[g][0], 1u) != gsize - 1) return false;
+    return atomicAdd(&lc->ticket, 1u) == min(gridDim.x, NSHARD) - 1;
+}
+
+// Sums of the four statistics over the shards, gathered by the 64 lanes of one wave (lane 16c + s
+// loads counter c of shard s); lane 16c returns the total of counter c.
+__device__ __forceinline__ u64 gather_stats(const LevelCounters* lc, u32 lane) {
+    const u64* w = reinterpret_cast<const u64*>(&lc->stat[lane & (NSHARD - 1)]) + (lane >> 4);
+    u64 v = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int d = 8; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+    return v;
+}
+
+// Reset of the statistics and the tickets for the next launch (one wave, lane = 0..63).
+__device__ __forceinline__ void reset_stats_tickets(LevelCounters* lc, u32 lane, bool stats) {
+    if (stats) reinterpret_cast<u64*>(&lc->stat[lane & (NSHARD - 1)])[lane >> 4] = 0;
+    if (lane < NSHARD) lc->gticket[lane][0] = 0;
+    if (lane == 0) lc->ticket = 0;
+}
 
 // Host-visible snapshot (hipHostMalloc'd), written by the publishing workgroup.
 struct HostCounters {
@@ -166,10 +214,7 @@ struct HostCounters {
 
 template <int NP>
 __device__ __forceinline__ void reset_counters(LevelCounters* lc) {
-    lc->successors = 0;
-    lc->enabled = 0;
-    lc->probes = 0;
-    lc->cas = 0;
+    for (u32 i = 0; i < NSHARD; ++i) lc->stat[i] = StatShard{};
     lc->claims = 0;
     lc->err = 0;
 #pragma unroll
@@ -208,46 +253,50 @@ __device__ __forceinline__ void publish(LevelCounters* lc, HostCounters* h, u32 
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
 #endif
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        last = atomicAdd(&lc->ticket, 1u) == gridDim.x - 1;
+        last = take_ticket(lc);
     }
     if (!__shfl(last, 0, 64)) return;
 #if SR_TICKET_FENCE
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 #endif
-    // word map: [0, 8) successors/enabled/probes/cas (same offsets in both structs), 8 claims,
-    // 9 err, 10 aux, 11 + p disc[p], 11 + NP + q sendc[q]
-    u32* lcw = reinterpret_cast<u32*>(lc);
+    // statistics: summed over the shards (lane 16c holds counter c), written as two u32 words
     u32* hw = reinterpret_cast<u32*>(h);
+    const u64 st = gather_stats(lc, lane);
+    if ((lane & 15) == 0) {
+        hw[(lane >> 4) * 2] = (u32)st;
+        hw[(lane >> 4) * 2 + 1] = (u32)(st >> 32);
+    }
+    // word map: 0 claims, 1 err, 2 aux, 3 + p disc[p], 3 + NP + q sendc[q]
+    const u32* lcw = reinterpret_cast<const u32*>(lc);
     constexpr u32 O_CLAIMS = offsetof(LevelCounters, claims) / 4, O_ERR = offsetof(LevelCounters, err) / 4;
     constexpr u32 O_DISC = offsetof(LevelCounters, disc) / 4;
     constexpr u32 H_CLAIMS = offsetof(HostCounters, claims) / 4, H_ERR = offsetof(HostCounters, err) / 4;
     constexpr u32 H_AUX = offsetof(HostCounters, aux) / 4, H_DISC = offsetof(HostCounters, disc) / 4;
     constexpr u32 H_SENDC = offsetof(HostCounters, sendc) / 4;
-    const u32 nwords = 11 + NP + nparts;
+    static_assert(offsetof(HostCounters, successors) == 0 && offsetof(HostCounters, cas) == 24, "host stats layout");
+    const u32 nwords = 3 + NP + nparts;
     u32 claims = 0;
     for (u32 i0 = 0; i0 < nwords; i0 += 64) {
         const u32 i = i0 + lane;
         const u32* src = nullptr;
         u32 dst = 0;
-        if (i < 8) src = lcw + i, dst = i;
-        else if (i == 8) src = lcw + O_CLAIMS, dst = H_CLAIMS;
-        else if (i == 9) src = lcw + O_ERR, dst = H_ERR;
-        else if (i == 10) src = aux, dst = H_AUX;
-        else if (i < 11 + NP) src = lcw + O_DISC + (i - 11), dst = H_DISC + (i - 11);
-        else if (i < nwords) src = sendc + (i - 11 - NP), dst = H_SENDC + (i - 11 - NP);
+        if (i == 0) src = lcw + O_CLAIMS, dst = H_CLAIMS;
+        else if (i == 1) src = lcw + O_ERR, dst = H_ERR;
+        else if (i == 2) src = aux, dst = H_AUX;
+        else if (i < 3 + NP) src = lcw + O_DISC + (i - 3), dst = H_DISC + (i - 3);
+        else if (i < nwords) src = sendc + (i - 3 - NP), dst = H_SENDC + (i - 3 - NP);
         const u32 v = src ? __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
         if (i < nwords) hw[dst] = v;
-        if (i0 == 0) claims = __shfl(v, 8, 64);
+        if (i0 == 0) claims = __shfl(v, 0, 64);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every word read before any is reset
     if (reset) {
-        if (lane < 8) lcw[lane] = 0;  // successors, enabled, probes, cas
-        if (lane == 8) lc->claims = 0;
-        if (lane == 9) lc->err = 0;
-        if (lane >= 11 && lane < 11 + NP) lc->disc[lane - 11] = ~0u;
+        if (lane == 0) lc->claims = 0;
+        if (lane == 1) lc->err = 0;
+        if (lane >= 3 && lane < 3 + NP) lc->disc[lane - 3] = ~0u;
         if (lane == 0) lc->prev_claims = claims;
     }
-    if (lane == 0) lc->ticket = 0;
+    reset_stats_tickets(lc, lane, reset);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the whole wave's host stores issued and acked
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");     // system scope: host memory
     if (lane == 0) __hip_atomic_store(&h->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -256,6 +305,59 @@ __device__ __forceinline__ void publish(LevelCounters* lc, HostCounters* h, u32 
 // Standalone publish (after kernels that do not publish themselves).
 __global__ void publish_kernel(LevelCounters* lc, HostCounters* h, u32 seq, u32 reset, const u32* aux) {
     publish<MAX_PROPS>(lc, h, seq, reset != 0, aux);
+}
+
+// ---- per-level counter slots (the pipelined FAST level loop) ----
+// A level's publish (ticket, gather, host stores, system fence, seq) used to end every expand
+// launch: ~4-6 dependent round trips between the level's last workgroup and the next level. In the
+// pipelined loop each level instead counts into its own slot (a ring of SLOTS); the next level's
+// launch reads its frontier size from the previous slot, and its workgroup 0 publishes that slot to
+// the host in wave 0 while the rest of the grid expands. The wave also resets slot K-2 for reuse:
+// it was published (by launch K-1 or by slot_publish_kernel) before launch K starts. When the
+// host waits for a level without having enqueued its successor, slot_publish_kernel publishes it.
+constexpr u32 SLOTS = 4;
+struct SlotWork {
+    const u32* prev_n;          // frontier size = the previous level's claims (nullptr: `hi` is exact)
+    const LevelCounters* pub;   // slot to publish (nullptr: none)
+    HostCounters* hc;           // its host mirror
+    u32 seq;                    // its launch's sequence number
+    LevelCounters* zero;        // slot to reset (nullptr: none)
+};
+
+// One wave (lane = 0..63): publish sw.pub to sw.hc, then reset sw.zero.
+template <int NP>
+__device__ __forceinline__ void slot_service(const SlotWork& sw, u32 lane) {
+    if (sw.pub) {
+        const LevelCounters* lc = sw.pub;
+        u32* hw = reinterpret_cast<u32*>(sw.hc);
+        const u64 st = gather_stats(lc, lane);
+        if ((lane & 15) == 0) {
+            hw[(lane >> 4) * 2] = (u32)st;
+            hw[(lane >> 4) * 2 + 1] = (u32)(st >> 32);
+        }
+        // lane 0 claims, 1 err, 2 aux (0), 3 + p disc[p]
+        const u32* src = lane == 0 ? &lc->claims : lane == 1 ? &lc->err : lane >= 3 && lane < 3 + NP ? &lc->disc[lane - 3] : nullptr;
+        const u32 v = src ? __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+        if (lane == 0) sw.hc->claims = v;
+        if (lane == 1) sw.hc->err = v;
+        if (lane == 2) sw.hc->aux = 0;
+        if (lane >= 3 && lane < 3 + NP) sw.hc->disc[lane - 3] = v;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the whole wave's host stores issued and acked
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");     // system scope: host memory
+        if (lane == 0) __hip_atomic_store(&sw.hc->seq, sw.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    if (sw.zero) {
+        LevelCounters* z = sw.zero;
+        reinterpret_cast<u64*>(&z->stat[lane & (NSHARD - 1)])[lane >> 4] = 0;
+        if (lane == 0) z->claims = 0;
+        if (lane == 1) z->err = 0;
+        if (lane < MAX_PROPS) z->disc[lane] = ~0u;
+    }
+}
+
+template <int NP>
+__global__ void slot_publish_kernel(SlotWork sw) {
+    slot_service<NP>(sw, threadIdx.x);
 }
 
 // Probe loads of the visited set. POL selects the cache policy of the plain probe load:
@@ -560,7 +662,7 @@ __global__ void __launch_bounds__(256) expand_fast(M m, const u64* __restrict__ 
                                                    TableView t, u64* __restrict__ next, u32* __restrict__ next_par,
                                                    u32 next_cap, LevelCounters* lc, u32 undiscovered,
                                                    HostCounters* hc, u32 seq, u32 reset, u32 ppw_log2,
-                                                   u32 filt_log2, u32 dev_n, MultiCtl* mc) {
+                                                   u32 filt_log2, SlotWork sw, MultiCtl* mc) {
     constexpr int W = M::W, MW = M::MW;
     constexpr int STAGE = SR_STAGE_WORDS / W;
     extern __shared__ u64 filt[];       // 2^filt_log2 fingerprints (dynamic LDS; 0 = no filter)
@@ -575,10 +677,12 @@ __global__ void __launch_bounds__(256) expand_fast(M m, const u64* __restrict__ 
     __shared__ u32 stage_n, base, scratch[4];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     if (threadIdx.x == 0) stage_n = 0;
-    if (dev_n) {
+    if (!MULTI && blockIdx.x == 0 && threadIdx.x < 64 && (sw.pub || sw.zero))
+        slot_service<M::NPROPS>(sw, threadIdx.x);  // the previous level's publish (see SlotWork)
+    if (sw.prev_n) {
         // Pipelined launch (enqueued before the host saw the previous level finish): the frontier
         // is the previous level's claims, and the next level starts right after it.
-        const u32 nn = lc->prev_claims;
+        const u32 nn = __hip_atomic_load(sw.prev_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         hi = lo + nn;
         next += (u64)nn * W;
         next_par += nn;
@@ -765,10 +869,7 @@ __global__ void __launch_bounds__(256) expand_fast(M m, const u64* __restrict__ 
     const u32 n = min(stage_n, (u32)STAGE);
     if (threadIdx.x == 0) {
         base = n ? atomicAdd(&lc->claims, n) : 0;
-        if (total_succ) atomicAdd(reinterpret_cast<unsigned long long*>(&lc->successors), (unsigned long long)total_succ);
-        if (total_enabled) atomicAdd(reinterpret_cast<unsigned long long*>(&lc->enabled), (unsigned long long)total_enabled);
-        if (total_probes) atomicAdd(reinterpret_cast<unsigned long long*>(&lc->probes), (unsigned long long)total_probes);
-        if (total_cas) atomicAdd(reinterpret_cast<unsigned long long*>(&lc->cas), (unsigned long long)total_cas);
+        add_stats(lc, total_succ, total_enabled, total_probes, total_cas);
     }
     __syncthreads();
     for (u32 i = threadIdx.x; i < n; i += blockDim.x) {
@@ -790,7 +891,7 @@ __global__ void __launch_bounds__(256) expand_fast(M m, const u64* __restrict__ 
     };
     if constexpr (!MULTI) {
         level(frontier, lo, hi, next, next_par, next_cap, lc, undiscovered);
-        publish<M::NPROPS>(lc, hc, seq, reset != 0, nullptr);
+        if (hc) publish<M::NPROPS>(lc, hc, seq, reset != 0, nullptr);  // a slotted launch is published by its successor
     } else {
         multi_levels<M::NPROPS>(level, frontier, lo, hi, next, next_par, next_cap, undiscovered, (u32)W, mc, hc, seq);
     }
@@ -829,7 +930,7 @@ __global__ void __launch_bounds__(256) expand_fifo(M m, const u64* __restrict__ 
     u32 ts = block_sum(succ, scratch);
     u32 tc = block_sum(claims, scratch);
     if (threadIdx.x == 0) {
-        if (ts) atomicAdd(reinterpret_cast<unsigned long long*>(&lc->successors), (unsigned long long)ts);
+        add_stats(lc, ts, 0);
         if (tc) atomicAdd(&lc->claims, tc);
     }
     publish<M::NPROPS>(lc, hc, seq, false, nullptr);

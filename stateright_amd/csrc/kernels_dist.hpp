@@ -54,8 +54,7 @@ __device__ __forceinline__ bool last_workgroup(LevelCounters* lc) {
 #if SR_TICKET_FENCE
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
 #endif
-    u32 t = atomicAdd(&lc->ticket, 1u);
-    if (t != gridDim.x - 1) return false;
+    if (!take_ticket(lc)) return false;
 #if SR_TICKET_FENCE
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 #endif
@@ -67,7 +66,7 @@ __device__ __forceinline__ bool last_block(LevelCounters* lc) {
     __shared__ u32 is_last;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (threadIdx.x == 0) is_last = atomicAdd(&lc->ticket, 1u) == gridDim.x - 1;
+    if (threadIdx.x == 0) is_last = take_ticket(lc);
     __syncthreads();
     return is_last != 0;
 }
@@ -352,29 +351,28 @@ __global__ void __launch_bounds__(256) expand_route(M m, u64* __restrict__ arena
     }
     u32 total_succ = block_sum(succ, scratch);
     u32 total_enabled = block_sum(enabled, scratch);
-    if (threadIdx.x == 0) {
-        if (total_succ) atomicAdd(reinterpret_cast<unsigned long long*>(&lc->successors), (unsigned long long)total_succ);
-        if (total_enabled) atomicAdd(reinterpret_cast<unsigned long long*>(&lc->enabled), (unsigned long long)total_enabled);
-    }
+    if (threadIdx.x == 0) add_stats(lc, total_succ, total_enabled);
     if (!last_block(lc)) return;
     // The row, one word per thread (every source word is a round trip to the coherence point: one
     // thread loading them in turn was the floor of a small level), staged in LDS for the headers.
     __shared__ u64 srow[MAX_PARTS + 6 + MAX_PROPS];
+    __shared__ u64 sstat[4];  // the statistics summed over their shards
+    if (threadIdx.x < 64) {
+        const u64 v = gather_stats(lc, threadIdx.x);
+        if ((threadIdx.x & 15) == 0) sstat[threadIdx.x >> 4] = v;
+    }
+    __syncthreads();
     const u32 rw = nparts + 6 + M::NPROPS;
     for (u32 w = threadIdx.x; w < rw; w += blockDim.x) {
         const u32 f = w - nparts;  // row fields after the per-destination counts
         const u32* src = w < nparts ? send_counts + w
-                         : f == 1   ? reinterpret_cast<const u32*>(&lc->successors)
                          : f == 2   ? &lc->claims
                          : f == 3   ? &lc->err
-                         : f == 4   ? reinterpret_cast<const u32*>(&lc->enabled)
                          : f == 5   ? &ctl->roots
                          : f >= 6   ? &ctl->disc_prev[f - 6]
-                                    : &lc->claims;  // f == 0: the frontier size n (no load needed)
-        const bool wide = w >= nparts && (f == 1 || f == 4);
-        const u64 lo = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const u64 hi = __hip_atomic_load(src + (wide ? 1 : 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const u64 v = w >= nparts && f == 0 ? n : (wide ? lo | hi << 32 : lo);
+                                    : &lc->claims;  // f == 0 (the frontier size n), 1, 4: no load needed
+        const u64 ld = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const u64 v = w < nparts ? ld : f == 0 ? n : f == 1 ? sstat[0] : f == 4 ? sstat[1] : ld;
         srow[w] = v;
         row[w] = v;
     }
@@ -385,11 +383,7 @@ __global__ void __launch_bounds__(256) expand_route(M m, u64* __restrict__ arena
             const u32 q = i / rw, w = i - q * rw;
             send[(u64)q * bucket_stride - DIST_HDR + w] = srow[w];
         }
-    if (threadIdx.x == 0) {
-        lc->successors = 0;
-        lc->enabled = 0;
-        lc->ticket = 0;
-    }
+    if (threadIdx.x < 64) reset_stats_tickets(lc, threadIdx.x, true);
 }
 
 // Insert the records this partition received (state + parent gid); new states continue the next
@@ -459,6 +453,7 @@ __global__ void __launch_bounds__(256) insert_recv(M m, const u64* __restrict__ 
     }
     ctl->roots = 0;
     lc->claims = 0;
+    for (u32 g = 0; g < NSHARD; ++g) lc->gticket[g][0] = 0;
     lc->ticket = 0;
 }
 
@@ -561,8 +556,8 @@ __global__ void __launch_bounds__(256) insert_recv_lag(M m, const u64* __restric
         ctl->n = min(claims, next_cap);
         ctl->roots = 0;
         lc->claims = 0;
-        lc->ticket = 0;
     }
+    reset_stats_tickets(lc, lane, false);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: host memory
     if (lane == 0) __hip_atomic_store(&pub->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
