@@ -1000,9 +1000,10 @@ class Engine final : public EngineBase {
         // a slotted launch: it counts into its own slot and is published by its successor
         const SlotWork sw = slot_work(dev_n);
         LevelCounters* lc = slot(slot_k_);
+        const u32 svc = sw.pub || sw.zero ? 1u : 0u;  // the extra service workgroup (SlotWork)
         timed([&] {
             auto launch = [&](auto kern) {
-                kern<<<grid, 256, filt_log2_ ? (8u << filt_log2_) : 0u, stream_>>>(
+                kern<<<grid + svc, 256, filt_log2_ ? (8u << filt_log2_) : 0u, stream_>>>(
                     m_, arena_.p + fbase * W, 0u, n, view(), arena_.p + nbase * W, apar_.p + nbase, ncap, lc,
                     undiscovered, nullptr, sq, 0u, ppw_log2, filt_log2_, sw, nullptr);
             };

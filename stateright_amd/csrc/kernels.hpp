@@ -495,6 +495,14 @@ __device__ __forceinline__ void eval_props(const M& m, const u64* s, u32 rank, u
     }
 }
 
+// Orders one wave's LDS accesses across its lanes: the LDS runs a wave's operations in issue
+// order, the wait retires the pending ones, and the clobber keeps the compiler from moving memory
+// accesses across this point (lanes write what other lanes of the same wave read next).
+__device__ __forceinline__ void wave_lds_sync() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+}
+
 // Sum of v over the workgroup, returned to every thread (one LDS round).
 __device__ __forceinline__ u32 block_sum(u32 v, u32* scratch) {
 #pragma unroll
@@ -509,16 +517,18 @@ __device__ __forceinline__ u32 block_sum(u32 v, u32* scratch) {
 
 // k-th set bit (0-based) of a 64-bit mask with popcount(m) > k.
 __device__ __forceinline__ u32 select_bit(u64 m, u32 k) {
-    u32 pos = 0;
+    // the half first, then five steps on 32 bits (u64 shifts and masks cost two VALU each)
+    const u32 lo = (u32)m, clo = (u32)__popc(lo);
+    const bool up = k >= clo;
+    u32 x = up ? (u32)(m >> 32) : lo, pos = up ? 32u : 0u;
+    k -= up ? clo : 0u;
 #pragma unroll
-    for (int w = 32; w >= 1; w >>= 1) {
-        u64 low = m & ((1ull << w) - 1);
-        u32 c = __popcll(low);
-        if (k >= c) {
-            k -= c;
-            m >>= w;
-            pos += w;
-        }
+    for (int w = 16; w >= 1; w >>= 1) {
+        const u32 c = (u32)__popc(x & ((1u << w) - 1));
+        const bool u = k >= c;
+        k -= u ? c : 0u;
+        x = u ? x >> w : x;
+        pos += u ? (u32)w : 0u;
     }
     return pos;
 }
@@ -672,13 +682,26 @@ __global__ void __launch_bounds__(256) expand_fast(M m, const u64* __restrict__ 
     // staging 64 of them cost 22.5 KB of LDS per block, which capped residency at 3 blocks per CU.
     constexpr u32 PPW_LOG2_MAX = W >= 4 ? 4 : 6;
     __shared__ u64 pst[4][(1 << PPW_LOG2_MAX) * W];     // parent states of each wave
-    __shared__ u64 pmask[4][(1 << PPW_LOG2_MAX) * MW];  // their enabled-action masks
-    __shared__ u32 pexcl[4][64];                        // exclusive prefix of their successor counts
+    // The wave's successor list, one u16 per successor: parent (bits 0-5) | action << 6, written by
+    // the parent lanes (a ctz loop over their enabled masks) in windows of MAPCAP successors. A
+    // successor lane reads its (parent, action) with one LDS load; the binary search over the
+    // parents' prefix sums (6 dependent LDS loads) and the k-th-set-bit select it replaces were
+    // the largest per-successor costs.
+    constexpr u32 MAPCAP = 1024;
+    static_assert(MW * 64 <= 1024, "action ids must fit 10 bits");
+    __shared__ u16 smap[4][MAPCAP];
     __shared__ u32 stage_n, base, scratch[4];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     if (threadIdx.x == 0) stage_n = 0;
-    if (!MULTI && blockIdx.x == 0 && threadIdx.x < 64 && (sw.pub || sw.zero))
-        slot_service<M::NPROPS>(sw, threadIdx.x);  // the previous level's publish (see SlotWork)
+    // The previous level's publish and the slot reset (SlotWork) run in one extra workgroup, the
+    // last of the grid: in a small level any workgroup that expands parents is on the critical
+    // path, and the publish waits for its host stores to be acknowledged.
+    const bool svc = !MULTI && (sw.pub || sw.zero);
+    if (svc && blockIdx.x == gridDim.x - 1) {
+        if (threadIdx.x < 64) slot_service<M::NPROPS>(sw, threadIdx.x);
+        return;
+    }
+    const u32 nblk = gridDim.x - (svc ? 1u : 0u);  // workgroups that expand parents
     if (sw.prev_n) {
         // Pipelined launch (enqueued before the host saw the previous level finish): the frontier
         // is the previous level's claims, and the next level starts right after it.
@@ -701,22 +724,34 @@ __global__ void __launch_bounds__(256) expand_fast(M m, const u64* __restrict__ 
     auto level = [&](const u64* __restrict__ frontier, u32 lo, u32 hi, u64* __restrict__ next,
                      u32* __restrict__ next_par, u32 next_cap, LevelCounters* lc, u32 undiscovered) {
     u32 succ = 0, enabled = 0, probes = 0, cas = 0;
-    for (u64 c0 = lo + (u64)blockIdx.x * chunk; c0 < hi; c0 += (u64)gridDim.x * chunk) {
+    // The wave's parents of the next chunk are loaded one chunk ahead: their latency overlaps this
+    // chunk's probes instead of stalling the chunk start.
+    const u64 cstride = (u64)nblk * chunk;
+    u64 nxt[W];
+    {
+        const u64 r0 = lo + (u64)blockIdx.x * chunk + ((u64)wid << ppw_log2) + lane;
+        if (lane < (int)ppw && r0 < hi) load_state<W>(frontier, r0, nxt);
+    }
+    for (u64 c0 = lo + (u64)blockIdx.x * chunk; c0 < hi; c0 += cstride) {
         const u32 wave0 = (u32)(c0 + ((u64)wid << ppw_log2));  // first parent of the wave
         const u32 r = wave0 + lane;
         u32 cnt = 0;
-        __syncthreads();  // the previous chunk's parents are no longer read
+        u64 s[W];
+#pragma unroll
+        for (int i = 0; i < W; ++i) s[i] = nxt[i];
+        if (lane < (int)ppw && r + cstride < hi) load_state<W>(frontier, r + cstride, nxt);
+        // the stage's fill is read by every thread at the end of the previous chunk before any
+        // wave appends again (and the wave's parents are no longer read)
+        __syncthreads();
+        u64 mk[MW];
+#pragma unroll
+        for (int i = 0; i < MW; ++i) mk[i] = 0;
         if (lane < ppw && r < hi) {
-            u64 s[W], mk[MW];
-            load_state<W>(frontier, r, s);
             m.enabled(s, mk);
 #pragma unroll
             for (int i = 0; i < W; ++i) pst[wid][lane * W + i] = s[i];
 #pragma unroll
-            for (int i = 0; i < MW; ++i) {
-                pmask[wid][lane * MW + i] = mk[i];
-                cnt += __popcll(mk[i]);
-            }
+            for (int i = 0; i < MW; ++i) cnt += __popcll(mk[i]);
         }
         // wave-inclusive scan of the counts
         u32 incl = cnt;
@@ -725,12 +760,25 @@ __global__ void __launch_bounds__(256) expand_fast(M m, const u64* __restrict__ 
             u32 y = __shfl_up(incl, d, 64);
             if (lane >= d) incl += y;
         }
-        pexcl[wid][lane] = incl - cnt;
+        u32 nidx = incl - cnt;  // this parent's next successor index (its entries are [excl, incl))
         const u32 total = __shfl(incl, 63, 64);
         if (lane == 0) enabled += total;
-        __syncthreads();
 
-        for (u32 it = 0; it < total; it += 64 * PB) {
+        for (u32 w0 = 0; w0 < total; w0 += MAPCAP) {
+        const u32 wend = min(total, w0 + MAPCAP);
+        // this window's entries: each parent lane writes its successors with index in [w0, wend)
+        while (nidx < wend && nidx < incl) {
+            u32 a = 0;
+#pragma unroll
+            for (int w = MW - 1; w >= 0; --w)  // the lowest set bit over the mask words
+                if (mk[w]) a = (u32)w * 64 + (u32)__builtin_ctzll(mk[w]);
+            mk[a >> 6] &= mk[a >> 6] - 1;
+            smap[wid][nidx - w0] = (u16)((u32)lane | a << 6);
+            ++nidx;
+        }
+        wave_lds_sync();  // pst and the map are the wave's own: no workgroup barrier
+
+        for (u32 it = w0; it < wend; it += 64 * PB) {
             u64 ns[PB][W], cur[PB];
             ProbeKey pk[PB];
             u32 par[PB];
@@ -738,27 +786,11 @@ __global__ void __launch_bounds__(256) expand_fast(M m, const u64* __restrict__ 
 #pragma unroll
             for (int j = 0; j < PB; ++j) {
                 const u32 i = it + j * 64 + lane;
-                ok[j] = i < total;
+                ok[j] = i < wend;
                 par[j] = 0;
                 if (ok[j]) {
-                    // parent p: last lane with pexcl[p] <= i (zero-count lanes share their successor's
-                    // prefix; the last of them has a non-zero count because i < its inclusive prefix)
-                    u32 p = 0;
-#pragma unroll
-                    for (int step = 32; step >= 1; step >>= 1)
-                        if (pexcl[wid][p + step] <= i) p += step;
-                    u32 k = i - pexcl[wid][p];
-                    u32 a = 0;
-#pragma unroll
-                    for (int w = 0; w < MW; ++w) {
-                        u64 mw = pmask[wid][p * MW + w];
-                        u32 c = __popcll(mw);
-                        if (k < c) {
-                            a = w * 64 + select_bit(mw, k);
-                            break;
-                        }
-                        k -= c;
-                    }
+                    const u32 e = smap[wid][i - w0];
+                    const u32 p = e & 63, a = e >> 6;
                     u64 ps[W];
 #pragma unroll
                     for (int x = 0; x < W; ++x) ps[x] = pst[wid][p * W + x];
@@ -835,6 +867,8 @@ __global__ void __launch_bounds__(256) expand_fast(M m, const u64* __restrict__ 
                     eval_props(m, ns[j], pos, undiscovered, lc);
                 }
             }
+        }
+        wave_lds_sync();  // the window's map is read before the next window overwrites it
         }
         // A block that strides over several chunks (a grid capped below the frontier) flushes its
         // stage once it is half full: otherwise it stays full after the first chunks and every

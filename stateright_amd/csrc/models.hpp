@@ -227,26 +227,26 @@ struct TwoPhase {
         m[0] = lo;
         m[1] = hi;
     }
+    // Branch-free: the lanes of a wave apply different actions, and a switch over them ran every
+    // taken arm for the whole wave. Every action writes at most one 2-bit field (rm_state[rm] or
+    // tm_state) and sets at most one bit:
+    //   a = 0 TmCommit         tm_state <- 1, bit 4n+2 (Commit)
+    //   a = 1 TmAbort          tm_state <- 2, bit 4n+3 (Abort)
+    //   k = 0 TmRcvPrepared    bit 2n+2+rm (tm_prepared)
+    //   k = 1 RmPrepare        rm_state <- 1, bit 3n+2+rm (Prepared{rm})
+    //   k = 2 RmChooseToAbort  rm_state <- 3
+    //   k = 3 RmRcvCommitMsg   rm_state <- 2
+    //   k = 4 RmRcvAbortMsg    rm_state <- 3
     SR_HD bool apply(const u64* sp, int a, u64* o) const {
-        u64 s = sp[0];
-        if (a == 0) {  // TmCommit
-            s = (s & ~(3ull << (2 * n))) | (1ull << (2 * n));
-            s |= 1ull << (4 * n + 2);
-        } else if (a == 1) {  // TmAbort
-            s = (s & ~(3ull << (2 * n))) | (2ull << (2 * n));
-            s |= 1ull << (4 * n + 3);
-        } else {
-            int rm = (a - 2) / 5, k = (a - 2) % 5;
-            u64 clr = ~(3ull << (2 * rm));
-            switch (k) {
-                case 0: s |= 1ull << (2 * n + 2 + rm); break;                               // TmRcvPrepared
-                case 1: s = (s & clr) | (1ull << (2 * rm)); s |= 1ull << (3 * n + 2 + rm); break;  // RmPrepare
-                case 2: s = (s & clr) | (3ull << (2 * rm)); break;                          // RmChooseToAbort
-                case 3: s = (s & clr) | (2ull << (2 * rm)); break;                          // RmRcvCommitMsg
-                default: s = (s & clr) | (3ull << (2 * rm)); break;                         // RmRcvAbortMsg
-            }
-        }
-        o[0] = s;
+        const u64 s = sp[0];
+        const bool tm = a < 2;
+        const u32 b = tm ? 0u : (u32)(a - 2), rm = b / 5, k = b - 5 * rm;
+        const u32 fpos = tm ? 2u * n : 2u * rm;
+        const u64 fval = tm ? (u64)(a + 1) : k == 1 ? 1ull : k == 3 ? 2ull : 3ull;
+        const u64 fmask = (tm || k != 0) ? 3ull << fpos : 0ull;
+        const u32 epos = tm ? 4u * n + 2 + (u32)a : (k == 0 ? 2u * n + 2 : 3u * n + 2) + rm;
+        const u64 ebit = (tm || k <= 1) ? 1ull << epos : 0ull;
+        o[0] = ((s & ~fmask) | ((fval << fpos) & fmask)) | ebit;
         return true;
     }
     SR_HD bool discovers(int p, const u64* sp) const {
