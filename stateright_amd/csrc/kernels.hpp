@@ -748,6 +748,16 @@ __global__ void __launch_bounds__(256) expand_fast(M m, const u64* __restrict__ 
         for (int i = 0; i < MW; ++i) mk[i] = 0;
         if (lane < ppw && r < hi) {
             m.enabled(s, mk);
+            if constexpr (has_self_loops<M>::value) {
+                // self-loops are counted here and never generated (has_self_loops)
+                u64 sl[MW];
+                m.self_loops(s, mk, sl);
+#pragma unroll
+                for (int i = 0; i < MW; ++i) {
+                    succ += __popcll(sl[i]);
+                    mk[i] &= ~sl[i];
+                }
+            }
 #pragma unroll
             for (int i = 0; i < W; ++i) pst[wid][lane * W + i] = s[i];
 #pragma unroll
