@@ -114,8 +114,10 @@ __global__ void __launch_bounds__(256) expand_route(M m, u64* __restrict__ arena
     u8* rown = reinterpret_cast<u8*>(rrank + rs);
     __shared__ u32 ocnt[MAX_PARTS], obase[MAX_PARTS];
     __shared__ u64 pst[4][64 * W];
-    __shared__ u64 pmask[4][64 * MW];
-    __shared__ u32 pexcl[4][64];
+    // the wave's successor list, (parent, action) per successor (see expand_fast), in windows
+    constexpr u32 MAPCAP = 512;
+    static_assert(MW * 64 <= 1024, "action ids must fit 10 bits");
+    __shared__ u16 smap[4][MAPCAP];
     __shared__ u32 stage_n, rstage_n, base, scratch[4];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const u64 lanes_below = (1ull << lane) - 1;
@@ -134,22 +136,36 @@ __global__ void __launch_bounds__(256) expand_route(M m, u64* __restrict__ arena
 
     u32 succ = 0, enabled = 0;
     const u64 chunk = (u64)(blockDim.x >> 6) * ppw;
-    for (u64 c0 = (u64)blockIdx.x * chunk; c0 < n; c0 += (u64)gridDim.x * chunk) {
+    const u64 cstride = (u64)gridDim.x * chunk;
+    u64 nxt[W];  // the wave's parents of the next chunk, loaded one chunk ahead
+    if (lane < (int)ppw && (u64)blockIdx.x * chunk + (u64)wid * ppw + lane < n)
+        load_state<W>(frontier, (u64)blockIdx.x * chunk + (u64)wid * ppw + lane, nxt);
+    for (u64 c0 = (u64)blockIdx.x * chunk; c0 < n; c0 += cstride) {
         const u64 wave0 = c0 + (u64)wid * ppw;  // first parent of the wave
         const u64 r = wave0 + lane;
         u32 cnt = 0;
+        u64 s[W], mk[MW];
+#pragma unroll
+        for (int i = 0; i < W; ++i) s[i] = nxt[i];
+#pragma unroll
+        for (int i = 0; i < MW; ++i) mk[i] = 0;
+        if (lane < (int)ppw && r + cstride < n) load_state<W>(frontier, r + cstride, nxt);
         __syncthreads();  // the previous chunk's parents and stages are no longer read
         if (lane < (int)ppw && r < n) {
-            u64 s[W], mk[MW];
-            load_state<W>(frontier, r, s);
             m.enabled(s, mk);
+            if constexpr (has_self_loops<M>::value) {  // counted, never generated
+                u64 sl[MW];
+                m.self_loops(s, mk, sl);
+#pragma unroll
+                for (int i = 0; i < MW; ++i) {
+                    succ += __popcll(sl[i]);
+                    mk[i] &= ~sl[i];
+                }
+            }
 #pragma unroll
             for (int i = 0; i < W; ++i) pst[wid][lane * W + i] = s[i];
 #pragma unroll
-            for (int i = 0; i < MW; ++i) {
-                pmask[wid][lane * MW + i] = mk[i];
-                cnt += __popcll(mk[i]);
-            }
+            for (int i = 0; i < MW; ++i) cnt += __popcll(mk[i]);
         }
         u32 incl = cnt;
 #pragma unroll
@@ -157,12 +173,24 @@ __global__ void __launch_bounds__(256) expand_route(M m, u64* __restrict__ arena
             u32 y = __shfl_up(incl, d, 64);
             if (lane >= d) incl += y;
         }
-        pexcl[wid][lane] = incl - cnt;
+        u32 nidx = incl - cnt;
         const u32 total = __shfl(incl, 63, 64);
         if (lane == 0) enabled += total;
-        __syncthreads();
 
-        for (u32 it = 0; it < total; it += 64 * PB) {
+        for (u32 w0 = 0; w0 < total; w0 += MAPCAP) {
+        const u32 wend = min(total, w0 + MAPCAP);
+        while (nidx < wend && nidx < incl) {
+            u32 a = 0;
+#pragma unroll
+            for (int w = MW - 1; w >= 0; --w)
+                if (mk[w]) a = (u32)w * 64 + (u32)__builtin_ctzll(mk[w]);
+            mk[a >> 6] &= mk[a >> 6] - 1;
+            smap[wid][nidx - w0] = (u16)((u32)lane | a << 6);
+            ++nidx;
+        }
+        wave_lds_sync();  // pst and the map are the wave's own
+
+        for (u32 it = w0; it < wend; it += 64 * PB) {
             u64 ns[PB][W], key[PB], cur[PB];
             ProbeKey pk[PB];
             u32 par[PB], own[PB];
@@ -170,25 +198,11 @@ __global__ void __launch_bounds__(256) expand_route(M m, u64* __restrict__ arena
 #pragma unroll
             for (int j = 0; j < PB; ++j) {
                 const u32 i = it + j * 64 + lane;
-                ok[j] = i < total;
+                ok[j] = i < wend;
                 par[j] = 0;
                 if (ok[j]) {
-                    u32 p = 0;
-#pragma unroll
-                    for (int step = 32; step >= 1; step >>= 1)
-                        if (pexcl[wid][p + step] <= i) p += step;
-                    u32 k = i - pexcl[wid][p];
-                    u32 a = 0;
-#pragma unroll
-                    for (int w = 0; w < MW; ++w) {
-                        u64 mw = pmask[wid][p * MW + w];
-                        u32 c = __popcll(mw);
-                        if (k < c) {
-                            a = w * 64 + select_bit(mw, k);
-                            break;
-                        }
-                        k -= c;
-                    }
+                    const u32 e = smap[wid][i - w0];
+                    const u32 p = e & 63, a = e >> 6;
                     u64 ps[W];
 #pragma unroll
                     for (int x = 0; x < W; ++x) ps[x] = pst[wid][p * W + x];
@@ -312,6 +326,9 @@ __global__ void __launch_bounds__(256) expand_route(M m, u64* __restrict__ arena
                     }
                 }
             }
+        }
+
+        wave_lds_sync();  // the window's map is read before the next window overwrites it
         }
 
         // ---- block flush of the chunk's stages ----
