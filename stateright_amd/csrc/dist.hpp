@@ -840,7 +840,8 @@ class DistEngine final : public EngineBase {
                 const u64 nb = p.lstart.back();  // start of the next frontier
                 ensure_arena(p, nb + local_new + nrec + 1, nb + local_new);
                 const u32 ncap = (u32)std::min<u64>(p.arena_cap - nb, 0xffffffffu);
-                insert_recv<M><<<std::max<u32>(1, blocks_for(nrec, 256)), 256, 0, stream_>>>(
+                // a capped grid: every workgroup reserves its span of the frontier at least once
+                insert_recv<M><<<(u32)std::min<u64>(std::max<u32>(1, blocks_for(nrec, 256)), INSERT_GRID_MAX), 256, 0, stream_>>>(
                     m_, p.recv.p, (u32)nrec, p.view(), p.arena.p + nb * W, p.apar.p + nb, ncap, p.lc, undiscovered, p.ctl);
                 SR_HIP(hipGetLastError());
                 p.local_prev = local_new;
@@ -1044,7 +1045,7 @@ class DistEngine final : public EngineBase {
                     SR_HIP(hipMemcpyAsync(dst.recv.p + (u64)src.id * S, src.send.p + (u64)dst.id * S, S * 8,
                                           hipMemcpyDeviceToDevice, stream_));
         }
-        const u32 ig = (u32)std::min<u64>(std::max<u64>(1, blocks_for((u64)T_ * C, 256)), 2048);
+        const u32 ig = (u32)std::min<u64>(std::max<u64>(1, blocks_for((u64)T_ * C, 256)), INSERT_GRID_MAX);
         for (auto& p : parts_) {
             p.seq++;
             auto& r = ctx_->parts[p.res];
@@ -1442,6 +1443,9 @@ class DistEngine final : public EngineBase {
         return (filt_log2_ ? (8u << filt_log2_) : 0u) + (size_t)rstage_recs() * (REC * 8 + 2 + 1) +
                (size_t)route_local_stage(T_, W) * (W * 8 + 4);
     }
+    // insert kernels: workgroups at most (each reserves frontier space with a same-line atomic,
+    // ~11 ns apiece; 512 x 256 threads keep enough probes in flight)
+    static constexpr u32 INSERT_GRID_MAX = 512;
     u32 rstage_words_ = std::getenv("SR_RSTAGE_WORDS") ? (u32)std::atoi(std::getenv("SR_RSTAGE_WORDS")) : 1024;
     int route_ppw_env_ = std::getenv("SR_ROUTE_PPW_LOG2") ? std::atoi(std::getenv("SR_ROUTE_PPW_LOG2")) : -1;
     bool trace_ = std::getenv("SR_DIST_TRACE") != nullptr;

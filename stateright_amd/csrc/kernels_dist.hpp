@@ -403,6 +403,84 @@ __global__ void __launch_bounds__(256) expand_route(M m, u64* __restrict__ arena
     if (threadIdx.x < 64) reset_stats_tickets(lc, threadIdx.x, true);
 }
 
+// Inserts received records [0, total) (record g at rec_at(g)), grid-strided over the workgroups:
+// probe / CAS claim, then the new states are appended per wave into an LDS stage (its parent is
+// PAR_SEARCH: a received state's generator is found by find_pred) that is flushed with ONE claims
+// reservation when half full and at the end. The old form reserved once per workgroup and round:
+// with up to 2048 workgroups that was ~2 K same-line atomics per level (~22 us at ~11 ns each,
+// scripts/microbench_atomics.hip), the whole duration of a typical insert launch.
+template <class M, class RecAt>
+__device__ __forceinline__ void insert_records(const M& m, RecAt rec_at, u32 total, const TableView& t, u64* next,
+                                               u64* next_par, u32 next_cap, LevelCounters* lc, u32 undiscovered,
+                                               u64* stage, u32 STAGE, u32& stage_n, u32& base) {
+    constexpr int W = M::W;
+    const int lane = threadIdx.x & 63;
+    auto flush = [&](u32 nl) {
+        if (threadIdx.x == 0) base = atomicAdd(&lc->claims, nl);
+        __syncthreads();
+        for (u32 k = threadIdx.x; k < nl; k += blockDim.x) {
+            const u32 pos = base + k;
+            u64 ns[W];
+#pragma unroll
+            for (int x = 0; x < W; ++x) ns[x] = stage[k * W + x];
+            if (pos < next_cap) {
+                store_state<W>(next, pos, ns);
+                next_par[pos] = PAR_SEARCH;
+            } else {
+                atomicOr(&lc->err, (u32)ERR_FRONTIER_OVERFLOW);
+            }
+            eval_props(m, ns, pos, undiscovered, lc);
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) stage_n = 0;
+    };
+    for (u64 g0 = (u64)blockIdx.x * blockDim.x; g0 < total; g0 += (u64)gridDim.x * blockDim.x) {
+        __syncthreads();  // every thread read the last fill (and the stage was reset) before appends
+        const u64 g = g0 + threadIdx.x;
+        bool nw = false;
+        u64 ns[W];
+        if (g < total) {
+            const u64* rec = rec_at((u32)g);
+#pragma unroll
+            for (int x = 0; x < W; ++x) ns[x] = rec[x];
+            find_or_claim(t, probe_key(m, t, ns), &nw, &lc->err);
+        }
+        const u64 mask = __ballot(nw);
+        if (mask) {  // wave-aggregated: one LDS atomic, the overflow with one claims atomic per wave
+            const u32 cnt = __popcll(mask), below = __popcll(mask & ((1ull << lane) - 1));
+            const int leader = __builtin_ctzll(mask);
+            u32 sb = 0;
+            if (lane == leader) sb = atomicAdd(&stage_n, cnt);
+            sb = __shfl(sb, leader, 64);
+            const u32 in_stage = sb >= STAGE ? 0u : min(cnt, STAGE - sb);
+            u32 gb = 0;
+            if (cnt > in_stage && lane == leader) gb = atomicAdd(&lc->claims, cnt - in_stage);
+            gb = __shfl(gb, leader, 64);
+            if (nw) {
+                if (below < in_stage) {
+#pragma unroll
+                    for (int x = 0; x < W; ++x) stage[(sb + below) * W + x] = ns[x];
+                } else {
+                    const u32 pos = gb + (below - in_stage);
+                    if (pos < next_cap) {
+                        store_state<W>(next, pos, ns);
+                        next_par[pos] = PAR_SEARCH;
+                    } else {
+                        atomicOr(&lc->err, (u32)ERR_FRONTIER_OVERFLOW);
+                    }
+                    eval_props(m, ns, pos, undiscovered, lc);
+                }
+            }
+        }
+        __syncthreads();
+        const u32 sn = min(stage_n, STAGE);  // the same value in every thread (no append until the next barrier)
+        if (sn >= STAGE / 2) flush(sn);
+    }
+    __syncthreads();
+    const u32 sn = min(stage_n, STAGE);
+    if (sn) flush(sn);
+}
+
 // Insert the records this partition received (state + parent gid); new states continue the next
 // frontier after the ones expand_route produced locally. The last workgroup closes the level:
 // ctl = {next frontier size, discoveries among it}, counters reset for the next level.
@@ -411,55 +489,12 @@ __global__ void __launch_bounds__(256) insert_recv(M m, const u64* __restrict__ 
                                                    u64* __restrict__ next, u64* __restrict__ next_par, u32 next_cap,
                                                    LevelCounters* lc, u32 undiscovered, DistCtl* ctl) {
     constexpr int W = M::W, REC = W;
-    constexpr int STAGE = 1024 / W;
+    constexpr u32 STAGE = 1024 / W;
     __shared__ u64 stage[STAGE * W];
-    __shared__ u64 stage_par[STAGE];
     __shared__ u32 stage_n, base;
     if (threadIdx.x == 0) stage_n = 0;
-    __syncthreads();
-    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < nrec) {
-        u64 ns[W];
-#pragma unroll
-        for (int x = 0; x < W; ++x) ns[x] = recv[(u64)i * REC + x];
-        const u64 pgid = PAR_SEARCH;
-        bool is_new;
-        find_or_claim(t, probe_key(m, t, ns), &is_new, &lc->err);
-        if (is_new) {
-            u32 kk = atomicAdd(&stage_n, 1u);
-            if (kk < (u32)STAGE) {
-#pragma unroll
-                for (int x = 0; x < W; ++x) stage[kk * W + x] = ns[x];
-                stage_par[kk] = pgid;
-            } else {
-                u32 pos = atomicAdd(&lc->claims, 1u);
-                if (pos < next_cap) {
-                    store_state<W>(next, pos, ns);
-                    next_par[pos] = pgid;
-                } else {
-                    atomicOr(&lc->err, (u32)ERR_FRONTIER_OVERFLOW);
-                }
-                eval_props(m, ns, pos, undiscovered, lc);
-            }
-        }
-    }
-    __syncthreads();
-    const u32 nl = min(stage_n, (u32)STAGE);
-    if (threadIdx.x == 0) base = nl ? atomicAdd(&lc->claims, nl) : 0;
-    __syncthreads();
-    for (u32 k = threadIdx.x; k < nl; k += blockDim.x) {
-        u32 pos = base + k;
-        u64 ns[W];
-#pragma unroll
-        for (int x = 0; x < W; ++x) ns[x] = stage[k * W + x];
-        if (pos < next_cap) {
-            store_state<W>(next, pos, ns);
-            next_par[pos] = stage_par[k];
-        } else {
-            atomicOr(&lc->err, (u32)ERR_FRONTIER_OVERFLOW);
-        }
-        eval_props(m, ns, pos, undiscovered, lc);
-    }
+    insert_records(m, [&](u32 g) { return recv + (u64)g * REC; }, nrec, t, next, next_par, next_cap, lc, undiscovered,
+                   stage, STAGE, stage_n, base);
     if (!last_workgroup<M::NPROPS>(lc)) return;
     const u32 claims = __hip_atomic_load(&lc->claims, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     ctl->n = min(claims, next_cap);
@@ -494,58 +529,39 @@ __global__ void __launch_bounds__(256) insert_recv_lag(M m, const u64* __restric
                                                        u64* __restrict__ apar, u64 arena_cap, LevelCounters* lc,
                                                        u32 undiscovered, DistCtl* ctl, LagPub* pub, u32 seq) {
     constexpr int W = M::W, REC = W;
-    constexpr int STAGE = 256;
+    constexpr u32 STAGE = 1024 / W;
     __shared__ u64 stage[STAGE * W];
-    __shared__ u64 stage_par[STAGE];
-    __shared__ u32 cnt_q[MAX_PARTS];
+    __shared__ u32 qoff[MAX_PARTS + 1];  // exclusive prefix of the received counts per source
     __shared__ u32 stage_n, base;
     const u64 nb = ctl->nb, n = ctl->n;
     u64* next = arena + (nb + n) * W;
     u64* next_par = apar + nb + n;
     const u32 next_cap = (u32)min<u64>(arena_cap > nb + n ? arena_cap - nb - n : 0, 0xffffffffull);
-    for (u32 q = threadIdx.x; q < nparts; q += blockDim.x) cnt_q[q] = (u32)min<u64>(recv[(u64)q * S + me], C);
-    const u64 slots = (u64)nparts * C;
-    for (u64 g0 = (u64)blockIdx.x * blockDim.x; g0 < slots; g0 += (u64)gridDim.x * blockDim.x) {
-        if (threadIdx.x == 0) stage_n = 0;
-        __syncthreads();
-        const u64 g = g0 + threadIdx.x;
-        if (g < slots) {
-            const u32 q = (u32)(g / C), i = (u32)(g - (u64)q * C);
-            if (i < cnt_q[q]) {
-                const u64* rec = recv + (u64)q * S + DIST_HDR + (u64)i * REC;
-                u64 ns[W];
+    if (threadIdx.x < 64) {  // counts from the bucket headers (source q's row, word `me`), scanned in wave 0
+        const u32 lane = threadIdx.x;
+        u32 c = 0;
+        if (lane < nparts) c = (u32)min<u64>(recv[(u64)lane * S + me], C);
+        u32 incl = c;
 #pragma unroll
-                for (int x = 0; x < W; ++x) ns[x] = rec[x];
-                const u64 pgid = PAR_SEARCH;
-                bool is_new;
-                find_or_claim(t, probe_key(m, t, ns), &is_new, &lc->err);
-                if (is_new) {
-                    const u32 kk = atomicAdd(&stage_n, 1u);  // < STAGE: one slot per thread
-#pragma unroll
-                    for (int x = 0; x < W; ++x) stage[kk * W + x] = ns[x];
-                    stage_par[kk] = pgid;
-                }
-            }
+        for (int d = 1; d < 64; d <<= 1) {
+            const u32 y = __shfl_up(incl, d, 64);
+            if ((int)lane >= d) incl += y;
         }
-        __syncthreads();
-        const u32 nl = stage_n;
-        if (threadIdx.x == 0) base = nl ? atomicAdd(&lc->claims, nl) : 0;
-        __syncthreads();
-        for (u32 k = threadIdx.x; k < nl; k += blockDim.x) {
-            const u32 pos = base + k;
-            u64 ns[W];
-#pragma unroll
-            for (int x = 0; x < W; ++x) ns[x] = stage[k * W + x];
-            if (pos < next_cap) {
-                store_state<W>(next, pos, ns);
-                next_par[pos] = stage_par[k];
-            } else {
-                atomicOr(&lc->err, (u32)ERR_FRONTIER_OVERFLOW);
-            }
-            eval_props(m, ns, pos, undiscovered, lc);
-        }
-        __syncthreads();  // the stage is reused by the next round
+        if (lane < nparts) qoff[lane] = incl - c;
+        if (lane == nparts - 1) qoff[nparts] = incl;
+        if (lane == 0) stage_n = 0;
     }
+    __syncthreads();
+    const u32 total = qoff[nparts];
+    // record g: source q = the last with qoff[q] <= g (binary search over <= 64 sources)
+    auto rec_at = [&](u32 g) {
+        u32 q = 0;
+#pragma unroll
+        for (u32 step = MAX_PARTS / 2; step >= 1; step >>= 1)
+            if (q + step < nparts && qoff[q + step] <= g) q += step;
+        return recv + (u64)q * S + DIST_HDR + (u64)(g - qoff[q]) * REC;
+    };
+    insert_records(m, rec_at, total, t, next, next_par, next_cap, lc, undiscovered, stage, STAGE, stage_n, base);
     if (!last_block(lc)) return;
     // every row (the bucket headers) to the host, then the close
     const u32 rw = nparts + 6 + M::NPROPS;
