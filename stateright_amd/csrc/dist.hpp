@@ -735,7 +735,7 @@ class DistEngine final : public EngineBase {
                 ensure_arena(p, nb + p.n_hi + (u64)((double)n_plan * npp) + 4096, nb + p.n_hi);
                 if (o_.profile) SR_HIP(hipEventRecord(event(2 * stats.expand_launches), stream_));
                 const u32 ppw_log2 = route_ppw_env_ >= 0 ? (u32)route_ppw_env_ : ppw_for(p.n_est);
-                const u32 grid = (u32)std::min<u64>(std::max<u64>(1, blocks_for(p.n_hi, 4u << ppw_log2)), 8192);
+                const u32 grid = (u32)std::min<u64>(std::max<u64>(1, blocks_for(p.n_hi, 4u << ppw_log2)), route_grid_cap());
                 u64* row = comm_ ? rows_mine_.p : rows_all_.p + (u64)p.id * RW;
                 expand_route<M, 1><<<grid, 256, route_lds(), stream_>>>(
                     m_, p.arena.p, p.apar.p, nb, p.arena_cap, p.view(), p.id, T_, p.send.p, (u32)p.bucket_cap,
@@ -1027,7 +1027,7 @@ class DistEngine final : public EngineBase {
         for (auto& p : parts_) {
             if (o_.profile) SR_HIP(hipEventRecord(event(2 * stats.expand_launches), stream_));
             const u32 ppw_log2 = route_ppw_env_ >= 0 ? (u32)route_ppw_env_ : ppw_for(n_plan[p.id]);
-            const u32 grid = (u32)std::min<u64>(std::max<u64>(1, blocks_for(n_plan[p.id], 4u << ppw_log2)), 8192);
+            const u32 grid = (u32)std::min<u64>(std::max<u64>(1, blocks_for(n_plan[p.id], 4u << ppw_log2)), route_grid_cap());
             u64* row = comm_ ? rows_mine_.p : rows_all_.p + (u64)p.id * RW;
             expand_route<M, 1><<<grid, 256, route_lds(), stream_>>>(
                 m_, p.arena.p, p.apar.p, 0, p.arena_cap, p.view(), p.id, T_, p.send.p + DIST_HDR, (u32)C, p.sendc.p,
@@ -1443,6 +1443,19 @@ class DistEngine final : public EngineBase {
         return (filt_log2_ ? (8u << filt_log2_) : 0u) + (size_t)rstage_recs() * (REC * 8 + 2 + 1) +
                (size_t)route_local_stage(T_, W) * (W * 8 + 4);
     }
+    // expand_route's grid: two device residencies at its LDS footprint (expand_fast's rule); the
+    // kernel strides over further parents. SR_ROUTE_GRID_MAX > 0 overrides it.
+    u32 route_grid_cap() {
+        if (route_grid_max_) return route_grid_max_;
+        if (const char* e = std::getenv("SR_ROUTE_GRID_MAX"))
+            if (std::atoi(e) > 0) return route_grid_max_ = (u32)std::atoi(e);
+        int per_cu = 0, cus = 0;
+        SR_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)expand_route<M, 1>, 256, route_lds()));
+        SR_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, o_.device));
+        route_grid_max_ = per_cu > 0 && cus > 0 ? (u32)(2 * per_cu * cus) : 8192u;
+        return route_grid_max_;
+    }
+    u32 route_grid_max_ = 0;
     // insert kernels: workgroups at most (each reserves frontier space with a same-line atomic,
     // ~11 ns apiece; 512 x 256 threads keep enough probes in flight)
     static constexpr u32 INSERT_GRID_MAX = 512;
