@@ -212,28 +212,34 @@ struct TwoPhase {
     int max_out_degree() const { return 2 + 3 * n; }
     SR_HD u64 rmask() const { return (1ull << n) - 1; }
     // per-rm bit vectors
-    SR_HD u64 working(u64 s) const {  // rm_state == 0
-        u64 w = 0;
-        for (int rm = 0; rm < n; ++rm) w |= (u64)(((s >> (2 * rm)) & 3) == 0) << rm;
+    SR_HD u64 working(u64 s) const {  // rm_state == 0, one bit per rm
+        const u64 ev = 0x5555555555555555ull & ((1ull << (2 * n)) - 1);
+        u64 w = ~(s | (s >> 1)) & ev;  // bit 2rm: field rm == 0
+        // compress the even bits to bits 0..n-1
+        w = (w | (w >> 1)) & 0x3333333333333333ull;
+        w = (w | (w >> 2)) & 0x0f0f0f0f0f0f0f0full;
+        w = (w | (w >> 4)) & 0x00ff00ff00ff00ffull;
+        w = (w | (w >> 8)) & 0x0000ffff0000ffffull;
+        w = (w | (w >> 16)) & 0x00000000ffffffffull;
         return w;
     }
+    // One 5-bit group per rm at slot 2 + 5rm (TmRcvPrepared, RmPrepare, RmChooseToAbort,
+    // RmRcvCommitMsg, RmRcvAbortMsg), placed without per-action branches.
     SR_HD void enabled(const u64* sp, u64* m) const {
-        u64 s = sp[0];
-        u64 tm = (s >> (2 * n)) & 3;
-        u64 prepared = (s >> (2 * n + 2)) & rmask();
-        u64 msgp = (s >> (3 * n + 2)) & rmask();
-        u64 commit = (s >> (4 * n + 2)) & 1, abort = (s >> (4 * n + 3)) & 1;
-        u64 work = working(s);
-        u64 lo = 0, hi = 0;
-        auto set = [&](int a) { if (a < 64) lo |= 1ull << a; else hi |= 1ull << (a - 64); };
-        if (tm == 0 && prepared == rmask()) set(0);
-        if (tm == 0) set(1);
+        const u64 s = sp[0];
+        const u64 tm = (s >> (2 * n)) & 3;
+        const u64 prepared = (s >> (2 * n + 2)) & rmask();
+        const u64 msgp = (s >> (3 * n + 2)) & rmask();
+        const u64 commit = (s >> (4 * n + 2)) & 1, abort = (s >> (4 * n + 3)) & 1;
+        const u64 work = working(s);
+        const u64 rcv = tm == 0 ? msgp : 0;
+        const u64 tail = commit << 3 | abort << 4;
+        u64 lo = (u64)(tm == 0 && prepared == rmask()) | (u64)(tm == 0) << 1, hi = 0;
         for (int rm = 0; rm < n; ++rm) {
-            int b = 2 + 5 * rm;
-            if (tm == 0 && ((msgp >> rm) & 1)) set(b);
-            if ((work >> rm) & 1) { set(b + 1); set(b + 2); }
-            if (commit) set(b + 3);
-            if (abort) set(b + 4);
+            const int b = 2 + 5 * rm;
+            const u64 bits = ((rcv >> rm) & 1) | ((work >> rm) & 1) * 6ull | tail;
+            if (b < 64) lo |= bits << b;
+            if (b + 4 >= 64) hi |= b >= 64 ? bits << (b - 64) : bits >> (64 - b);
         }
         m[0] = lo;
         m[1] = hi;
@@ -282,17 +288,16 @@ struct TwoPhase {
         o[0] = ((s & ~fmask) | ((fval << fpos) & fmask)) | ebit;
         return true;
     }
+    // rm_state fields, bit-parallel: bit 2rm of `ab` is set iff rm is Aborted (3), of `cm` iff
+    // Committed (2) (the loop over the rms ran once per property for every new state).
+    SR_HD u64 even_mask() const { return 0x5555555555555555ull & ((1ull << (2 * n)) - 1); }
     SR_HD bool discovers(int p, const u64* sp) const {
-        u64 s = sp[0];
-        u64 aborted = 0, committed = 0;
-        for (int rm = 0; rm < n; ++rm) {
-            u64 r = (s >> (2 * rm)) & 3;
-            aborted |= (u64)(r == 3) << rm;
-            committed |= (u64)(r == 2) << rm;
-        }
-        if (p == 0) return aborted == rmask();         // sometimes "abort agreement"
-        if (p == 1) return committed == rmask();       // sometimes "commit agreement"
-        return aborted != 0 && committed != 0;         // always "consistent" violated
+        const u64 s = sp[0], ev = even_mask();
+        const u64 lo = s & ev, hi = (s >> 1) & ev;
+        const u64 ab = hi & lo, cm = hi & ~lo;
+        if (p == 0) return ab == ev;           // sometimes "abort agreement"
+        if (p == 1) return cm == ev;           // sometimes "commit agreement"
+        return ab != 0 && cm != 0;             // always "consistent" violated
     }
     int init_states(u64* out) const { out[0] = 0; return 1; }
     int expectation(int p) const { return p == 2 ? ALWAYS : SOMETIMES; }
