@@ -945,6 +945,8 @@ class Engine final : public EngineBase {
             int cus = 0;
             SR_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, o_.device));
             multi_grid_ = (u32)std::max(1, cus);  // one workgroup per CU: always resident
+            if (const char* e = std::getenv("SR_MULTI_GRID"))
+                if (std::atoi(e) > 0) multi_grid_ = std::min<u32>((u32)std::atoi(e), multi_grid_);
         }
         MultiCtl* mc = reinterpret_cast<MultiCtl*>(multi_.p);
         multi_init<<<1, 256, 0, stream_>>>(mc, multi_max_n_, (u32)MULTI_MAX_LEVELS, D_, budget);
