@@ -17,6 +17,11 @@
  *   optional: undescribe(const i64*, u64*)    (sr_plugin.fingerprint)
  *             emask()                         (the mask of `eventually` properties)
  *             qkey_bits(), SR_HD qkey(s)      (exact quotient visited set for multi-word states)
+ *             SR_HD self_loops(s, enabled, out)   out = the enabled slots whose next_state is s itself:
+ *                                             FAST expansion counts them (state_count) without
+ *                                             generating them; it must be EXACT (2pc: 37% of successors)
+ *             SR_HD canonical(s, out)         a canonical representative under the model's symmetry
+ *                                             (the opt-in symmetry_canonical reduction)
  *
  * Equal states must have equal words (the words ARE the state), and slots are enumerated in the
  * reference's `actions()` order, so FIFO runs reproduce the reference's visit order and paths.
