@@ -236,6 +236,11 @@ int32_t sr_device_synchronize(int32_t device);
 /* Host-only self-test of the visited set's quotient encoding (kernels.hpp): the key permutation is
  * a bijection and slot values decode to their keys. SR_OK or SR_ERR_ARG (sr_last_error). */
 int32_t sr_selftest_tables(void);
+/* Host-only self-check of the compiled-in model encodings: every slot a model's optional
+ * `self_loops` reports (counted by the FAST expansion without being generated) is enabled and
+ * returns the state itself, over every reachable state of 2pc N=1..7 (and its canonical form).
+ * SR_OK or SR_ERR_ARG (sr_last_error says where). */
+int32_t sr_selftest_models(void);
 /* comm == NULL: `virtual_partitions` partitions in this process on opts->device (same protocol,
  * device-copy exchange). FAST order only. */
 sr_bfs* sr_gpu_bfs_spawn_partitioned(sr_dist* comm, int32_t virtual_partitions, int32_t model_id,

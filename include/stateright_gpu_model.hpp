@@ -17,9 +17,11 @@
  *   optional: undescribe(const i64*, u64*)    (sr_plugin.fingerprint)
  *             emask()                         (the mask of `eventually` properties)
  *             qkey_bits(), SR_HD qkey(s)      (exact quotient visited set for multi-word states)
- *             SR_HD self_loops(s, enabled, out)   out = the enabled slots whose next_state is s itself:
+ *             SR_HD self_loops(s, enabled, out)   out = enabled slots whose next_state is s itself:
  *                                             FAST expansion counts them (state_count) without
- *                                             generating them; it must be EXACT (2pc: 37% of successors)
+ *                                             generating them. Every slot reported must be a
+ *                                             self-loop; an unreported one is still detected
+ *                                             (2pc reports all of them: 37% of successors)
  *             SR_HD canonical(s, out)         a canonical representative under the model's symmetry
  *                                             (the opt-in symmetry_canonical reduction)
  *

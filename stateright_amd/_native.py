@@ -115,6 +115,7 @@ SIGNATURES = [
     ("sr_hip_runtime_version", ctypes.c_int32, [ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32)]),
     ("sr_device_synchronize", ctypes.c_int32, [ctypes.c_int32]),
     ("sr_selftest_tables", ctypes.c_int32, []),
+    ("sr_selftest_models", ctypes.c_int32, []),
     ("sr_gpu_bfs_spawn_plugin", _P, [_P, _I64P, ctypes.c_int32, ctypes.POINTER(sr_opts)]),
     ("sr_gpu_bfs_spawn_plugin_partitioned", _P, [_P, _P, ctypes.c_int32, _I64P, ctypes.c_int32,
                                                  ctypes.POINTER(sr_opts)]),

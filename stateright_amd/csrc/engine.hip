@@ -1,5 +1,6 @@
 // MI355X breadth-first model-checking engine library: the compiled-in GpuModel registry and the
 // C ABI (include/stateright_gpu.h). The engine itself is engine.hpp.
+#include <unordered_set>
 #include "engine.hpp"
 #include "dgraph.hpp"
 #include "paxos.hpp"
@@ -66,6 +67,57 @@ struct sr_bfs {
     std::thread th;
     bool joined = false;
 };
+
+namespace sr {
+// Host BFS over the reachable states of m: every slot self_loops() reports must be enabled and
+// must return the state itself (the FAST expansion counts those slots without generating them).
+template <class M>
+static bool check_self_loops(const M& m, std::string& why) {
+    constexpr int W = M::W, MW = M::MW;
+    struct H {
+        size_t operator()(const std::vector<u64>& v) const {
+            u64 h = 0;
+            for (u64 x : v) h = fmix64(h ^ x) + 0x9E3779B97F4A7C15ull;
+            return (size_t)h;
+        }
+    };
+    std::unordered_set<std::vector<u64>, H> seen;
+    std::vector<u64> inits(256 * W);
+    const int k = m.init_states(inits.data());
+    std::vector<std::vector<u64>> queue;
+    for (int i = 0; i < k; ++i) {
+        std::vector<u64> st(inits.begin() + i * W, inits.begin() + (i + 1) * W);
+        if (seen.insert(st).second) queue.push_back(st);
+    }
+    for (size_t q = 0; q < queue.size(); ++q) {
+        const std::vector<u64> st = queue[q];
+        u64 mk[MW], sl[MW], o[W];
+        m.enabled(st.data(), mk);
+        m.self_loops(st.data(), mk, sl);
+        for (int w = 0; w < MW; ++w) {
+            if (sl[w] & ~mk[w]) {
+                why = "self_loops reports a slot that is not enabled";
+                return false;
+            }
+            for (u64 bits = sl[w]; bits; bits &= bits - 1) {
+                const int a = w * 64 + __builtin_ctzll(bits);
+                if (!m.apply(st.data(), a, o) || !std::equal(o, o + W, st.data())) {
+                    why = "self_loops reports slot " + std::to_string(a) + ", whose next state differs";
+                    return false;
+                }
+            }
+            for (u64 bits = mk[w]; bits; bits &= bits - 1) {
+                const int a = w * 64 + __builtin_ctzll(bits);
+                if (!m.apply(st.data(), a, o)) continue;
+                std::vector<u64> nx(o, o + W);
+                if (seen.insert(nx).second) queue.push_back(std::move(nx));
+            }
+        }
+    }
+    return true;
+}
+
+}  // namespace sr
 
 extern "C" {
 
@@ -517,6 +569,23 @@ int32_t sr_selftest_tables(void) {
                 set_error("quotient slot encode/decode mismatch at B=" + std::to_string(c[0]));
                 return SR_ERR_ARG;
             }
+        }
+    }
+    return SR_OK;
+}
+
+int32_t sr_selftest_models(void) {
+    std::string why;
+    for (int n = 1; n <= 7; ++n) {
+        TwoPhase m;
+        m.n = n;
+        if (!sr::check_self_loops(m, why)) {
+            set_error("2pc n=" + std::to_string(n) + ": " + why);
+            return SR_ERR_ARG;
+        }
+        if (n <= 6 && !sr::check_self_loops(Canon<TwoPhase>(m), why)) {
+            set_error("2pc n=" + std::to_string(n) + " (canonical): " + why);
+            return SR_ERR_ARG;
         }
     }
     return SR_OK;

@@ -87,3 +87,10 @@ def test_quotient_table_encoding_selftest():
     from stateright_amd import _native
     lib = _native.load()
     assert lib.sr_selftest_tables() == 0, _native.last_error()
+
+
+def test_selftest_models_self_loops():
+    # every self-loop slot the FAST expansion skips really returns the state (host BFS, 2pc N<=7)
+    from stateright_amd import _native
+    lib = _native.load()
+    assert lib.sr_selftest_models() == 0, _native.last_error()
