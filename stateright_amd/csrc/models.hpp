@@ -446,33 +446,48 @@ struct IncrementLock {
     int max_out_degree() const { return n; }
     // threads 0..7 live in word 0 (bits 5..60), threads 8.. in word 1 (bits 0..)
     SR_HD static int toff(int t) { return t < 8 ? 5 + 7 * t : 64 + 7 * (t - 8); }
+    // Bit-parallel over the threads: bit 0 of thread t's pc field sits at pc_pos(t); pc_mask(w) has
+    // those bits of word w, so b0/b1/b2 of every pc are three masked shifts of the word.
+    SR_HD static int pc_pos(int t) { return t < 8 ? 9 + 7 * t : 4 + 7 * (t - 8); }
+    SR_HD u64 pc_mask(int w) const {
+        u64 m = 0;
+        for (int t = w == 0 ? 0 : 8; t < (w == 0 ? (n < 8 ? n : 8) : n); ++t) m |= 1ull << pc_pos(t);
+        return m;
+    }
     SR_HD void enabled(const u64* s, u64* m) const {
-        u64 lock = getb(s, 4, 1), r = 0;
-        for (int t = 0; t < n; ++t) {
-            u64 pc = getb(s, toff(t) + 4, 3);
-            bool en = (pc == 0 && !lock) || pc == 1 || pc == 2 || (pc == 3 && lock);
-            r |= (u64)en << t;
+        const bool lock = (s[0] >> 4) & 1;
+        u64 r = 0;
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+            const u64 M = pc_mask(w), x = s[w];
+            const u64 b0 = x & M, b1 = (x >> 1) & M, b2 = (x >> 2) & M;
+            // Lock at pc 0 (lock free), Read at 1, Write at 2, Release at 3 (lock held)
+            const u64 en = ~b2 & ((b1 ^ b0) | (~(b1 | b0) & (lock ? 0 : M)) | (b1 & b0 & (lock ? M : 0))) & M;
+            for (int t = w == 0 ? 0 : 8; t < (w == 0 ? (n < 8 ? n : 8) : n); ++t) r |= ((en >> pc_pos(t)) & 1) << t;
         }
         m[0] = r;
     }
+    // Every action advances pc by one (Lock 0->1, Read 1->2, Write 2->3, Release 3->4); the other
+    // field it writes is selected without branches (the lanes of a wave run different threads).
     SR_HD bool apply(const u64* s, int t, u64* o) const {
 #pragma unroll
         for (int i = 0; i < W; ++i) o[i] = s[i];
-        u64 pc = getb(s, toff(t) + 4, 3);
-        switch (pc) {
-            case 0: setb(o, toff(t) + 4, 3, 1); setb(o, 4, 1, 1); break;                    // Lock
-            case 1: setb(o, toff(t) + 4, 3, 2); setb(o, toff(t), 4, getb(s, 0, 4)); break;  // Read
-            case 2: setb(o, toff(t) + 4, 3, 3); setb(o, 0, 4, getb(s, toff(t), 4) + 1); break; // Write
-            default: setb(o, toff(t) + 4, 3, 4); setb(o, 4, 1, 0); break;                  // Release
-        }
+        const u64 pc = getb(s, toff(t) + 4, 3), iv = getb(s, 0, 4), tv = getb(s, toff(t), 4);
+        const u64 lock = getb(s, 4, 1);
+        setb(o, toff(t) + 4, 3, pc + 1);
+        setb(o, 4, 1, pc == 0 ? 1 : pc == 3 ? 0 : lock);  // Lock / Release
+        setb(o, toff(t), 4, pc == 1 ? iv : tv);           // Read: t = i
+        setb(o, 0, 4, pc == 2 ? tv + 1 : iv);             // Write: i = t + 1
         return true;
     }
     SR_HD bool discovers(int p, const u64* s) const {
         u64 fin = 0, crit = 0;
-        for (int t = 0; t < n; ++t) {
-            u64 pc = getb(s, toff(t) + 4, 3);
-            fin += pc >= 3;
-            crit += pc >= 1 && pc < 4;
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+            const u64 M = pc_mask(w), x = s[w];
+            const u64 b0 = x & M, b1 = (x >> 1) & M, b2 = (x >> 2) & M;
+            fin += __builtin_popcountll(b2 | (b1 & b0));   // pc >= 3
+            crit += __builtin_popcountll(~b2 & (b1 | b0) & M);  // 1 <= pc < 4
         }
         if (p == 0) return fin != getb(s, 0, 4);  // always "fin"
         return crit > 1;                          // always "mutex"
