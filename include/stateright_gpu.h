@@ -146,6 +146,9 @@ int32_t sr_gpu_bfs_stats(const sr_bfs* bfs, sr_stats* out);
  * it expanded (0 if unknown); returns the number of launches (FAST pipelined order: launch i
  * expands level i, a last launch past the end expands nothing). */
 int64_t sr_gpu_bfs_launch_profile(const sr_bfs* bfs, double* kernel_ms, uint64_t* frontier, int64_t cap);
+/* Visited-set probes and CAS claims of every expand launch of the pipelined FAST loop, in launch
+ * order (sr_opts.counters = 1; zeros otherwise). Returns the number of launches. */
+int64_t sr_gpu_bfs_launch_counters(const sr_bfs* bfs, uint64_t* probes, uint64_t* cas, int64_t cap);
 
 int32_t sr_gpu_bfs_property_count(const sr_bfs* bfs);
 /* Copies the property name (NUL-terminated) and its expectation; returns the name length. */

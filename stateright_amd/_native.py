@@ -80,6 +80,8 @@ SIGNATURES = [
     ("sr_gpu_bfs_unique_state_count", ctypes.c_uint64, [_P]),
     ("sr_gpu_bfs_max_depth", ctypes.c_uint32, [_P]),
     ("sr_gpu_bfs_stats", ctypes.c_int32, [_P, ctypes.POINTER(sr_stats)]),
+    ("sr_gpu_bfs_launch_counters", ctypes.c_int64, [_P, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
+                                                    ctypes.c_int64]),
     ("sr_gpu_bfs_launch_profile", ctypes.c_int64, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64),
                                                    ctypes.c_int64]),
     ("sr_gpu_bfs_property_count", ctypes.c_int32, [_P]),

@@ -444,6 +444,14 @@ class GpuBfsChecker:
         self._lib.sr_gpu_bfs_launch_profile(self._h, ms, fr, n)
         return [(ms[i], fr[i]) for i in range(n)]
 
+    def launch_counters(self):
+        """[(probes, cas)] of every expand launch (builder.counters(); zeros otherwise)."""
+        n = self._lib.sr_gpu_bfs_launch_counters(self._h, None, None, 0)
+        pr = (ctypes.c_uint64 * max(1, n))()
+        cs = (ctypes.c_uint64 * max(1, n))()
+        self._lib.sr_gpu_bfs_launch_counters(self._h, pr, cs, n)
+        return [(pr[i], cs[i]) for i in range(n)]
+
     # --- report / asserts (src/checker.rs:216-337) ---------------------------------------------
     def discovery_classification(self, name):
         exp = dict(self.properties())[name]

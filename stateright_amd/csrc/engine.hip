@@ -284,6 +284,18 @@ int64_t sr_gpu_bfs_launch_profile(const sr_bfs* b, double* kernel_ms, uint64_t* 
     return n;
 }
 
+int64_t sr_gpu_bfs_launch_counters(const sr_bfs* b, uint64_t* probes, uint64_t* cas, int64_t cap) {
+    if (!b) return SR_ERR_ARG;
+    const auto& pr = b->e->launch_probes;
+    const auto& cs = b->e->launch_cas;
+    const int64_t n = (int64_t)pr.size();
+    for (int64_t i = 0; i < std::min(n, cap); ++i) {
+        if (probes) probes[i] = pr[i];
+        if (cas) cas[i] = i < (int64_t)cs.size() ? cs[i] : 0;
+    }
+    return n;
+}
+
 int32_t sr_gpu_bfs_property_count(const sr_bfs* b) { return b ? b->e->nprops() : 0; }
 
 int32_t sr_gpu_bfs_property(const sr_bfs* b, int32_t p, char* name, int32_t cap, int32_t* expectation) {

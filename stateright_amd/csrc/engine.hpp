@@ -84,6 +84,8 @@ class EngineBase {
     std::vector<DiscoveryRec> disc;
     std::vector<double> launch_ms;    // per timed launch (profile=1), in launch order
     std::vector<u64> launch_frontier; // the frontier each launch expanded (0 if unknown)
+    std::vector<u64> launch_probes;   // visited-set probes / CAS claims of each launch (the pipelined
+    std::vector<u64> launch_cas;      // FAST loop with sr_opts.counters; 0 otherwise)
 };
 
 template <class M>
@@ -567,6 +569,8 @@ class Engine final : public EngineBase {
         if (o_.profile) SR_HIP(hipEventRecord(ctx_->event(i + 1), stream_));
         stats.expand_launches++;
         launch_frontier.push_back(frontier);
+        launch_probes.push_back(0);
+        launch_cas.push_back(0);
     }
     void collect_timing() {
         if (!o_.profile || !stats.expand_launches) return;
@@ -595,6 +599,8 @@ class Engine final : public EngineBase {
         stats.order_used = (u32)order;
         launch_ms.clear();
         launch_frontier.clear();
+        launch_probes.clear();
+        launch_cas.clear();
         seq_launch_.clear();
 
         // Visited set sized for <= table_load_ load at the hinted unique count.
@@ -909,7 +915,11 @@ class Engine final : public EngineBase {
 
             wait_publish(sq);  // lc_ = this level's counters
             auto it = seq_launch_.find(sq);
-            if (it != seq_launch_.end() && it->second < launch_frontier.size()) launch_frontier[it->second] = n;
+            if (it != seq_launch_.end() && it->second < launch_frontier.size()) {
+                launch_frontier[it->second] = n;
+                launch_probes[it->second] = lc_.probes;
+                launch_cas[it->second] = lc_.cas;
+            }
             if (!account(lc_, spec ? " (next enqueued)" : "")) break;
             sq = spec ? sq_next : launch_next(n, undiscovered, multi);
         }
