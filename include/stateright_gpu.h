@@ -129,6 +129,10 @@ typedef struct sr_stats {
 typedef struct sr_bfs sr_bfs;
 
 void sr_opts_init(sr_opts* opts);
+/* The same for a caller whose sr_opts mirror has `size` bytes (a binding written against an older
+ * header): writes at most `size` bytes and sets struct_size to what it wrote. Bindings in other
+ * languages should call this with their own struct size rather than sr_opts_init. */
+void sr_opts_init_sized(sr_opts* opts, uint32_t size);
 const char* sr_last_error(void);
 int sr_device_count(void);
 

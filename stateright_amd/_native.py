@@ -70,6 +70,7 @@ _P = ctypes.c_void_p
 _I64P = ctypes.POINTER(ctypes.c_int64)
 SIGNATURES = [
     ("sr_opts_init", None, [ctypes.POINTER(sr_opts)]),
+    ("sr_opts_init_sized", None, [ctypes.POINTER(sr_opts), ctypes.c_uint32]),
     ("sr_last_error", ctypes.c_char_p, []),
     ("sr_device_count", ctypes.c_int, []),
     ("sr_gpu_bfs_spawn", _P, [ctypes.c_int32, _I64P, ctypes.c_int32, ctypes.POINTER(sr_opts)]),

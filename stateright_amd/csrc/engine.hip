@@ -126,6 +126,15 @@ void sr_opts_init(sr_opts* o) {
     o->struct_size = sizeof(sr_opts);
 }
 
+void sr_opts_init_sized(sr_opts* o, uint32_t size) {
+    // a caller built against an older (shorter) sr_opts: only its own bytes are written, and the
+    // engine reads only struct_size bytes back (normalized_opts), defaulting the rest
+    const uint32_t n = size < (uint32_t)sizeof(sr_opts) ? size : (uint32_t)sizeof(sr_opts);
+    if (!o || n < sizeof(uint32_t)) return;
+    std::memset(o, 0, n);
+    o->struct_size = n;
+}
+
 const char* sr_last_error(void) { return g_last_error.c_str(); }
 
 int sr_device_count(void) {

@@ -94,3 +94,18 @@ def test_selftest_models_self_loops():
     from stateright_amd import _native
     lib = _native.load()
     assert lib.sr_selftest_models() == 0, _native.last_error()
+
+
+def test_opts_init_sized_writes_only_the_callers_bytes():
+    # a binding built against an older, shorter sr_opts: the library must not write past it
+    import ctypes as C
+    from stateright_amd import _native
+    lib = _native.load()
+    buf = (C.c_uint8 * 128)(*([0xAB] * 128))
+    lib.sr_opts_init_sized(C.cast(buf, C.POINTER(_native.sr_opts)), 24)
+    assert int.from_bytes(bytes(buf[0:4]), "little") == 24  # struct_size = what it wrote
+    assert bytes(buf[4:24]) == bytes(20)
+    assert bytes(buf[24:128]) == bytes([0xAB] * 104)
+    full = _native.sr_opts()
+    lib.sr_opts_init_sized(C.byref(full), 4096)  # a larger mirror: the library's own size
+    assert full.struct_size == C.sizeof(_native.sr_opts)
