@@ -1169,9 +1169,11 @@ class Engine final : public EngineBase {
         const u32 lmax = W >= 4 ? 4 : 6;  // expand_fast's PPW_LOG2_MAX
         u32 l = 2;
         while (l < lmax && (double)(2u << l) <= ppw) ++l;
-        while (l > 2 && ((c + (1u << l) - 1) >> l) < 1024) --l;
+        while (l > 2 && ((c + (1u << l) - 1) >> l) < ppw_waves_) --l;
         return l;
     }
+    u64 ppw_waves_ = std::getenv("SR_PPW_WAVES") && std::atoll(std::getenv("SR_PPW_WAVES")) > 0
+                         ? (u64)std::atoll(std::getenv("SR_PPW_WAVES")) : 1024;
 
     // The frontier being expanded: the arena's second-to-last level.
     const u64* cur() const { return arena_.p + lstart_[lstart_.size() - 2] * W; }
