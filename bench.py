@@ -412,7 +412,11 @@ def main():
         },
         "state_count_per_sec": float(final_state_count) * (1 if partitioned else world) * args.steps / elapsed,
         "roofline": {
+            # HBM-side, but by random transactions (8-byte probes and CAS claims that each move a
+            # memory line), not by bytes: `limiter` names the largest measured fraction
             "bound": "hbm",
+            "bound_detail": "random HBM transactions (visited-set probes + CAS claims) against the "
+                            "microbenchmarked 49 G/s mix ceiling; bytes/s against 8 TB/s is `frac`",
             "limiter": max(fracs, key=fracs.get),
             "fractions": fracs,
             "kernel": ("expand_route" if partitioned else "expand_fast") +
