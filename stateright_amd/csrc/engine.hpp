@@ -1166,7 +1166,7 @@ class Engine final : public EngineBase {
     u32 ppw_for(u64 c) const {
         const double rounds = W >= 4 ? 4.0 : 16.0;
         const double ppw = 64.0 * rounds / en_ratio_;
-        const u32 lmax = W >= 4 ? 4 : 6;  // expand_fast's PPW_LOG2_MAX
+        const u32 lmax = W >= 4 ? SR_WIDE_PPW_LOG2_MAX : 6;  // expand_fast's PPW_LOG2_MAX
         u32 l = 2;
         while (l < lmax && (double)(2u << l) <= ppw) ++l;
         while (l > 2 && ((c + (1u << l) - 1) >> l) < ppw_waves_) --l;

@@ -29,9 +29,17 @@ constexpr u32 CAND_NONE = 0xffffffffu;
 constexpr int MAX_PROBE = 1 << 16;
 constexpr int MAX_PROPS = 32;
 constexpr int MAX_PARTS = 64;  // visited-set partitions (one per GPU, or virtual ones on one GPU)
+// expand_fast's largest parents per wave (log2) for wide states (W >= 4).
+#ifndef SR_WIDE_PPW_LOG2_MAX
+#define SR_WIDE_PPW_LOG2_MAX 4
+#endif
 // expand_fast's LDS stage of new states, in 64-bit words (its size sets the blocks per CU).
 #ifndef SR_STAGE_WORDS
 #define SR_STAGE_WORDS 1024
+#endif
+// ... and for wide states (W >= 4), whose blocks per CU are set by registers, not LDS.
+#ifndef SR_WIDE_STAGE_WORDS
+#define SR_WIDE_STAGE_WORDS 2048
 #endif
 
 enum ErrBits { ERR_TABLE_FULL = 1, ERR_FRONTIER_OVERFLOW = 2 };
@@ -674,13 +682,13 @@ __global__ void __launch_bounds__(256) expand_fast(M m, const u64* __restrict__ 
                                                    HostCounters* hc, u32 seq, u32 reset, u32 ppw_log2,
                                                    u32 filt_log2, SlotWork sw, MultiCtl* mc) {
     constexpr int W = M::W, MW = M::MW;
-    constexpr int STAGE = SR_STAGE_WORDS / W;
+    constexpr int STAGE = (W >= 4 ? SR_WIDE_STAGE_WORDS : SR_STAGE_WORDS) / W;
     extern __shared__ u64 filt[];       // 2^filt_log2 fingerprints (dynamic LDS; 0 = no filter)
     __shared__ u64 stage[STAGE * W];
     __shared__ u32 stage_par[STAGE];
     // Parents per wave at most: wide states (paxos, W = 11) take few parents per wave (ppw_for), and
     // staging 64 of them cost 22.5 KB of LDS per block, which capped residency at 3 blocks per CU.
-    constexpr u32 PPW_LOG2_MAX = W >= 4 ? 4 : 6;
+    constexpr u32 PPW_LOG2_MAX = W >= 4 ? SR_WIDE_PPW_LOG2_MAX : 6;
     __shared__ u64 pst[4][(1 << PPW_LOG2_MAX) * W];     // parent states of each wave
     // The wave's successor list, one u16 per successor: parent (bits 0-5) | action << 6, written by
     // the parent lanes (a ctz loop over their enabled masks) in windows of MAPCAP successors. A
