@@ -123,7 +123,7 @@ typedef struct sr_stats {
     uint64_t head_levels;        /* partitioned search: levels run replicated before partitioning */
     uint64_t probes;             /* visited-set slots loaded by the expand kernels (first probe + linear steps) */
     uint64_t cas;                /* 64-bit atomicCAS claims attempted on the visited set */
-    uint64_t multi_levels;       /* levels run inside multi-level launches (small frontiers, FAST order) */
+    uint64_t multi_levels;       /* reserved, always 0 (multi-level launches were measured and removed) */
 } sr_stats;
 
 typedef struct sr_bfs sr_bfs;

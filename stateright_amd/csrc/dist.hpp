@@ -945,7 +945,7 @@ class DistEngine final : public EngineBase {
             p0.seq++;
             expand_fast<M, 1, 0><<<grid, 256, filt_log2_ ? (8u << filt_log2_) : 0u, stream_>>>(
                 m_, harena_.p + fb * W, 0u, (u32)n, hv, harena_.p + nb * W, hpar_.p + nb, ncap, p0.lc, und, p0.hc_dev, p0.seq,
-                1u, ppw_log2, filt_log2_, SlotWork{}, nullptr);
+                1u, ppw_log2, filt_log2_, SlotWork{});
             SR_HIP(hipGetLastError());
             wait(p0);
             if (p0.last.err) {

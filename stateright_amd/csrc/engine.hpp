@@ -641,8 +641,7 @@ class Engine final : public EngineBase {
         // FAST pipelined order: level 0 is enqueued before the host reads the roots' outcome (it is
         // ignored if the roots already discover every property)
         const bool pipelined = !fifo_ && !emask_ && !o_.target_state_count && M::NPROPS > 0 && pipeline_;
-        bool multi0 = false;
-        const u32 sq_level0 = pipelined ? launch_next((u64)k, (1u << M::NPROPS) - 1, multi0) : 0u;
+        const u32 sq_level0 = pipelined ? launch_sync((u64)k, (1u << M::NPROPS) - 1) : 0u;
         wait_publish(sq);
         state_count = (u64)k;
         unique = lc_.claims;
@@ -652,7 +651,7 @@ class Engine final : public EngineBase {
         u32 level = 0;
         bool order_dependent = false;
         auto t_loop = Clock::now();
-        if (pipelined) order_dependent = pipeline_levels(n, sq_level0, multi0);
+        if (pipelined) order_dependent = pipeline_levels(n, sq_level0);
         else for (;;) {
             // 1. Discoveries among this level's states (evaluated when they were produced).
             u32 newly = 0, max_rank = 0;
@@ -799,7 +798,7 @@ class Engine final : public EngineBase {
     // the visited set or the arena might not hold it (that level is then launched after the wait,
     // sized exactly). A speculative level launched past the end (an exhausted frontier or an early
     // exit) is ignored. Returns whether the run stopped early inside a level.
-    bool pipeline_levels(u64 n, u32 sq_level0, bool multi) {
+    bool pipeline_levels(u64 n, u32 sq_level0) {
         u32 undiscovered = (1u << M::NPROPS) - 1;
         u32 level = 0;
         bool order_dependent = false;
@@ -866,47 +865,12 @@ class Engine final : public EngineBase {
         };
         u32 sq = sq_level0;  // enqueued before the roots' outcome was read
         for (;;) {
-            if (multi) {
-                // a multi-level launch: the per-level counters of every level it ran
-                wait_publish(sq);
-                const u32 k = lc_.aux;
-                if (k == 0 || k > (u32)MULTI_MAX_LEVELS) throw Error(SR_ERR_HIP, "multi-level launch: bad level count");
-                std::vector<LevelCounters> recs(k);
-                u32 merr = 0;
-                MultiCtl* mc = reinterpret_cast<MultiCtl*>(multi_.p);
-                SR_HIP(hipMemcpyAsync(recs.data(), mc->lcs, k * sizeof(LevelCounters), hipMemcpyDeviceToHost, stream_));
-                SR_HIP(hipMemcpyAsync(&merr, &mc->err, sizeof(u32), hipMemcpyDeviceToHost, stream_));
-                SR_HIP(hipStreamSynchronize(stream_));
-                if (merr) throw Error(SR_ERR_HIP, "multi-level launch: the device-wide barrier timed out");
-                stats.multi_levels += k;
-                bool go = true;
-                for (u32 i = 0; i < k && go; ++i) {
-                    HostCounters c{};
-                    for (const StatShard& sh : recs[i].stat) {  // summed over the shards
-                        c.successors += sh.successors;
-                        c.enabled += sh.enabled;
-                        c.probes += sh.probes;
-                        c.cas += sh.cas;
-                    }
-                    c.claims = recs[i].claims;
-                    c.err = recs[i].err;
-                    for (int p = 0; p < M::NPROPS; ++p) c.disc[p] = recs[i].disc[p];
-                    if (c.err & ERR_TABLE_FULL) throw Error(SR_ERR_CAPACITY, "visited set probe limit exceeded");
-                    if (c.err & ERR_FRONTIER_OVERFLOW) throw Error(SR_ERR_CAPACITY, "frontier overflow");
-                    go = account(c, " (multi-level launch)");
-                }
-                if (!go) break;
-                sq = launch_next(n, undiscovered, multi);
-                continue;
-            }
-            // enqueue the next level before waiting for this one, unless it is predicted small:
-            // the multi-level form is then launched after the wait, sized exactly
+            // enqueue the next level before waiting for this one
             const double g = std::max(ratio_, 1.0) * 1.5;
             const u64 est1 = (u64)((double)n * g) + 1024;     // the next frontier
             const u64 est2 = (u64)((double)est1 * g) + 1024;  // the states it will claim
             const u64 nb_next = lstart_.back();
-            const bool small_next = multi_max_n_ && (double)n * ratio_ <= (double)multi_max_n_;
-            const bool spec = !pessimistic_ && !small_next && (double)(unique + est1 + est2) < 0.8 * (double)cap_ &&
+            const bool spec = !pessimistic_ && (double)(unique + est1 + est2) < 0.8 * (double)cap_ &&
                               nb_next + est1 + est2 <= arena_cap_;
             // launch shape: a tight estimate (the grid strides over any excess)
             const u64 shape = (u64)((double)n * std::max(ratio_, 0.05) * 1.1) + 64;
@@ -921,55 +885,11 @@ class Engine final : public EngineBase {
                 launch_cas[it->second] = lc_.cas;
             }
             if (!account(lc_, spec ? " (next enqueued)" : "")) break;
-            sq = spec ? sq_next : launch_next(n, undiscovered, multi);
+            sq = spec ? sq_next : launch_sync(n, undiscovered);
         }
         (void)hipStreamSynchronize(stream_);
         fill_discovery_fps();
         return order_dependent;
-    }
-
-    // The next level after a host wait: the multi-level form when its frontier is small (and the
-    // visited set and arena leave room for it), otherwise one ordinary launch.
-    u32 launch_next(u64 n, u32 undiscovered, bool& multi) {
-        multi = false;
-        if (multi_max_n_ && n <= multi_max_n_) {
-            const u64 fbase = lstart_[lstart_.size() - 2];
-            const u64 d_eff = std::min<u64>(D_, (u64)std::ceil(2.0 * ratio_ + 1.0));
-            while ((double)(unique + n * d_eff) > 0.8 * (double)cap_) grow_table();
-            ensure_arena(fbase + n + std::max<u64>(n * D_, multi_arena_min_), fbase + n);
-            const u64 nbase = fbase + n;
-            const u64 room_t = (u64)(0.8 * (double)cap_) > unique.load() ? (u64)(0.8 * (double)cap_) - unique.load() : 0;
-            const u64 room_a = arena_cap_ > nbase ? arena_cap_ - nbase : 0;
-            const u64 budget = std::min(room_t, room_a);
-            if (budget >= n * D_) {
-                multi = true;
-                return launch_multi(fbase, (u32)n, undiscovered, budget);
-            }
-        }
-        return launch_sync(n, undiscovered);
-    }
-
-    u32 launch_multi(u64 fbase, u32 n, u32 undiscovered, u64 budget) {
-        if (!multi_.p) multi_.alloc(o_.device, (sizeof(MultiCtl) + 7) / 8);
-        if (!multi_grid_) {
-            int cus = 0;
-            SR_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, o_.device));
-            multi_grid_ = (u32)std::max(1, cus);  // one workgroup per CU: always resident
-            if (const char* e = std::getenv("SR_MULTI_GRID"))
-                if (std::atoi(e) > 0) multi_grid_ = std::min<u32>((u32)std::atoi(e), multi_grid_);
-        }
-        MultiCtl* mc = reinterpret_cast<MultiCtl*>(multi_.p);
-        multi_init<<<1, 256, 0, stream_>>>(mc, multi_max_n_, (u32)MULTI_MAX_LEVELS, D_, budget);
-        SR_HIP(hipGetLastError());
-        const u32 sq = next_seq();
-        const u64 nbase = fbase + n;
-        const u32 ncap = (u32)std::min<u64>(arena_cap_ - nbase, 0xffffffffu);
-        timed([&] {
-            expand_fast<M, 1, 0, false, true><<<multi_grid_, 256, filt_log2_ ? (8u << filt_log2_) : 0u, stream_>>>(
-                m_, arena_.p + fbase * W, 0u, n, view(), arena_.p + nbase * W, apar_.p + nbase, ncap, lc_d_, undiscovered,
-                hcd(sq), sq, 0u, 2u, filt_log2_, SlotWork{}, mc);
-        }, n);
-        return sq;
     }
 
     // Launch of the level whose frontier (n states) ends the arena, after the previous one is done:
@@ -1017,7 +937,7 @@ class Engine final : public EngineBase {
             auto launch = [&](auto kern) {
                 kern<<<grid + svc, 256, filt_log2_ ? (8u << filt_log2_) : 0u, stream_>>>(
                     m_, arena_.p + fbase * W, 0u, n, view(), arena_.p + nbase * W, apar_.p + nbase, ncap, lc,
-                    undiscovered, nullptr, sq, 0u, ppw_log2, filt_log2_, sw, nullptr);
+                    undiscovered, nullptr, sq, 0u, ppw_log2, filt_log2_, sw);
             };
             if (o_.counters) launch(expand_fast<M, 1, 0, true>);
             else switch (probe_batch_ * 10 + probe_load_) {
@@ -1108,7 +1028,7 @@ class Engine final : public EngineBase {
                     auto launch = [&](auto kern) {
                         kern<<<grid, 256, filt_log2_ ? (8u << filt_log2_) : 0u, stream_>>>(
                             m_, cur(), ulo, uhi, view(), next, npar, ncap, lc_d_, undiscovered, hcd(sq), sq,
-                            last ? 1u : 0u, ppw_log2, filt_log2_, SlotWork{}, nullptr);
+                            last ? 1u : 0u, ppw_log2, filt_log2_, SlotWork{});
                     };
                     if (o_.counters) launch(expand_fast<M, 1, 0, true>);
                     else switch (probe_batch_ * 10 + probe_load_) {
@@ -1190,13 +1110,6 @@ class Engine final : public EngineBase {
     u32 grid_max_ = 0;       // cap on expand_fast's grid, 0 = two device residencies (SR_GRID_MAX)
     u64 query_mask_ = 4095;  // spins between hipStreamQuery calls in wait_publish (SR_QUERY_LOG2)
     bool pipeline_ = true;  // FAST-order level pipelining (SR_PIPELINE=0 disables, for A/B runs)
-    // Multi-level launches for frontiers up to multi_max_n_ states (SR_MULTI_MAX_N; 0 = off, the
-    // default: measured no faster than pipelined single-level launches, a small level costs ~16 us
-    // either way, profiles/r02_multi_level_ab.txt).
-    u32 multi_max_n_ = std::getenv("SR_MULTI_MAX_N") ? (u32)std::atoi(std::getenv("SR_MULTI_MAX_N")) : 0;
-    u64 multi_arena_min_ = 1u << 20;  // arena room reserved ahead of a multi-level launch (states)
-    u32 multi_grid_ = 0;              // its workgroups: one per CU
-    DBuf<u64> multi_;                 // its MultiCtl
     DBuf<u64> slots_;                 // SLOTS per-level counter slots (the pipelined loop)
     u32 slot_k_ = 0;                  // slotted launches in this run
     u32 slot_seq_ = 0;                // sequence number of the last one

@@ -558,129 +558,12 @@ __device__ __forceinline__ u32 select_bit(u64 m, u32 k) {
 // STATS = 1 also counts visited-set probes and CAS attempts (sr_opts.counters): a separate
 // instantiation, because the per-lane counters cost registers (SGPR spills 8 -> 47) and ~20% of
 // the kernel's time.
-// ---- the multi-level form of expand_fast (small levels, FAST order) ----
-// A level of a few thousand states takes a launch of ~13-17 us, almost all of it a chain of
-// dependent memory round trips (parent load, probe, claim, append, counters, ticket, publish) plus
-// the launch itself, and the host learns its outcome before it can size the next one. The
-// multi-level form runs consecutive small levels in ONE launch of one resident workgroup per CU:
-// each level is the ordinary expand_fast body over the frontier, then a device-wide barrier, then
-// every workgroup reads the next frontier size and the discoveries from that level's own counters
-// (lcs[l]) and decides the same way whether to go on. It stops before a level with more than max_n
-// parents, when every property is discovered, when the frontier is exhausted, at max_levels, or
-// when the next level could overflow the visited set / arena budget; the host then reads the
-// per-level counters once and continues with ordinary launches.
-constexpr int MULTI_MAX_LEVELS = 48;
-struct MultiCtl {
-    u32 bar_count;       // barrier arrivals
-    u32 pad0[31];
-    u32 bar_gen;         // barrier generation
-    u32 pad1[31];
-    u32 max_n;           // largest frontier run here
-    u32 max_levels;      // <= MULTI_MAX_LEVELS
-    u32 max_deg;         // new states per parent at most (the model's out-degree)
-    u32 levels;          // levels completed (the last workgroup's publish carries it as aux)
-    u32 err;             // 1: a barrier timed out
-    u32 pad2[27];
-    u64 budget;          // new states the visited set and the arena can still take
-    u64 pad3[15];
-    LevelCounters lcs[MULTI_MAX_LEVELS];
-};
-
-__global__ void multi_init(MultiCtl* mc, u32 max_n, u32 max_levels, u32 max_deg, u64 budget) {
-    const u32 lcw = sizeof(LevelCounters) / 4;
-    u32* w = reinterpret_cast<u32*>(mc->lcs);
-    for (u32 i = threadIdx.x; i < lcw * MULTI_MAX_LEVELS; i += blockDim.x) {
-        const u32 o = i % lcw;
-        const bool disc = o >= offsetof(LevelCounters, disc) / 4 && o < offsetof(LevelCounters, disc) / 4 + MAX_PROPS;
-        w[i] = disc ? ~0u : 0u;
-    }
-    if (threadIdx.x == 0) {
-        mc->bar_count = 0;
-        mc->max_n = max_n;
-        mc->max_levels = max_levels;
-        mc->max_deg = max_deg;
-        mc->levels = 0;
-        mc->err = 0;
-        mc->budget = budget;
-    }
-}
-
-// Device-wide barrier over a resident grid (MI355X_MICROARCH.md "barrier-counter": release before
-// the arrival, acquire after the generation flips; a bounded spin so that a grid that is not fully
-// resident fails with mc->err instead of hanging). Returns false on timeout.
-__device__ __forceinline__ bool grid_sync(MultiCtl* mc) {
-    __shared__ u32 ok_s;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        u32 ok = 1;
-        const u32 gen = __hip_atomic_load(&mc->bar_gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        if (atomicAdd(&mc->bar_count, 1u) == gridDim.x - 1) {
-            __hip_atomic_store(&mc->bar_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&mc->bar_gen, gen + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            const u64 t0 = wall_clock64();
-            while (__hip_atomic_load(&mc->bar_gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen) {
-                __builtin_amdgcn_s_sleep(1);
-                if (wall_clock64() - t0 > 200000000ull) {  // ~2 s at the 100 MHz constant clock
-                    ok = 0;
-                    atomicOr(&mc->err, 1u);
-                    break;
-                }
-            }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        ok_s = ok;
-    }
-    __syncthreads();
-    return ok_s != 0;
-}
-
-// The level loop of the multi-level form (see MultiCtl). `level` is expand_fast's per-level body.
-template <int NP, class Level>
-__device__ __forceinline__ void multi_levels(Level& level, const u64* frontier, u32 lo, u32 hi, u64* next,
-                                             u32* next_par, u32 next_cap, u32 undiscovered, u32 W, MultiCtl* mc,
-                                             HostCounters* hc, u32 seq) {
-    const u64* fr = frontier + (u64)lo * W;
-    u32 n = hi - lo, und = undiscovered;
-    u64 total = 0;
-    const u32 max_n = mc->max_n, max_levels = mc->max_levels, max_deg = mc->max_deg;
-    const u64 budget = mc->budget;
-    for (u32 l = 0;; ++l) {
-        LevelCounters* L = &mc->lcs[l];
-        level(fr, 0u, n, next, next_par, next_cap, L, und);
-        const bool ok = grid_sync(mc);
-        const u32 nn = __hip_atomic_load(&L->claims, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const u32 err = __hip_atomic_load(&L->err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        u32 newly = 0;
-#pragma unroll
-        for (int p = 0; p < NP; ++p)
-            if ((und >> p & 1) && __hip_atomic_load(&L->disc[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != ~0u)
-                newly |= 1u << p;
-        total += nn;
-        const bool stop = !ok || err || nn == 0 || nn > max_n || l + 1 >= max_levels || (newly && (und & ~newly) == 0) ||
-                          total + (u64)nn * max_deg > budget;
-        if (stop) {
-            if (threadIdx.x == 0) atomicMax(&mc->levels, l + 1);
-            publish<NP>(L, hc, seq, false, &mc->levels);
-            return;
-        }
-        und &= ~newly;
-        fr = next;
-        next += (u64)nn * W;
-        next_par += nn;
-        next_cap = next_cap > nn ? next_cap - nn : 0u;
-        n = nn;
-    }
-}
-
-template <class M, int PB, int POL, bool STATS = false, bool MULTI = false>
+template <class M, int PB, int POL, bool STATS = false>
 __global__ void __launch_bounds__(256) expand_fast(M m, const u64* __restrict__ frontier, u32 lo, u32 hi,
                                                    TableView t, u64* __restrict__ next, u32* __restrict__ next_par,
                                                    u32 next_cap, LevelCounters* lc, u32 undiscovered,
                                                    HostCounters* hc, u32 seq, u32 reset, u32 ppw_log2,
-                                                   u32 filt_log2, SlotWork sw, MultiCtl* mc) {
+                                                   u32 filt_log2, SlotWork sw) {
     constexpr int W = M::W, MW = M::MW;
     constexpr int STAGE = (W >= 4 ? SR_WIDE_STAGE_WORDS : SR_STAGE_WORDS) / W;
     extern __shared__ u64 filt[];       // 2^filt_log2 fingerprints (dynamic LDS; 0 = no filter)
@@ -704,7 +587,7 @@ __global__ void __launch_bounds__(256) expand_fast(M m, const u64* __restrict__ 
     // The previous level's publish and the slot reset (SlotWork) run in one extra workgroup, the
     // last of the grid: in a small level any workgroup that expands parents is on the critical
     // path, and the publish waits for its host stores to be acknowledged.
-    const bool svc = !MULTI && (sw.pub || sw.zero);
+    const bool svc = sw.pub || sw.zero;
     if (svc && blockIdx.x == gridDim.x - 1) {
         if (threadIdx.x < 64) slot_service<M::NPROPS>(sw, threadIdx.x);
         return;
@@ -726,9 +609,9 @@ __global__ void __launch_bounds__(256) expand_fast(M m, const u64* __restrict__ 
     const u32 ppw = 1u << ppw_log2;
     const u64 chunk = (u64)(blockDim.x >> 6) << ppw_log2;
     const u32 fmask = filt_log2 ? (1u << filt_log2) - 1 : 0;
-    if (MULTI || lo + (u64)blockIdx.x * chunk < hi)  // blocks past the frontier only take their ticket
+    if (lo + (u64)blockIdx.x * chunk < hi)  // blocks past the frontier only take their ticket
         for (u32 i = threadIdx.x; i < (fmask ? fmask + 1 : 0u); i += blockDim.x) filt[i] = 0;
-    // One level: parents [lo, hi) of `frontier` into `next` (the multi-level form calls it per level).
+    // One level: parents [lo, hi) of `frontier` into `next`.
     auto level = [&](const u64* __restrict__ frontier, u32 lo, u32 hi, u64* __restrict__ next,
                      u32* __restrict__ next_par, u32 next_cap, LevelCounters* lc, u32 undiscovered) {
     u32 succ = 0, enabled = 0, probes = 0, cas = 0;
@@ -937,16 +820,9 @@ __global__ void __launch_bounds__(256) expand_fast(M m, const u64* __restrict__ 
         }
         eval_props(m, ns, pos, undiscovered, lc);
     }
-    if constexpr (MULTI) {
-        if (threadIdx.x == 0) stage_n = 0;  // every thread read it before the flush's barrier
-    }
     };
-    if constexpr (!MULTI) {
-        level(frontier, lo, hi, next, next_par, next_cap, lc, undiscovered);
-        if (hc) publish<M::NPROPS>(lc, hc, seq, reset != 0, nullptr);  // a slotted launch is published by its successor
-    } else {
-        multi_levels<M::NPROPS>(level, frontier, lo, hi, next, next_par, next_cap, undiscovered, (u32)W, mc, hc, seq);
-    }
+    level(frontier, lo, hi, next, next_par, next_cap, lc, undiscovered);
+    if (hc) publish<M::NPROPS>(lc, hc, seq, reset != 0, nullptr);  // a slotted launch is published by its successor
 }
 
 // FIFO order, pass 1: insert-or-find every successor and record (level, parent rank, slot) in

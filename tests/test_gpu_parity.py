@@ -294,37 +294,3 @@ def test_small_grid_strides(case, grid, monkeypatch):
         assert (c.unique_state_count(), c.state_count(), c.max_depth()) == \
             (o.unique_state_count, o.state_count, o.max_depth)
         assert sorted(c.discoveries()) == o.discovery_names()
-
-
-@pytest.mark.parametrize("multi", ["0", "1000000000"])
-@pytest.mark.parametrize("case", [(TWO_PHASE, [3]), (TWO_PHASE, [7]), (INCREMENT_LOCK, [7]), (PAXOS, [2]),
-                                  (LINEAR_EQUATION, [2, 4, 7]), (LINEAR_EQUATION, [2, 10, 14]), (BINARY_CLOCK, [])],
-                         ids=ids)
-def test_multi_level_launches(case, multi, monkeypatch):
-    # SR_MULTI_MAX_N: frontiers up to this size run inside multi-level launches (one resident
-    # workgroup per CU, a device-wide barrier between levels). 0 disables them; 10^9 puts every
-    # level of these checks into them (budget permitting). AUTO order: an early exit reruns FIFO.
-    monkeypatch.setenv("SR_MULTI_MAX_N", multi)
-    model, params = case
-    o = oracle(model, params)
-    c, _ = gpu(model, params, "auto")
-    assert (c.unique_state_count(), c.state_count(), c.max_depth()) == (o.unique_state_count, o.state_count, o.max_depth)
-    assert sorted(c.discoveries()) == o.discovery_names()
-    for name, path in c.discoveries().items():
-        r = replay(model, params, path.action_ids, n_props=len(c.properties()))
-        assert r is not None
-    st = c.stats()
-    if multi == "0":
-        assert st["multi_levels"] == 0
-    elif st["order_used"] == 2:  # FAST (no early-exit rerun); the budget may hand levels back
-        assert 0 < st["multi_levels"] <= st["levels"], st
-
-
-def test_multi_level_on_bench_config(monkeypatch):
-    monkeypatch.setenv("SR_MULTI_MAX_N", "8192")
-    n = 9
-    c = sr.TwoPhaseSys(n).checker().capacity_hint(6 ** n + 4 ** n + 2 ** n).order("fast").spawn_bfs().join()
-    assert c.unique_state_count() == 6 ** n + 4 ** n + 2 ** n
-    assert 3 * c.state_count() == 4 * n * 6 ** n + 3 * (n + 1) * 4 ** n + 3 * n * 2 ** n + 6
-    assert c.max_depth() == 3 * n + 1
-    assert c.stats()["multi_levels"] > 0
