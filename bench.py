@@ -237,7 +237,12 @@ def main():
     from stateright_amd import IncrementLock, Paxos, TwoPhaseSys
     from stateright_amd import _native as N
     lib = N.load()
-    dev = local_rank if world > 1 else 0
+    # one GPU per rank: LOCAL_RANK when every rank sees the node's GPUs; a launcher that restricts
+    # each rank's visible devices leaves fewer (then the rank's own GPU is visible device 0)
+    ndev = lib.sr_device_count()
+    if ndev < 1:
+        raise SystemExit(f"rank {rank}: no GPU visible ({N.last_error()})")
+    dev = (local_rank % ndev) if world > 1 else 0
     versions = N.runtime_versions()
     hip_rt, hip_cc = versions["hip"]
     rccl_rt, rccl_cc = versions["rccl"]
