@@ -19,11 +19,13 @@ for _ in range(reps + 1):
         b = TwoPhaseSys(n).checker().capacity_hint(want).defer_paths()
         b = b.comm(c) if c is not None else b.partitions(world)
         cs.append(b.spawn_bfs())
+    recs = 0
     for c in cs:
         c.join()
         assert c.unique_state_count() == want
+        recs = c.stats()["records_routed"]
     del cs
 for c in comms:
     if c is not None:
         c.close()
-print("ok", kind, world, n, reps)
+print("ok", kind, world, n, reps, "records_routed", recs)

@@ -1045,7 +1045,7 @@ class DistEngine final : public EngineBase {
                     SR_HIP(hipMemcpyAsync(dst.recv.p + (u64)src.id * S, src.send.p + (u64)dst.id * S, S * 8,
                                           hipMemcpyDeviceToDevice, stream_));
         }
-        const u32 ig = (u32)std::min<u64>(std::max<u64>(1, blocks_for((u64)T_ * C, 256)), INSERT_GRID_MAX);
+        const u32 ig = insert_grid((u64)T_ * C);
         for (auto& p : parts_) {
             p.seq++;
             auto& r = ctx_->parts[p.res];
@@ -1459,6 +1459,19 @@ class DistEngine final : public EngineBase {
     // insert kernels: workgroups at most (each reserves frontier space with a same-line atomic,
     // ~11 ns apiece; 512 x 256 threads keep enough probes in flight)
     static constexpr u32 INSERT_GRID_MAX = 512;
+    // The insert grid for up to `recs` records: at most INSERT_GRID_MAX workgroups (each one's
+    // final flush is a same-line claims atomic, so inserts of a few million records keep few of
+    // them: 2pc N=9 at T = 2 / 8 is 15% / 6% slower on more), and for inserts of more than 8 M
+    // records up to insert_grid_big_ workgroups with four records per thread (insert_records
+    // batches the probes when every thread has at least two): 2pc N=11 at T = 8 inserts in 59.5
+    // instead of 76.6 ms per check (profiles/r02_insert_ab.txt).
+    u32 insert_grid(u64 recs) const {
+        const u64 small = std::max<u64>(1, blocks_for(recs, 256));
+        if (recs <= (8ull << 20)) return (u32)std::min<u64>(small, INSERT_GRID_MAX);
+        return (u32)std::min<u64>(insert_grid_big_, std::max<u64>(INSERT_GRID_MAX, blocks_for(recs, 1024)));
+    }
+    u32 insert_grid_big_ = std::getenv("SR_INSERT_GRID") && std::atoi(std::getenv("SR_INSERT_GRID")) > 0
+                               ? (u32)std::atoi(std::getenv("SR_INSERT_GRID")) : 4096u;
     u32 rstage_words_ = std::getenv("SR_RSTAGE_WORDS") ? (u32)std::atoi(std::getenv("SR_RSTAGE_WORDS")) : 1024;
     int route_ppw_env_ = std::getenv("SR_ROUTE_PPW_LOG2") ? std::atoi(std::getenv("SR_ROUTE_PPW_LOG2")) : -1;
     bool trace_ = std::getenv("SR_DIST_TRACE") != nullptr;

@@ -434,19 +434,42 @@ __device__ __forceinline__ void insert_records(const M& m, RecAt rec_at, u32 tot
         __syncthreads();
         if (threadIdx.x == 0) stage_n = 0;
     };
-    for (u64 g0 = (u64)blockIdx.x * blockDim.x; g0 < total; g0 += (u64)gridDim.x * blockDim.x) {
+    // IPB records per thread and round: their probes and claims are issued back to back before any
+    // is resolved (one round of barriers per IPB x blockDim records). Large inserts take 4 (one-word
+    // and two-word states); small ones, latency-bound, keep one record per thread.
+    auto rounds = [&](auto ipb_tag) {
+    constexpr int IPB = decltype(ipb_tag)::value;
+    const u64 per_round = (u64)gridDim.x * blockDim.x * IPB;
+    for (u64 g0 = (u64)blockIdx.x * blockDim.x * IPB; g0 < total; g0 += per_round) {
         __syncthreads();  // every thread read the last fill (and the stage was reset) before appends
-        const u64 g = g0 + threadIdx.x;
-        bool nw = false;
-        u64 ns[W];
-        if (g < total) {
-            const u64* rec = rec_at((u32)g);
+        u64 ns[IPB][W], cur[IPB];
+        ProbeKey pk[IPB];
+        bool ok[IPB];
 #pragma unroll
-            for (int x = 0; x < W; ++x) ns[x] = rec[x];
-            find_or_claim(t, probe_key(m, t, ns), &nw, &lc->err);
+        for (int j = 0; j < IPB; ++j) {
+            const u64 g = g0 + (u64)j * blockDim.x + threadIdx.x;
+            ok[j] = g < total;
+            pk[j] = ProbeKey{0, 0};
+            if (ok[j]) {
+                const u64* rec = rec_at((u32)g);
+#pragma unroll
+                for (int x = 0; x < W; ++x) ns[j][x] = rec[x];
+                pk[j] = probe_key(m, t, ns[j]);
+            }
         }
-        const u64 mask = __ballot(nw);
-        if (mask) {  // wave-aggregated: one LDS atomic, the overflow with one claims atomic per wave
+#pragma unroll
+        for (int j = 0; j < IPB; ++j) cur[j] = ok[j] ? t.keys[pk[j].home] : 0;
+        bool nws[IPB];  // every claim of the round before any append (their CASes overlap)
+#pragma unroll
+        for (int j = 0; j < IPB; ++j) {
+            nws[j] = false;
+            if (ok[j] && cur[j] != pk[j].tag) find_or_claim_from(t, pk[j], cur[j], &nws[j], &lc->err);
+        }
+#pragma unroll
+        for (int j = 0; j < IPB; ++j) {
+            const bool nw = nws[j];
+            const u64 mask = __ballot(nw);
+            if (!mask) continue;  // wave-aggregated: one LDS atomic, the overflow with one claims atomic per wave
             const u32 cnt = __popcll(mask), below = __popcll(mask & ((1ull << lane) - 1));
             const int leader = __builtin_ctzll(mask);
             u32 sb = 0;
@@ -456,26 +479,28 @@ __device__ __forceinline__ void insert_records(const M& m, RecAt rec_at, u32 tot
             u32 gb = 0;
             if (cnt > in_stage && lane == leader) gb = atomicAdd(&lc->claims, cnt - in_stage);
             gb = __shfl(gb, leader, 64);
-            if (nw) {
-                if (below < in_stage) {
+            if (!nw) continue;
+            if (below < in_stage) {
 #pragma unroll
-                    for (int x = 0; x < W; ++x) stage[(sb + below) * W + x] = ns[x];
+                for (int x = 0; x < W; ++x) stage[(sb + below) * W + x] = ns[j][x];
+            } else {
+                const u32 pos = gb + (below - in_stage);
+                if (pos < next_cap) {
+                    store_state<W>(next, pos, ns[j]);
+                    next_par[pos] = PAR_SEARCH;
                 } else {
-                    const u32 pos = gb + (below - in_stage);
-                    if (pos < next_cap) {
-                        store_state<W>(next, pos, ns);
-                        next_par[pos] = PAR_SEARCH;
-                    } else {
-                        atomicOr(&lc->err, (u32)ERR_FRONTIER_OVERFLOW);
-                    }
-                    eval_props(m, ns, pos, undiscovered, lc);
+                    atomicOr(&lc->err, (u32)ERR_FRONTIER_OVERFLOW);
                 }
+                eval_props(m, ns[j], pos, undiscovered, lc);
             }
         }
         __syncthreads();
         const u32 sn = min(stage_n, STAGE);  // the same value in every thread (no append until the next barrier)
         if (sn >= STAGE / 2) flush(sn);
     }
+    };
+    if (W <= 2 && total >= (u64)gridDim.x * blockDim.x * 2) rounds(std::integral_constant<int, 4>{});
+    else rounds(std::integral_constant<int, 1>{});
     __syncthreads();
     const u32 sn = min(stage_n, STAGE);
     if (sn) flush(sn);
