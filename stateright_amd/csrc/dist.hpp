@@ -1049,8 +1049,10 @@ class DistEngine final : public EngineBase {
         for (auto& p : parts_) {
             p.seq++;
             auto& r = ctx_->parts[p.res];
-            insert_recv_lag<M><<<ig, 256, 0, stream_>>>(m_, p.recv.p, S, (u32)C, p.id, T_, p.view(), p.arena.p, p.apar.p,
-                                                        p.arena_cap, p.lc, undiscovered, p.ctl, r.pub_dev[p.seq & 1], p.seq);
+            // four records per thread on the large grid (insert_grid), one otherwise
+            auto kern = ig > INSERT_GRID_MAX && W <= 2 ? insert_recv_lag<M, 4> : insert_recv_lag<M, 1>;
+            kern<<<ig, 256, 0, stream_>>>(m_, p.recv.p, S, (u32)C, p.id, T_, p.view(), p.arena.p, p.apar.p, p.arena_cap, p.lc,
+                                          undiscovered, p.ctl, r.pub_dev[p.seq & 1], p.seq);
             SR_HIP(hipGetLastError());
         }
         (void)level;
@@ -1463,7 +1465,7 @@ class DistEngine final : public EngineBase {
     // final flush is a same-line claims atomic, so inserts of a few million records keep few of
     // them: 2pc N=9 at T = 2 / 8 is 15% / 6% slower on more), and for inserts of more than 8 M
     // records up to insert_grid_big_ workgroups with four records per thread (insert_records
-    // batches the probes when every thread has at least two): 2pc N=11 at T = 8 inserts in 59.5
+    // batches the probes): 2pc N=11 at T = 8 inserts in 59.5
     // instead of 76.6 ms per check (profiles/r02_insert_ab.txt).
     u32 insert_grid(u64 recs) const {
         const u64 small = std::max<u64>(1, blocks_for(recs, 256));

@@ -409,7 +409,7 @@ __global__ void __launch_bounds__(256) expand_route(M m, u64* __restrict__ arena
 // reservation when half full and at the end. The old form reserved once per workgroup and round:
 // with up to 2048 workgroups that was ~2 K same-line atomics per level (~22 us at ~11 ns each,
 // scripts/microbench_atomics.hip), the whole duration of a typical insert launch.
-template <class M, class RecAt>
+template <int IPB, class M, class RecAt>
 __device__ __forceinline__ void insert_records(const M& m, RecAt rec_at, u32 total, const TableView& t, u64* next,
                                                u64* next_par, u32 next_cap, LevelCounters* lc, u32 undiscovered,
                                                u64* stage, u32 STAGE, u32& stage_n, u32& base) {
@@ -435,10 +435,9 @@ __device__ __forceinline__ void insert_records(const M& m, RecAt rec_at, u32 tot
         if (threadIdx.x == 0) stage_n = 0;
     };
     // IPB records per thread and round: their probes and claims are issued back to back before any
-    // is resolved (one round of barriers per IPB x blockDim records). Large inserts take 4 (one-word
-    // and two-word states); small ones, latency-bound, keep one record per thread.
-    auto rounds = [&](auto ipb_tag) {
-    constexpr int IPB = decltype(ipb_tag)::value;
+    // is resolved (one round of barriers per IPB x blockDim records). The host takes 4 for large
+    // inserts; small ones, latency-bound, keep one (a separate instantiation: the batched form's
+    // registers would lower the occupancy of the small ones).
     const u64 per_round = (u64)gridDim.x * blockDim.x * IPB;
     for (u64 g0 = (u64)blockIdx.x * blockDim.x * IPB; g0 < total; g0 += per_round) {
         __syncthreads();  // every thread read the last fill (and the stage was reset) before appends
@@ -498,9 +497,6 @@ __device__ __forceinline__ void insert_records(const M& m, RecAt rec_at, u32 tot
         const u32 sn = min(stage_n, STAGE);  // the same value in every thread (no append until the next barrier)
         if (sn >= STAGE / 2) flush(sn);
     }
-    };
-    if (W <= 2 && total >= (u64)gridDim.x * blockDim.x * 2) rounds(std::integral_constant<int, 4>{});
-    else rounds(std::integral_constant<int, 1>{});
     __syncthreads();
     const u32 sn = min(stage_n, STAGE);
     if (sn) flush(sn);
@@ -518,7 +514,7 @@ __global__ void __launch_bounds__(256) insert_recv(M m, const u64* __restrict__ 
     __shared__ u64 stage[STAGE * W];
     __shared__ u32 stage_n, base;
     if (threadIdx.x == 0) stage_n = 0;
-    insert_records(m, [&](u32 g) { return recv + (u64)g * REC; }, nrec, t, next, next_par, next_cap, lc, undiscovered,
+    insert_records<1>(m, [&](u32 g) { return recv + (u64)g * REC; }, nrec, t, next, next_par, next_cap, lc, undiscovered,
                    stage, STAGE, stage_n, base);
     if (!last_workgroup<M::NPROPS>(lc)) return;
     const u32 claims = __hip_atomic_load(&lc->claims, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -548,7 +544,7 @@ struct LagPub {
 // header (source q's row, word `me`). Grid-strided over the T x C slots (counts are known only on
 // the device). The last workgroup closes the level on the device (ctl: arena offset, frontier
 // size, discoveries) and publishes every row plus the close to pinned host memory.
-template <class M>
+template <class M, int IPB = 1>
 __global__ void __launch_bounds__(256) insert_recv_lag(M m, const u64* __restrict__ recv, u64 S, u32 C, u32 me,
                                                        u32 nparts, TableView t, u64* __restrict__ arena,
                                                        u64* __restrict__ apar, u64 arena_cap, LevelCounters* lc,
@@ -586,7 +582,7 @@ __global__ void __launch_bounds__(256) insert_recv_lag(M m, const u64* __restric
             if (q + step < nparts && qoff[q + step] <= g) q += step;
         return recv + (u64)q * S + DIST_HDR + (u64)(g - qoff[q]) * REC;
     };
-    insert_records(m, rec_at, total, t, next, next_par, next_cap, lc, undiscovered, stage, STAGE, stage_n, base);
+    insert_records<IPB>(m, rec_at, total, t, next, next_par, next_cap, lc, undiscovered, stage, STAGE, stage_n, base);
     if (!last_block(lc)) return;
     // every row (the bucket headers) to the host, then the close
     const u32 rw = nparts + 6 + M::NPROPS;
