@@ -1469,9 +1469,12 @@ class DistEngine final : public EngineBase {
     // instead of 76.6 ms per check (profiles/r02_insert_ab.txt).
     u32 insert_grid(u64 recs) const {
         const u64 small = std::max<u64>(1, blocks_for(recs, 256));
-        if (recs <= (8ull << 20)) return (u32)std::min<u64>(small, INSERT_GRID_MAX);
+        if (recs <= insert_batch_min_) return (u32)std::min<u64>(small, INSERT_GRID_MAX);
         return (u32)std::min<u64>(insert_grid_big_, std::max<u64>(INSERT_GRID_MAX, blocks_for(recs, 1024)));
     }
+    // planned records above which the batched insert runs (SR_INSERT_BATCH_MIN; tests force it low)
+    u64 insert_batch_min_ = std::getenv("SR_INSERT_BATCH_MIN") ? std::strtoull(std::getenv("SR_INSERT_BATCH_MIN"), nullptr, 10)
+                                                               : (8ull << 20);
     u32 insert_grid_big_ = std::getenv("SR_INSERT_GRID") && std::atoi(std::getenv("SR_INSERT_GRID")) > 0
                                ? (u32)std::atoi(std::getenv("SR_INSERT_GRID")) : 4096u;
     u32 rstage_words_ = std::getenv("SR_RSTAGE_WORDS") ? (u32)std::atoi(std::getenv("SR_RSTAGE_WORDS")) : 1024;

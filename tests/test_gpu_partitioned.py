@@ -48,6 +48,21 @@ def test_partitioned_counts_match_oracle(case, parts):
     assert sorted(c.discoveries()) == o.discovery_names()
 
 
+@pytest.mark.parametrize("parts", [2, 3, 8])
+@pytest.mark.parametrize("case", [(TWO_PHASE, [3]), (TWO_PHASE, [7]), (INCREMENT_LOCK, [5]), (INCREMENT_LOCK, [8])],
+                         ids=ids)
+def test_batched_insert_counts_match_oracle(case, parts, monkeypatch):
+    # SR_INSERT_BATCH_MIN=0: every level's insert takes the batched form (four records per thread,
+    # probes and claims issued back to back, the large grid), which otherwise runs only on inserts
+    # of more than 8 M planned records (2pc N=11); one- and two-word states.
+    monkeypatch.setenv("SR_INSERT_BATCH_MIN", "0")
+    model, params = case
+    o = oracle(model, params)
+    c = MODELS[model](params).checker().partitions(parts).spawn_bfs().join()
+    assert (c.unique_state_count(), c.state_count(), c.max_depth()) == (o.unique_state_count, o.state_count, o.max_depth)
+    assert sorted(c.discoveries()) == o.discovery_names()
+
+
 @pytest.mark.parametrize("parts", [2, 5])
 def test_partitioned_paths_replay(parts):
     c = sr.TwoPhaseSys(5).checker().partitions(parts).spawn_bfs().join()
