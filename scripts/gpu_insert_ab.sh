@@ -7,7 +7,7 @@ O=gpurun_out/insert_ab
 mkdir -p "$O"
 timeout -k 10 400 python -u -m pytest tests/test_gpu_partitioned.py tests/test_gpu_dist_ranks.py -x -q --timeout 300 --timeout-method thread > "$O/tests.log" 2>&1 || { tail -30 "$O/tests.log"; exit 1; }
 tail -1 "$O/tests.log"
-for N in 9 11; do for T in 8 2; do for v in head new; do for g in 4096; do
+for N in 9 11; do for T in 2 4; do for v in head new; do for g in 4096; do
   lib=stateright_amd/libstateright_gpu.so; [ $v = head ] && lib=build_ab/lib_head.so
   sc=4; [ $v = nosent ] && sc=0
   d=$O/${v}_g${g}_t${T}_n$N

@@ -228,22 +228,27 @@ __global__ void __launch_bounds__(256) expand_route(M m, u64* __restrict__ arena
                 }
                 own[j] = ok[j] ? owner_of(key[j], nparts) : my_part;
                 rem[j] = ok[j] && own[j] != my_part;
-                // Sent cache (small T): a lossy direct-mapped record of the fingerprints this
-                // partition already routed in this check. A hit is skipped: its owner received
-                // that state in this level's exchange or an earlier one, so it is visited. A miss,
-                // an eviction or a race only re-sends (the owner dedups).
-                if (sent && rem[j]) {
-                    u64* slot = &sent[key[j] & sent_mask];
-                    if (*slot == key[j]) {
-                        ++succ;
-                        ok[j] = rem[j] = false;
-                    } else {
-                        *slot = key[j];
-                    }
+            }
+            // One memory round trip per round: a local successor's visited-set probe and a remote
+            // one's sent-cache lookup are issued together (the lookup used to be resolved before
+            // the probes were issued: two dependent round trips per round).
+            // Sent cache (small T): a lossy direct-mapped record of the fingerprints this
+            // partition already routed in this check. A hit is skipped: its owner received that
+            // state in this level's exchange or an earlier one, so it is visited. A miss, an
+            // eviction or a race only re-sends (the owner dedups).
+#pragma unroll
+            for (int j = 0; j < PB; ++j)
+                cur[j] = !ok[j] ? 0 : !rem[j] ? probe_load<0>(&t.keys[pk[j].home]) : sent ? sent[key[j] & sent_mask] : 0;
+#pragma unroll
+            for (int j = 0; j < PB; ++j) {
+                if (!(sent && rem[j])) continue;
+                if (cur[j] == key[j]) {
+                    ++succ;
+                    ok[j] = rem[j] = false;
+                } else {
+                    sent[key[j] & sent_mask] = key[j];
                 }
             }
-#pragma unroll
-            for (int j = 0; j < PB; ++j) cur[j] = (ok[j] && !rem[j]) ? probe_load<0>(&t.keys[pk[j].home]) : 0;
             bool nw[PB];
 #pragma unroll
             for (int j = 0; j < PB; ++j) {
