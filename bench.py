@@ -15,7 +15,9 @@ WORLD_SIZE == N. The ranks partition ONE check: the visited set
 are hash-partitioned by fingerprint owner; after a few replicated head levels, every BFS level does
 ONE RCCL all-to-all of fixed-capacity buckets whose headers carry every rank's row.
 The workload stays 2pc N=9 at every N ("scaling": "strong"); value = unique states of the check /
-max-over-ranks time. `--mode replicas` instead runs an independent full check per GPU.
+max-over-ranks time. At N > 1 the line also carries `replicas`: the whole node's throughput on
+independent full checks (one per GPU and step, weak scaling). `--mode replicas` makes that the
+`value` instead.
 
 torch is never imported: the engine library (and with it /opt/rocm's HIP runtime and RCCL, the ones
 it was compiled against) is the only GPU runtime in the process; ranks bootstrap RCCL from the
@@ -215,6 +217,28 @@ def measure_config4(args, world, comm, dev, barrier):
             "restarts": st["restarts"], "head_levels": st["head_levels"], "records_routed": st["records_routed"]}
 
 
+def measure_replicas(args, world, comm, dev, make, expect_unique, label, barrier):
+    """N > 1, beside the partitioned `value`: the whole node's throughput on INDEPENDENT checks of
+    the same workload (every rank runs one full single-GPU check per step on its own GPU, no
+    collective inside a check: weak scaling)."""
+    def check():
+        c = make().checker().capacity_hint(expect_unique).device(dev).order("fast").spawn_bfs().join()
+        if c.unique_state_count() != expect_unique:
+            raise SystemExit(f"replicas: wrong unique count {c.unique_state_count()} != {expect_unique}")
+
+    check()  # warmup
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        check()
+    barrier()
+    el = comm.allreduce([time.perf_counter() - t0], "max")[0]
+    return {"workload": f"{label} spawn_bfs, one independent full check per GPU and step",
+            "parallelism": f"replicas{world} (no collective inside a check)", "scaling": "weak",
+            "n_gpus": world, "steps": args.steps, "ms_per_step": el / args.steps * 1e3,
+            "value": float(expect_unique) * world * args.steps / el, "unit": "unique states/s"}
+
+
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -353,6 +377,10 @@ def main():
     config4 = None
     if args.config4_steps > 0 and args.model == "2pc":
         config4 = measure_config4(args, world, comm, dev, barrier)
+    replicas = None
+    # (SR_BENCH_REPLICAS=1 runs it at N=1 in --mode rccl1 too: the rehearsal of this code path)
+    if partitioned and (world > 1 or os.environ.get("SR_BENCH_REPLICAS") == "1"):
+        replicas = measure_replicas(args, world, comm, dev, make, expect_unique, label, barrier)
 
     if rank != 0:
         comm.close()
@@ -462,6 +490,8 @@ def main():
     }
     if config4 is not None:
         res["config4"] = config4
+    if replicas is not None:
+        res["replicas"] = replicas
     if args.cpu_baseline and world == 1:
         try:
             res["cpu_baseline"] = cpu_baseline(args, n)
