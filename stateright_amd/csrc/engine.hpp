@@ -492,16 +492,11 @@ class Engine final : public EngineBase {
     // Device counters to their level-start values (once per run; afterwards the publishing
     // workgroup of each level resets them).
     void init_counters() {
-        std::vector<LevelCounters> z(1 + SLOTS);
-        std::memset(z.data(), 0, z.size() * sizeof(LevelCounters));
-        for (auto& c : z)
-            for (auto& d : c.disc) d = ~0u;
-        SR_HIP(hipMemcpyAsync(lc_d_, z.data(), sizeof(LevelCounters), hipMemcpyHostToDevice, stream_));
         if (!slots_.p) slots_.alloc(o_.device, (SLOTS * sizeof(LevelCounters) + 7) / 8);
-        SR_HIP(hipMemcpyAsync(slots_.p, z.data() + 1, SLOTS * sizeof(LevelCounters), hipMemcpyHostToDevice, stream_));
+        init_level_counters<<<1, 256, 0, stream_>>>(lc_d_, reinterpret_cast<LevelCounters*>(slots_.p), SLOTS);
+        SR_HIP(hipGetLastError());
         slot_k_ = 0;
         slot_published_ = true;
-        SR_HIP(hipStreamSynchronize(stream_));
     }
 
     // Per-level counter slots of the pipelined loop (SlotWork, kernels.hpp).
@@ -632,11 +627,16 @@ class Engine final : public EngineBase {
         SR_HIP(hipMemcpyAsync(arena_.p, rev.data(), rev.size() * sizeof(u64), hipMemcpyHostToDevice, stream_));
         SR_HIP(hipMemsetAsync(apar_.p, 0xff, (size_t)k * sizeof(u32), stream_));
         init_counters();
-        insert_roots<M><<<blocks_for(k, 64), 64, 0, stream_>>>(m_, view(), arena_.p, (u32)k, lc_d_);
-        eval_roots<M><<<blocks_for(k, 64), 64, 0, stream_>>>(m_, arena_.p, (u32)k, lc_d_, ((1u << M::NPROPS) - 1) & ~emask_);
         if (emask_) fill_u32<<<blocks_for(k, 64), 64, 0, stream_>>>(aeb_.p, (u32)k, emask_);  // bfs.rs:52-60
         u32 sq = next_seq();
-        publish_kernel<<<1, 64, 0, stream_>>>(lc_d_, hcd(sq), sq, 1, nullptr);
+        if (k <= 256) {
+            roots_fused<M><<<1, 256, 0, stream_>>>(m_, view(), arena_.p, (u32)k, lc_d_, ((1u << M::NPROPS) - 1) & ~emask_,
+                                                  hcd(sq), sq);
+        } else {
+            insert_roots<M><<<blocks_for(k, 64), 64, 0, stream_>>>(m_, view(), arena_.p, (u32)k, lc_d_);
+            eval_roots<M><<<blocks_for(k, 64), 64, 0, stream_>>>(m_, arena_.p, (u32)k, lc_d_, ((1u << M::NPROPS) - 1) & ~emask_);
+            publish_kernel<<<1, 64, 0, stream_>>>(lc_d_, hcd(sq), sq, 1, nullptr);
+        }
         SR_HIP(hipGetLastError());
         // FAST pipelined order: level 0 is enqueued before the host reads the roots' outcome (it is
         // ignored if the roots already discover every property)

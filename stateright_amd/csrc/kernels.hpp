@@ -1000,6 +1000,41 @@ __global__ void eval_roots(M m, const u64* frontier, u32 n, LevelCounters* lc, u
     }
 }
 
+// The roots in ONE workgroup (n <= blockDim.x init states): insert_roots + eval_roots + the
+// resetting publish, one launch instead of three at the start of every check.
+template <class M>
+__global__ void __launch_bounds__(256) roots_fused(M m, TableView t, const u64* states, u32 n, LevelCounters* lc,
+                                                   u32 undiscovered, HostCounters* h, u32 seq) {
+    const u32 r = threadIdx.x;
+    if (r < n) {
+        u64 s[M::W];
+        load_state<M::W>(states, r, s);
+        bool is_new;
+        const u64 slot = find_or_claim(t, probe_key(m, t, s), &is_new, &lc->err);
+        if (is_new) {
+            if (t.meta) t.meta[slot] = 0;  // level 0
+            atomicAdd(&lc->claims, 1u);
+        }
+        for (u32 und = undiscovered; und; und &= und - 1) {
+            const int p = __builtin_ctz(und);
+            if (m.discovers(p, s)) atomicMin(&lc->disc[p], r);
+        }
+    }
+    publish<M::NPROPS>(lc, h, seq, true, nullptr);
+}
+
+// Device counters and the pipelined loop's counter slots to their level-start values (no host
+// buffer, so no host wait at the start of a check).
+__global__ void init_level_counters(LevelCounters* lc, LevelCounters* slots, u32 nslots) {
+    constexpr u32 WORDS = sizeof(LevelCounters) / 4;
+    constexpr u32 D0 = offsetof(LevelCounters, disc) / 4;
+    for (u32 i = threadIdx.x; i < WORDS * (1 + nslots); i += blockDim.x) {
+        const u32 o = i % WORDS;
+        u32* w = i < WORDS ? reinterpret_cast<u32*>(lc) + i : reinterpret_cast<u32*>(slots) + (i - WORDS);
+        *w = o >= D0 && o < D0 + MAX_PROPS ? ~0u : 0u;
+    }
+}
+
 // Rehash into a table of twice the capacity (keys and meta move together).
 __global__ void rehash(TableView from, u64 from_cap, TableView to, LevelCounters* lc) {
     u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
