@@ -122,8 +122,6 @@ struct DeviceContext {
     HostMirror* hc_dev = nullptr;  // the same memory, device pointer
     uint32_t seq = 0;
     std::vector<hipEvent_t> events;
-    uint64_t* stage = nullptr;     // pinned: a few states read back at the end of a check
-    static constexpr size_t STAGE_WORDS = 1024;
 
     void init(int d) {
         dev = d;
@@ -135,7 +133,6 @@ struct DeviceContext {
         SR_HIP(hipHostMalloc(&hc, 2 * sizeof(HostMirror), hipHostMallocCoherent | hipHostMallocMapped));
         SR_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&hc_dev), hc, 0));
         std::memset(hc, 0, 2 * sizeof(HostMirror));
-        SR_HIP(hipHostMalloc(&stage, STAGE_WORDS * sizeof(uint64_t), hipHostMallocDefault));
     }
     hipEvent_t event(size_t i) {
         while (events.size() <= i) {

@@ -44,8 +44,7 @@ struct CtxLease {
 
 struct DiscoveryRec {
     bool found = false;
-    u32 level = 0, rank = 0;
-    u64 fp = 0;
+    u32 level = 0, rank = 0;  // the discovering state: rank in the visit order of its level
 };
 
 class EngineBase {
@@ -662,9 +661,6 @@ class Engine final : public EngineBase {
                     disc[p].found = true;
                     disc[p].level = level;
                     disc[p].rank = lc_.disc[p];
-                    u64 s[W];
-                    SR_HIP(hipMemcpy(s, arena_.p + (lstart_[level] + lc_.disc[p]) * W, W * sizeof(u64), hipMemcpyDeviceToHost));
-                    disc[p].fp = fingerprint<W>(s);
                 }
             // `eventually` properties: the first terminal candidate of each undiscovered one.
             const u32 eund = undiscovered & emask_;
@@ -753,9 +749,6 @@ class Engine final : public EngineBase {
                 disc[p].found = true;
                 disc[p].level = level;
                 disc[p].rank = evl[p] - 1;
-                u64 s[W];
-                SR_HIP(hipMemcpy(s, arena_.p + (lstart_[level] + evl[p] - 1) * W, W * sizeof(u64), hipMemcpyDeviceToHost));
-                disc[p].fp = fingerprint<W>(s);
                 undiscovered &= ~(1u << p);
             }
             state_count += lc_.successors;
@@ -821,7 +814,6 @@ class Engine final : public EngineBase {
             lvisited_.push_back(max_rank + 1);
             reference_done = true;
             SR_HIP(hipStreamSynchronize(stream_));  // the level-0 launch is not counted
-            fill_discovery_fps();
             return true;
         }
         // One level's outcome (counters c); false when the check is over.
@@ -888,7 +880,6 @@ class Engine final : public EngineBase {
             sq = spec ? sq_next : launch_sync(n, undiscovered);
         }
         (void)hipStreamSynchronize(stream_);
-        fill_discovery_fps();
         return order_dependent;
     }
 
@@ -949,24 +940,6 @@ class Engine final : public EngineBase {
         slot_published_ = false;
         ++slot_k_;
         return sq;
-    }
-
-    // disc[p].fp from the discovering state in the arena (after the level loop).
-    // The copies are queued together into pinned memory and waited for once (one round trip, not
-    // one blocking copy per property).
-    void fill_discovery_fps() {
-        static_assert((size_t)M::NPROPS * W <= Ctx::STAGE_WORDS, "discovery staging");
-        bool any = false;
-        for (int p = 0; p < M::NPROPS; ++p) {
-            if (!disc[p].found) continue;
-            SR_HIP(hipMemcpyAsync(ctx_->stage + (size_t)p * W, arena_.p + (lstart_[disc[p].level] + disc[p].rank) * W,
-                                  W * sizeof(u64), hipMemcpyDeviceToHost, stream_));
-            any = true;
-        }
-        if (!any) return;
-        SR_HIP(hipStreamSynchronize(stream_));
-        for (int p = 0; p < M::NPROPS; ++p)
-            if (disc[p].found) disc[p].fp = fingerprint<W>(ctx_->stage + (size_t)p * W);
     }
 
     // Smallest 1500-pop block boundary inside this level at which state_count >= target.
