@@ -475,11 +475,14 @@ class Engine final : public EngineBase {
             SR_HIP(hipMemcpyAsync(np.p, apar_.p, used * sizeof(u32), hipMemcpyDeviceToDevice, stream_));
             if (emask_) SR_HIP(hipMemcpyAsync(ne.p, aeb_.p, used * sizeof(u32), hipMemcpyDeviceToDevice, stream_));
         }
+        const bool had = arena_.p != nullptr;
         arena_.swap(na);
         apar_.swap(np);
         if (emask_) aeb_.swap(ne);
         arena_cap_ = cap;
-        SR_HIP(hipStreamSynchronize(stream_));
+        // the old buffers go back to the pool when na/np/ne leave scope: wait until no enqueued work
+        // reads them (a first allocation has none, and the start of a check does not wait here)
+        if (had) SR_HIP(hipStreamSynchronize(stream_));
     }
 
     void bind(Ctx* c) {
