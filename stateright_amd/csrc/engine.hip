@@ -64,9 +64,81 @@ using namespace sr;
 
 struct sr_bfs {
     std::unique_ptr<EngineBase> e;
-    std::thread th;
     bool joined = false;
 };
+
+namespace sr {
+// Driver threads of the checks, pooled: a check runs on an idle pooled thread, which after its
+// job spins for up to ~2 ms for the next one before it sleeps, so back-to-back checks pay neither
+// thread creation nor a wake-up (~20-50 us per check on a 2 ms check). Threads are never joined:
+// the pool lives for the process.
+class DriverPool {
+    struct Worker {
+        std::mutex mu;
+        std::condition_variable cv;
+        std::function<void()> job;
+        std::atomic<bool> has_job{false};
+        std::atomic<bool> idle{false};
+    };
+
+  public:
+    static DriverPool& get() {
+        static DriverPool* p = new DriverPool();  // never destroyed (its threads outlive main)
+        return *p;
+    }
+    void submit(std::function<void()> f) {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            for (Worker* w : workers_) {
+                bool t = true;
+                if (w->idle.compare_exchange_strong(t, false)) {
+                    hand(w, std::move(f));
+                    return;
+                }
+            }
+        }
+        Worker* w = new Worker();
+        hand(w, std::move(f));
+        std::thread([this, w] { loop(w); }).detach();
+        std::lock_guard<std::mutex> g(mu_);
+        workers_.push_back(w);
+    }
+
+  private:
+    static void hand(Worker* w, std::function<void()> f) {
+        {
+            std::lock_guard<std::mutex> g(w->mu);
+            w->job = std::move(f);
+            w->has_job.store(true, std::memory_order_release);
+        }
+        w->cv.notify_one();
+    }
+    static void loop(Worker* w) {
+        for (;;) {
+            const auto t0 = std::chrono::steady_clock::now();
+            for (u32 spin = 1; !w->has_job.load(std::memory_order_acquire); ++spin) {
+                _mm_pause();
+                if ((spin & 1023) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) {
+                    std::unique_lock<std::mutex> g(w->mu);
+                    w->cv.wait(g, [w] { return w->has_job.load(std::memory_order_acquire); });
+                    break;
+                }
+            }
+            std::function<void()> job;
+            {
+                std::lock_guard<std::mutex> g(w->mu);
+                job.swap(w->job);
+                w->has_job.store(false, std::memory_order_relaxed);
+            }
+            job();
+            job = nullptr;
+            w->idle.store(true, std::memory_order_release);
+        }
+    }
+    std::mutex mu_;
+    std::vector<Worker*> workers_;
+};
+}  // namespace sr
 
 namespace sr {
 // Host BFS over the reachable states of m: every slot self_loops() reports must be enabled and
@@ -160,7 +232,7 @@ static sr_bfs* start(std::unique_ptr<EngineBase> engine) {
     auto b = std::make_unique<sr_bfs>();
     b->e = std::move(engine);
     EngineBase* e = b->e.get();
-    b->th = std::thread([e] {
+    DriverPool::get().submit([e] {
         try {
             e->run();
         } catch (const Error& x) {
@@ -170,7 +242,7 @@ static sr_bfs* start(std::unique_ptr<EngineBase> engine) {
             e->status = SR_ERR_HIP;
             e->error = x.what();
         }
-        e->finished = true;
+        e->finished.store(true, std::memory_order_release);  // the last access to the engine
     });
     return b.release();
 }
@@ -259,17 +331,22 @@ int32_t sr_model_fingerprint(int32_t model, const int64_t* p, int32_t np, const 
     }
 }
 
+// Until the check's driver job has finished: a spin for the first ~20 ms (a short check's end is
+// seen at once), then polls every 50 us.
+static void wait_finished(sr_bfs* b) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (u32 spin = 1; !b->e->finished.load(std::memory_order_acquire); ++spin) {
+        if ((spin & 1023) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(20))
+            std::this_thread::sleep_for(std::chrono::microseconds(50));
+        else
+            _mm_pause();
+    }
+}
+
 int32_t sr_gpu_bfs_join(sr_bfs* b) {
     if (!b) return SR_ERR_ARG;
     if (!b->joined) {
-        // Spin briefly on the engine's finished flag before blocking in join: a check of a few ms
-        // otherwise pays the sleeping thread's wake-up (~20-40 us per check) after it ends.
-        const auto t0 = std::chrono::steady_clock::now();
-        for (u32 spin = 0; !b->e->finished.load(std::memory_order_acquire); ++spin) {
-            _mm_pause();
-            if ((spin & 1023) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(20)) break;
-        }
-        b->th.join();
+        wait_finished(b);
         b->joined = true;
     }
     if (b->e->status != SR_OK) set_error(b->e->error);
@@ -642,7 +719,7 @@ sr_bfs* sr_gpu_bfs_spawn_partitioned(sr_dist* comm, int32_t virtual_parts, int32
 
 void sr_gpu_bfs_free(sr_bfs* b) {
     if (!b) return;
-    if (!b->joined && b->th.joinable()) b->th.join();
+    if (!b->joined) wait_finished(b);  // the pooled driver thread must be done with the engine
     delete b;
 }
 
