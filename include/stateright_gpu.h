@@ -102,7 +102,8 @@ typedef struct sr_opts {
                                     representatives are not canonical (src/checker/dfs.rs:258-283) */
 } sr_opts;
 
-/* Timing/throughput counters of a finished run (sr_gpu_bfs_stats). */
+/* Timing/throughput counters of a finished run (sr_gpu_bfs_stats / sr_gpu_bfs_stats_sized).
+ * Layout of SR_PLUGIN_ABI 3 (the ABI-2 fields bucketed_levels and multi_levels are retired). */
 typedef struct sr_stats {
     double level_loop_sec;       /* first expand launch .. last level synchronised              */
     double total_sec;            /* spawn .. done, excluding one-time device allocation          */
@@ -118,12 +119,16 @@ typedef struct sr_stats {
     uint32_t order_used;         /* enum sr_order actually used for the reported counts          */
     uint32_t restarts;           /* capacity restarts of this check (larger buffers / synchronous) */
     uint32_t pipelined;          /* partitioned search: 1 = levels pipelined, no host wait inside */
-    uint64_t bucketed_levels;    /* levels expanded by the bucketed path (expand_bucket + bucket_insert) */
     uint64_t records_routed;     /* partitioned search: successor records sent between partitions (all ranks) */
     uint64_t head_levels;        /* partitioned search: levels run replicated before partitioning */
     uint64_t probes;             /* visited-set slots loaded by the expand kernels (first probe + linear steps) */
     uint64_t cas;                /* 64-bit atomicCAS claims attempted on the visited set */
-    uint64_t multi_levels;       /* reserved, always 0 (multi-level launches were measured and removed) */
+    uint64_t max_displacement;   /* longest linear-probe displacement (slots past home) of any entry
+                                    of the final visited set; measured with counters=1, else 0    */
+    uint32_t displacement_limit; /* probe limit of the final table's slot encoding (quotient mode:
+                                    2^dbits - 2; fingerprint mode: 65536)                          */
+    uint32_t table_doublings;    /* quotient mode: in-check doublings after a level overflowed the
+                                    probe limit (the level is finished on the larger table)       */
 } sr_stats;
 
 typedef struct sr_bfs sr_bfs;
@@ -146,6 +151,9 @@ uint64_t sr_gpu_bfs_state_count(const sr_bfs* bfs);
 uint64_t sr_gpu_bfs_unique_state_count(const sr_bfs* bfs);
 uint32_t sr_gpu_bfs_max_depth(const sr_bfs* bfs);
 int32_t sr_gpu_bfs_stats(const sr_bfs* bfs, sr_stats* out);
+/* The same for a caller whose sr_stats mirror has `size` bytes (a binding written against another
+ * header): copies at most `size` bytes; returns the engine's sizeof(sr_stats). */
+int32_t sr_gpu_bfs_stats_sized(const sr_bfs* bfs, sr_stats* out, uint32_t size);
 /* profile=1: HIP-event duration (ms) of every expand launch in launch order and the frontier size
  * it expanded (0 if unknown); returns the number of launches (FAST pipelined order: launch i
  * expands level i, a last launch past the end expands nothing). */
@@ -259,7 +267,7 @@ sr_bfs* sr_gpu_bfs_spawn_partitioned(sr_dist* comm, int32_t virtual_partitions, 
  * include/stateright_gpu_model.hpp; the macro SR_GPU_PLUGIN(name, Model, make) there exports
  * `const sr_plugin* sr_plugin_<name>(void)`. The engine library then runs it like a registered
  * model. The plugin must be built from the same headers (abi). */
-#define SR_PLUGIN_ABI 2
+#define SR_PLUGIN_ABI 3
 typedef struct sr_plugin {
     uint32_t abi;         /* SR_PLUGIN_ABI of the headers the plugin was built with */
     uint32_t opts_size;   /* sizeof(sr_opts) in that build */

@@ -14,7 +14,11 @@
  *   SR_HD bool discovers(int p, const u64* s);           always: !condition; sometimes/eventually: condition
  *   host: init_states(u64*) -> count, expectation(p), prop_name(p), describe_width(), describe(s, i64*),
  *         action_id(s, a), action_name(id), action_id_bound()
- *   optional: undescribe(const i64*, u64*)    (sr_plugin.fingerprint)
+ *         init_states writes at most 256 states (sr::MAX_INIT_STATES) unless the model reports its
+ *         count with init_count(); the engine checks the count once at spawn (SR_ERR_ARG)
+ *   optional: init_count()                    the number of init states (any count; the engine sizes
+ *                                             its host buffers from it)
+ *             undescribe(const i64*, u64*)    (sr_plugin.fingerprint)
  *             emask()                         (the mask of `eventually` properties)
  *             qkey_bits(), SR_HD qkey(s)      (exact quotient visited set for multi-word states)
  *             SR_HD self_loops(s, enabled, out)   out = enabled slots whose next_state is s itself:

@@ -53,12 +53,13 @@ class sr_stats(ctypes.Structure):
         ("order_used", ctypes.c_uint32),
         ("restarts", ctypes.c_uint32),
         ("pipelined", ctypes.c_uint32),
-        ("bucketed_levels", ctypes.c_uint64),
         ("records_routed", ctypes.c_uint64),
         ("head_levels", ctypes.c_uint64),
         ("probes", ctypes.c_uint64),
         ("cas", ctypes.c_uint64),
-        ("multi_levels", ctypes.c_uint64),
+        ("max_displacement", ctypes.c_uint64),
+        ("displacement_limit", ctypes.c_uint32),
+        ("table_doublings", ctypes.c_uint32),
     ]
 
     def as_dict(self):
@@ -81,6 +82,7 @@ SIGNATURES = [
     ("sr_gpu_bfs_unique_state_count", ctypes.c_uint64, [_P]),
     ("sr_gpu_bfs_max_depth", ctypes.c_uint32, [_P]),
     ("sr_gpu_bfs_stats", ctypes.c_int32, [_P, ctypes.POINTER(sr_stats)]),
+    ("sr_gpu_bfs_stats_sized", ctypes.c_int32, [_P, ctypes.POINTER(sr_stats), ctypes.c_uint32]),
     ("sr_gpu_bfs_launch_counters", ctypes.c_int64, [_P, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
                                                     ctypes.c_int64]),
     ("sr_gpu_bfs_launch_profile", ctypes.c_int64, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64),

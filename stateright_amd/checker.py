@@ -390,18 +390,22 @@ class GpuBfsChecker:
         n = len(fingerprints)
         fps = (ctypes.c_uint64 * max(1, n))(*fingerprints)
         width = self._lib.sr_gpu_bfs_describe_width(self._h)
-        cap = 4096
-        acts = (ctypes.c_int64 * cap)()
-        has = (ctypes.c_int32 * cap)()
-        fpo = (ctypes.c_uint64 * cap)()
-        st = (ctypes.c_int64 * (cap * max(1, width)))()
-        v = self._lib.sr_gpu_bfs_explore(self._h, fps, n, acts, has, fpo, st, cap)
-        if v == -1:
-            return None
-        if v < 0:
-            raise CheckerError("sr_gpu_bfs_explore", v)
+        cap = 64
+        while True:  # re-called with room for every view when the first buffer is too small
+            acts = (ctypes.c_int64 * cap)()
+            has = (ctypes.c_int32 * cap)()
+            fpo = (ctypes.c_uint64 * cap)()
+            st = (ctypes.c_int64 * (cap * max(1, width)))()
+            v = self._lib.sr_gpu_bfs_explore(self._h, fps, n, acts, has, fpo, st, cap)
+            if v == -1:
+                return None
+            if v < 0:
+                raise CheckerError("sr_gpu_bfs_explore", v)
+            if v <= cap:
+                break
+            cap = v
         out = []
-        for i in range(min(v, cap)):
+        for i in range(v):
             name = None if acts[i] < 0 else self.action_name(acts[i])
             if has[i]:
                 out.append((name, tuple(st[i * width:(i + 1) * width]), fpo[i]))
@@ -433,7 +437,7 @@ class GpuBfsChecker:
 
     def stats(self):
         s = N.sr_stats()
-        self._lib.sr_gpu_bfs_stats(self._h, ctypes.byref(s))
+        self._lib.sr_gpu_bfs_stats_sized(self._h, ctypes.byref(s), ctypes.sizeof(s))
         return s.as_dict()
 
     def launch_profile(self):

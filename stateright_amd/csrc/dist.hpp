@@ -157,10 +157,18 @@ struct LocalGroup {
     std::condition_variable cv;
     int arrived = 0;
     u64 generation = 0;
+    bool failed = false;  // a rank timed out: every later call fails at once (the group is poisoned)
+    // How long a rank waits for the others (SR_LOCAL_BARRIER_SEC, default 300 s: a rank may be busy
+    // with a long host-side walk or rehash while the others wait).
+    const std::chrono::seconds timeout{std::getenv("SR_LOCAL_BARRIER_SEC") ? std::max(1, std::atoi(std::getenv("SR_LOCAL_BARRIER_SEC")))
+                                                                          : 300};
 
     // All ranks arrive; false on timeout (a rank issued a different collective sequence, or failed).
+    // A timed-out rank takes its arrival back and marks the group failed, so that no later call can
+    // complete with a stale count.
     bool barrier() {
         std::unique_lock<std::mutex> g(mu);
+        if (failed) return false;
         const u64 gen = generation;
         if (++arrived == world) {
             arrived = 0;
@@ -168,7 +176,14 @@ struct LocalGroup {
             cv.notify_all();
             return true;
         }
-        return cv.wait_for(g, std::chrono::seconds(60), [&] { return generation != gen; });
+        cv.wait_for(g, timeout, [&] { return generation != gen || failed; });
+        if (generation != gen) return true;
+        if (!failed) {
+            --arrived;
+            failed = true;
+            cv.notify_all();
+        }
+        return false;
     }
 };
 
@@ -367,6 +382,7 @@ class DistEngine final : public EngineBase {
     DistEngine(M m, const sr_opts& o, Comm* comm, int virtual_parts)
         : m_(m), o_(o), comm_(comm), D_((u32)m.max_out_degree()) {
         disc.resize(M::NPROPS);
+        (void)init_states_of(m_);  // a model with more init states than it declares fails at spawn
         if (model_emask(m))
             throw Error(SR_ERR_UNSUPPORTED, "partitioned search: `eventually` properties need the FIFO order of one GPU");
         T_ = comm_ ? (u32)comm_->world : (u32)std::max(1, virtual_parts);
@@ -398,17 +414,14 @@ class DistEngine final : public EngineBase {
     int width() const override { return m_.describe_width(); }
     std::string action_name(i64 id) const override { return m_.action_name(id); }
     i64 action_id_bound() const override { return m_.action_id_bound(); }
-    int init_count() const override {
-        u64 inits[8 * W];
-        return m_.init_states(inits);
-    }
+    int init_count() const override { return (int)(init_states_of(base_model(m_)).size() / W); }
     int replay(int init, const i64* ids, int n, std::vector<i64>& states, std::vector<int>& conds,
                std::vector<int>* all_conds, int* terminal) const override {
-        return replay_model(m_, init, ids, n, states, conds, all_conds, terminal);
+        return replay_model(base_model(m_), init, ids, n, states, conds, all_conds, terminal);
     }
     int explore(const u64* fps, int n, std::vector<i64>& action, std::vector<int>& has, std::vector<u64>& fp,
                 std::vector<i64>& states) const override {
-        return explore_model(m_, fps, n, action, has, fp, states);
+        return explore_model(base_model(m_), fps, n, action, has, fp, states);
     }
     std::vector<i64> visits() const override { return {}; }
     int partitions() const { return (int)T_; }
@@ -504,8 +517,7 @@ class DistEngine final : public EngineBase {
         out.clear();
         std::vector<u64> st;
         if (!path_states(p, st)) return 0;
-        for (size_t i = 0; i < st.size() / W; ++i) out.push_back(fingerprint<W>(&st[i * W]));
-        return (int)out.size();
+        return fingerprint_chain(m_, st, out);
     }
     int path(int p, std::vector<i64>& actions, std::vector<i64>& states) override {
         std::vector<u64> st;
@@ -594,7 +606,7 @@ class DistEngine final : public EngineBase {
         p.cap *= 2;
         p.keys.alloc(o_.device, p.cap);
         SR_HIP(hipMemsetAsync(p.keys.p, 0, p.cap * 8, stream_));
-        rehash<<<blocks_for(old_cap, 256), 256, 0, stream_>>>(make_table_view(m_, ok.p, nullptr, old_cap), old_cap, p.view(), p.lc);
+        rehash<<<blocks_for(old_cap, 256), 256, 0, stream_>>>(make_table_view(m_, ok.p, nullptr, old_cap), old_cap, p.view(), &p.lc->err);
         SR_HIP(hipGetLastError());
         SR_HIP(hipStreamSynchronize(stream_));
         stats.rehashes++;
@@ -629,8 +641,8 @@ class DistEngine final : public EngineBase {
         const u64 per_part = hint / T_ + 1;
 
         // ---- partitions: visited sets, arenas, level 0 ----
-        u64 inits[8 * W];
-        int k = m_.init_states(inits);
+        const std::vector<u64> inits = init_states_of(m_);
+        const int k = (int)(inits.size() / W);
         std::vector<u64> rev(k * W);
         for (int i = 0; i < k; ++i) std::copy(&inits[i * W], &inits[i * W] + W, &rev[(k - 1 - i) * W]);
         DBuf<u64> dinit;
@@ -643,7 +655,7 @@ class DistEngine final : public EngineBase {
         if (comm_) rows_mine_.alloc(o_.device, RW);
         for (auto& p : parts_) {
             u64 cap = std::max<u64>((u64)(1u << 16) * grow_factor_, min_table_cap(m_));
-            while ((double)cap * 0.5 < (double)per_part * grow_factor_) cap <<= 1;
+            while ((double)cap * std::min(0.5, lmax(cap)) < (double)per_part * grow_factor_) cap <<= 1;
             p.uniq = 0;
             p.cap = cap;
             p.keys.alloc(o_.device, cap);
@@ -718,7 +730,7 @@ class DistEngine final : public EngineBase {
                 // most successors are duplicates)
                 const double g = std::min((double)d_eff, std::max(1.0, growth) * 1.5);
                 const u64 expect_new = (u64)((double)glob_est * g / (double)T_) + 1024;
-                while ((double)(p.uniq + p.n_hi + expect_new) > 0.75 * (double)p.cap) grow_table(p);
+                while ((double)(p.uniq + p.n_hi + expect_new) > lmax(p.cap) * (double)p.cap) grow_table(p);
                 const u64 nb = p.lstart.back();  // arena offset of the frontier being expanded
                 const u64 n_plan = pessimistic_ ? p.n_hi : std::min(p.n_hi, p.n_est * 2 + 1024);
                 // records per destination: last level's records per parent (measured), with slack
@@ -869,6 +881,7 @@ class DistEngine final : public EngineBase {
         stats.level_loop_sec = secs(t_loop, t_end);
         stats.total_sec = secs(t_start, t_end);
         stats.table_capacity = parts_[0].cap * T_;
+        stats.displacement_limit = parts_[0].view().plimit;
     }
 
     // ---- pipelined level loop ------------------------------------------------------------------
@@ -892,7 +905,7 @@ class DistEngine final : public EngineBase {
         Part& p0 = parts_[0];
         const u64 cap_states = head_max_ * (u64)(D_ + 4) * 2 + 4096;
         u64 hcap = std::max<u64>(1u << 12, min_table_cap(m_));
-        while ((double)hcap * 0.5 < (double)cap_states) hcap <<= 1;
+        while ((double)hcap * std::min(0.5, lmax(hcap)) < (double)cap_states) hcap <<= 1;
         if (hkeys_.n < hcap) hkeys_.alloc(o_.device, hcap);
         if (harena_.n < cap_states * W) {
             harena_.alloc(o_.device, cap_states * W);
@@ -984,7 +997,7 @@ class DistEngine final : public EngineBase {
         for (auto& p : parts_) {
             // sized from the global head (the same on every rank): a rank-local overflow here would
             // leave the other ranks waiting in the first all-to-all
-            while ((double)total > 0.5 * (double)p.cap) grow_table(p);
+            while ((double)total > std::min(0.5, lmax(p.cap)) * (double)p.cap) grow_table(p);
             ensure_arena(p, n + n / 4 + 4096, 0);
             SR_HIP(hipMemsetAsync(cnt.p, 0, 8, stream_));
             take_owned<M><<<blocks_for(total, 256), 256, 0, stream_>>>(m_, harena_.p, (u32)total, (u32)hlstart_[level], p.id, T_,
@@ -1009,6 +1022,12 @@ class DistEngine final : public EngineBase {
     }
 
     u64 lag_S(u64 C) const { return DIST_HDR + C * REC; }
+
+    // Growth threshold of a partition's visited set of `cap` slots: 0.75 load, lower for a
+    // quotient-mode table whose probe limit would be reached sooner (kernels.hpp max_load_for).
+    double lmax(u64 cap) const {
+        return max_load_for(make_table_view(m_, nullptr, nullptr, cap, true).plimit, (double)cap, 0.75);
+    }
 
     void lag_enqueue(u32 level, u64 C, u32 undiscovered, const std::vector<u64>& n_plan) {
         const u64 S = lag_S(C);
@@ -1131,7 +1150,7 @@ class DistEngine final : public EngineBase {
                 const u64 fr = ahead == 2 ? (u64)((double)c1 * gc) + 1024 : c1;
                 const u64 nw = (u64)((double)fr * gc) + 1024;
                 const u64 before = ahead == 2 ? hi : 0;  // a frontier between the rows and the target
-                while ((double)(p.uniq + before + hi + fr + nw) > 0.75 * (double)p.cap) grow_table(p);
+                while ((double)(p.uniq + before + hi + fr + nw) > lmax(p.cap) * (double)p.cap) grow_table(p);
                 const u64 need = p.lstart.back() + hi + (ahead == 2 ? fr : 0) + nw + 1024;
                 if (p.arena_cap < need) ensure_arena(p, std::max<u64>(need + need / 4, p.arena_cap * 2), p.arena_cap);
                 n_plan[p.id] = fr;

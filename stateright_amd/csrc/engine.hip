@@ -99,7 +99,7 @@ class DriverPool {
         }
         Worker* w = new Worker();
         hand(w, std::move(f));
-        std::thread([this, w] { loop(w); }).detach();
+        std::thread([w] { loop(w); }).detach();
         std::lock_guard<std::mutex> g(mu_);
         workers_.push_back(w);
     }
@@ -154,8 +154,8 @@ static bool check_self_loops(const M& m, std::string& why) {
         }
     };
     std::unordered_set<std::vector<u64>, H> seen;
-    std::vector<u64> inits(256 * W);
-    const int k = m.init_states(inits.data());
+    const std::vector<u64> inits = init_states_of(m);
+    const int k = (int)(inits.size() / W);
     std::vector<std::vector<u64>> queue;
     for (int i = 0; i < k; ++i) {
         std::vector<u64> st(inits.begin() + i * W, inits.begin() + (i + 1) * W);
@@ -363,6 +363,12 @@ int32_t sr_gpu_bfs_stats(const sr_bfs* b, sr_stats* out) {
     if (!b || !out) return SR_ERR_ARG;
     *out = b->e->stats;
     return SR_OK;
+}
+
+int32_t sr_gpu_bfs_stats_sized(const sr_bfs* b, sr_stats* out, uint32_t size) {
+    if (!b || (!out && size)) return SR_ERR_ARG;
+    if (out) std::memcpy(out, &b->e->stats, std::min<size_t>(size, sizeof(sr_stats)));
+    return (int32_t)sizeof(sr_stats);
 }
 
 int64_t sr_gpu_bfs_launch_profile(const sr_bfs* b, double* kernel_ms, uint64_t* frontier, int64_t cap) {

@@ -87,12 +87,28 @@ class EngineBase {
     std::vector<u64> launch_cas;      // FAST loop with sr_opts.counters; 0 otherwise)
 };
 
+// The model's init states (k * W words), in a buffer sized by init_capacity; a model that reports
+// more states than fit is refused (every host-side caller goes through here, and the engines call
+// it once when they are created, so a bad plugin fails at spawn).
+template <class M>
+std::vector<u64> init_states_of(const M& m) {
+    const int cap = init_capacity(m);
+    std::vector<u64> v((size_t)cap * M::W + M::W);  // one spare state: a model off by one is caught, not silent
+    const int k = m.init_states(v.data());
+    if (k < 0 || k > cap)
+        throw Error(SR_ERR_ARG, "init_states returned " + std::to_string(k) + " states; at most " + std::to_string(cap) +
+                                    " fit (a model with more than " + std::to_string(MAX_INIT_STATES) +
+                                    " init states must report init_count())");
+    v.resize((size_t)k * M::W);
+    return v;
+}
+
 template <class M>
 int replay_model(const M& m, int init, const i64* ids, int n, std::vector<i64>& states, std::vector<int>& conds,
                  std::vector<int>* all_conds, int* terminal) {
     constexpr int W = M::W;
-    u64 inits[8 * W];
-    const int k = m.init_states(inits);
+    const std::vector<u64> inits = init_states_of(m);
+    const int k = (int)(inits.size() / W);
     if (init < 0 || init >= k) return -1;
     const int wd = m.describe_width();
     std::vector<u64> cur(&inits[init * W], &inits[init * W] + W);
@@ -154,8 +170,8 @@ int explore_model(const M& m, const u64* fps, int n, std::vector<i64>& action, s
         states.resize(o + wd, 0);
         if (s) m.describe(s, &states[o]);
     };
-    u64 inits[8 * W];
-    const int k = m.init_states(inits);
+    const std::vector<u64> inits = init_states_of(m);
+    const int k = (int)(inits.size() / W);
     if (n == 0) {
         for (int i = 0; i < k; ++i) emit(-1, &inits[i * W]);
         return k;
@@ -193,22 +209,33 @@ int explore_model(const M& m, const u64* fps, int n, std::vector<i64>& action, s
     return views;
 }
 
+// The model a host-side walk runs on: the original model under the canonical symmetry reduction
+// (Canon<M> steps through orbit representatives; replay, the Explorer and discovery paths speak of
+// concrete states of the original model), the model itself otherwise.
+template <class M>
+decltype(auto) base_model(const M& m) {
+    if constexpr (is_canon<M>::value) return m.base();
+    else return (m);
+}
+
 // `Path::from_fingerprints` (src/checker/path.rs:20-86) over the states of a BFS-tree path (W words
 // each): from the init state, each step is the FIRST action in `actions()` order whose successor is
 // the next state. Under the canonical symmetry reduction (Canon<M>) the tree holds orbit
 // representatives; the path is then made concrete in the original model: an init state whose
 // representative is the first state, and at each step the first action whose successor's
-// representative is the next one. Returns the number of actions.
+// representative is the next one. Returns the number of actions; `raw` (optional) receives the
+// concrete states (W words each), whose fingerprints are the discovery's chain.
 template <class M>
-int concrete_path(const M& m, const std::vector<u64>& st, std::vector<i64>& actions, std::vector<i64>& states) {
+int concrete_path(const M& m, const std::vector<u64>& st, std::vector<i64>& actions, std::vector<i64>& states,
+                  std::vector<u64>* raw = nullptr) {
     constexpr int W = M::W;
     const size_t len = st.size() / W;
     if (!len) return -1;
     const int wd = m.describe_width();
     std::vector<u64> cur(st.begin(), st.begin() + W);
     if constexpr (is_canon<M>::value) {
-        u64 inits[8 * W];
-        const int k = m.base().init_states(inits);
+        const std::vector<u64> inits = init_states_of(m.base());
+        const int k = (int)(inits.size() / W);
         cur.clear();
         for (int i = 0; i < k && cur.empty(); ++i) {
             u64 c[W];
@@ -221,6 +248,7 @@ int concrete_path(const M& m, const std::vector<u64>& st, std::vector<i64>& acti
         const size_t o = states.size();
         states.resize(o + wd);
         m.describe(s, &states[o]);
+        if (raw) raw->insert(raw->end(), s, s + W);
     };
     for (size_t i = 1; i < len; ++i) {
         const u64* target = &st[i * W];
@@ -248,6 +276,24 @@ int concrete_path(const M& m, const std::vector<u64>& st, std::vector<i64>& acti
     return (int)actions.size();
 }
 
+// `reconstruct_path`'s fingerprint chain (src/checker/bfs.rs:314-342) of a BFS-tree path: the
+// fingerprints of its states, or under Canon<M> of the concrete states of the original model that
+// concrete_path walks (the ones `discovery_path`, `replay` and the Explorer speak of).
+template <class M>
+int fingerprint_chain(const M& m, const std::vector<u64>& st, std::vector<u64>& out) {
+    constexpr int W = M::W;
+    out.clear();
+    std::vector<u64> raw;
+    if constexpr (is_canon<M>::value) {
+        std::vector<i64> actions, described;
+        concrete_path(m, st, actions, described, &raw);
+    } else {
+        raw = st;
+    }
+    for (size_t i = 0; i < raw.size() / W; ++i) out.push_back(fingerprint<W>(&raw[i * W]));
+    return (int)out.size();
+}
+
 template <class M>
 class Engine final : public EngineBase {
     static constexpr int W = M::W;
@@ -256,6 +302,7 @@ class Engine final : public EngineBase {
     Engine(M m, const sr_opts& o)
         : m_(m), o_(o), A_((u32)m.max_actions()), D_((u32)m.max_out_degree()), emask_(model_emask(m)) {
         disc.resize(M::NPROPS);
+        (void)init_states_of(m_);  // a model with more init states than it declares fails at spawn
         // Internal tuning knobs (not part of the ABI): successors per lane per probe round and
         // the visited-set load factor the capacity hint is sized for.
         if (const char* e = std::getenv("SR_PROBE_BATCH")) probe_batch_ = std::atoi(e);
@@ -323,8 +370,7 @@ class Engine final : public EngineBase {
         SR_HIP(hipSetDevice(o_.device));
         std::vector<u64> st;
         tree_path(disc[p].level, disc[p].rank, st);
-        for (size_t i = 0; i < st.size() / W; ++i) out.push_back(fingerprint<W>(&st[i * W]));
-        return (int)out.size();
+        return fingerprint_chain(m_, st, out);
     }
 
     // States (W words each) from the init state down to (level, rank).
@@ -355,17 +401,15 @@ class Engine final : public EngineBase {
     }
 
     i64 action_id_bound() const override { return m_.action_id_bound(); }
-    int init_count() const override {
-        u64 inits[8 * W];
-        return m_.init_states(inits);
-    }
+    int init_count() const override { return (int)(init_states_of(base_model(m_)).size() / W); }
+    // replay and the Explorer walk concrete states of the original model (under Canon<M> too)
     int replay(int init, const i64* ids, int n, std::vector<i64>& states, std::vector<int>& conds,
                std::vector<int>* all_conds, int* terminal) const override {
-        return replay_model(m_, init, ids, n, states, conds, all_conds, terminal);
+        return replay_model(base_model(m_), init, ids, n, states, conds, all_conds, terminal);
     }
     int explore(const u64* fps, int n, std::vector<i64>& action, std::vector<int>& has, std::vector<u64>& fp,
                 std::vector<i64>& states) const override {
-        return explore_model(m_, fps, n, action, has, fp, states);
+        return explore_model(base_model(m_), fps, n, action, has, fp, states);
     }
 
     // The visitor's paths (src/checker/bfs.rs:187-189 builds `Path::from_fingerprints` of every
@@ -433,6 +477,7 @@ class Engine final : public EngineBase {
 
     void alloc_table(u64 cap) {
         cap_ = cap;
+        lmax_ = max_load(cap);
         keys_.alloc(o_.device, cap);
         SR_HIP(hipMemsetAsync(keys_.p, 0, cap * sizeof(u64), stream_));
         if (fifo_) {
@@ -441,23 +486,59 @@ class Engine final : public EngineBase {
         }
     }
 
-    // Doubles the visited set. In FIFO order the level's candidate slots (cand) are remapped to
-    // the new table, since the rehash moves every entry.
+    // Doubles the visited set (quotient mode: one more displacement bit per slot, so twice the
+    // probe limit). If an entry does not fit the new table's probe limit, the rehash starts over
+    // from the old table into one twice as large again. In FIFO order the level's candidate slots
+    // (cand) are remapped to the new table, since the rehash moves every entry.
     void grow_table(u32* cand = nullptr, u64 cand_n = 0) {
         DBuf<u64> ok, om;
         ok.swap(keys_);
         if (fifo_) om.swap(meta_);
-        TableView from = make_table_view(m_, ok.p, fifo_ ? om.p : nullptr, cap_);
-        u64 old_cap = cap_;
-        alloc_table(cap_ * 2);
-        rehash<<<blocks_for(old_cap, 256), 256, 0, stream_>>>(from, old_cap, view(), lc_d_);
-        SR_HIP(hipGetLastError());
+        const TableView from = make_table_view(m_, ok.p, fifo_ ? om.p : nullptr, cap_);
+        const u64 old_cap = cap_;
+        if (!aux_.p) aux_.alloc(o_.device, 2);
+        for (u64 f = 2;; f *= 2) {
+            alloc_table(old_cap * f);
+            SR_HIP(hipMemsetAsync(aux_.p, 0, sizeof(u32), stream_));
+            rehash<<<blocks_for(old_cap, 256), 256, 0, stream_>>>(from, old_cap, view(), aux_.p);
+            SR_HIP(hipGetLastError());
+            u32 err = 0;
+            SR_HIP(hipMemcpyAsync(&err, aux_.p, sizeof(u32), hipMemcpyDeviceToHost, stream_));
+            SR_HIP(hipStreamSynchronize(stream_));
+            if (!err) break;
+            if (f >= 64) throw Error(SR_ERR_CAPACITY, "rehash: probe limit exceeded at 64x the capacity");
+        }
         if (cand && cand_n) {
             remap_slots<<<blocks_for(cand_n, 256), 256, 0, stream_>>>(cand, cand_n, from, view());
             SR_HIP(hipGetLastError());
         }
         SR_HIP(hipStreamSynchronize(stream_));
         stats.rehashes++;
+    }
+
+    // The growth threshold of the visited set: 0.8 load, or lower for a quotient-mode table whose
+    // probe limit (set by its displacement bits) would otherwise be reached by the longest
+    // linear-probe run to be expected at that load (kernels.hpp max_load_for).
+    double max_load(u64 cap) const {
+        const TableView v = make_table_view(m_, nullptr, nullptr, cap, true);
+        return max_load_for(v.plimit, (double)cap, 0.8);
+    }
+
+    // sr_stats.max_displacement / displacement_limit of the final table (the scan runs only in a
+    // measurement pass, sr_opts.counters: it reads the whole table).
+    void displacement_stats() {
+        const TableView v = view();
+        stats.displacement_limit = v.plimit;
+        if (!o_.counters || !cap_) return;
+        if (!aux_.p) aux_.alloc(o_.device, 2);
+        SR_HIP(hipMemsetAsync(aux_.p + 1, 0, sizeof(u32), stream_));
+        const u32 grid = (u32)std::min<u64>(blocks_for(cap_, 256), 8192);
+        table_max_disp<<<grid, 256, 0, stream_>>>(v, cap_, aux_.p + 1);
+        SR_HIP(hipGetLastError());
+        u32 d = 0;
+        SR_HIP(hipMemcpyAsync(&d, aux_.p + 1, sizeof(u32), hipMemcpyDeviceToHost, stream_));
+        SR_HIP(hipStreamSynchronize(stream_));
+        stats.max_displacement = d;
     }
 
     // The BFS-tree arena holds every level's states (visit order) and their parent ranks; grows
@@ -535,7 +616,9 @@ class Engine final : public EngineBase {
     // Waits until the launch tagged `seq` has published its counters to pinned host memory: a
     // spin on one host word (no stream synchronisation, no copy), with a periodic stream query
     // so that a failed launch cannot hang the host.
-    void wait_publish(u32 seq) {
+    // recoverable: a level that overflowed the visited set's probe limit (and nothing else) returns
+    // false instead of throwing; the caller doubles the table and repairs the level.
+    bool wait_publish(u32 seq, bool recoverable = false) {
         volatile u32* flag = &ctx_->hc[seq & 1].seq;
         for (u64 spin = 1;; ++spin) {
             if (*flag == seq) break;
@@ -551,8 +634,47 @@ class Engine final : public EngineBase {
         }
         std::atomic_thread_fence(std::memory_order_acquire);
         std::memcpy(&lc_, (const void*)&ctx_->hc[seq & 1], sizeof(lc_));
+        if (recoverable && lc_.err == ERR_TABLE_FULL) return false;
         if (lc_.err & ERR_TABLE_FULL) throw Error(SR_ERR_CAPACITY, "visited set probe limit exceeded");
         if (lc_.err & ERR_FRONTIER_OVERFLOW) throw Error(SR_ERR_CAPACITY, "frontier overflow");
+        return true;
+    }
+
+    // A level (frontier of n states at arena offset fbase) whose expansion overflowed the visited
+    // set's probe limit: its successors were all counted, but some were neither found nor claimed.
+    // The table is doubled (quotient mode: one more displacement bit, twice the probe limit) and
+    // the level is expanded again in repair mode on the larger table: every successor is probed
+    // again, the states still missing are claimed and appended after the ones the first pass
+    // appended, and no successor is counted twice. A launch enqueued behind the failed level saw
+    // its err word and expanded nothing. lc_ holds the failed pass's counters on entry and the
+    // level's complete counters on return (the slot ring starts over).
+    void repair_level(u64 fbase, u64 n, u32 undiscovered) {
+        const HostCounters first = lc_;
+        u32 dmin[MAX_PROPS];  // discoveries among the states appended by every pass, failed ones too
+        std::copy(first.disc, first.disc + MAX_PROPS, dmin);
+        for (int attempt = 0;; ++attempt) {
+            if (attempt >= 8) throw Error(SR_ERR_CAPACITY, "visited set probe limit exceeded after 8 doublings");
+            SR_HIP(hipStreamSynchronize(stream_));
+            if (o_.verbose)
+                std::fprintf(stderr, "[sr] level of %llu states overflowed the probe limit %u at %llu slots: doubling\n",
+                             (unsigned long long)n, view().plimit, (unsigned long long)cap_);
+            grow_table();
+            stats.table_doublings++;
+            const u32 partial = lc_.claims;
+            init_counters();  // the slot ring starts over: slot 0 continues the level's frontier cursor
+            SR_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(&slot(0)->claims), (int)partial, 1, stream_));
+            const u32 sq = launch_expand(fbase, (u32)n, false, n, undiscovered, SLOT_REPAIR);
+            publish_pending_slot();
+            const bool ok = wait_publish(sq, true);
+            for (int p = 0; p < MAX_PROPS; ++p) dmin[p] = std::min(dmin[p], lc_.disc[p]);
+            if (ok) break;
+        }
+        // successors and enabled slots: the first pass counted them all; claims: the repair's cursor
+        lc_.successors = first.successors;
+        lc_.enabled = first.enabled;
+        lc_.probes += first.probes;
+        lc_.cas += first.cas;
+        std::copy(dmin, dmin + MAX_PROPS, lc_.disc);
     }
 
     // Launch bracketed by pooled events (profile=1); durations are summed once at the end of the
@@ -606,7 +728,9 @@ class Engine final : public EngineBase {
         // the arena with 30% slack, so that table + arena fit one MI355X's 288 GB.
         const bool huge = o_.capacity_hint > (1ull << 31);
         const double load = huge && !load_env_ ? 0.75 : table_load_;
-        if (o_.capacity_hint) while ((double)cap * load < (double)o_.capacity_hint * grow_factor_) cap <<= 1;
+        // (a quotient-mode table also stays under the load its probe limit allows, max_load)
+        if (o_.capacity_hint)
+            while ((double)cap * std::min(load, max_load(cap)) < (double)o_.capacity_hint * grow_factor_) cap <<= 1;
         ratio_ = (double)D_;
         en_ratio_ = std::max(1.0, (double)D_ / 2.0);
         alloc_table(cap);
@@ -614,9 +738,8 @@ class Engine final : public EngineBase {
         // Init states (bfs.rs:43-66): all of them are counted and queued (duplicates too), the
         // visited set keeps distinct ones; `pending` pops from the back, so level 0 is visited in
         // REVERSE init order.
-        std::vector<u64> inits(256 * W);
-        int k = m_.init_states(inits.data());
-        std::vector<u64> f0(inits.begin(), inits.begin() + k * W);
+        const std::vector<u64> f0 = init_states_of(m_);
+        const int k = (int)(f0.size() / W);
         std::vector<u64> rev(k * W);
         for (int i = 0; i < k; ++i) std::copy(&f0[i * W], &f0[i * W] + W, &rev[(k - 1 - i) * W]);
         arena_cap_ = 0;
@@ -781,6 +904,7 @@ class Engine final : public EngineBase {
         }
         auto t_end = Clock::now();
         collect_timing();
+        displacement_stats();
         stats.level_loop_sec = secs(t_loop, t_end);
         stats.total_sec = secs(t_start, t_end);
         stats.table_capacity = cap_;
@@ -865,22 +989,28 @@ class Engine final : public EngineBase {
             const u64 est1 = (u64)((double)n * g) + 1024;     // the next frontier
             const u64 est2 = (u64)((double)est1 * g) + 1024;  // the states it will claim
             const u64 nb_next = lstart_.back();
-            const bool spec = !pessimistic_ && (double)(unique + est1 + est2) < 0.8 * (double)cap_ &&
+            const bool spec = !pessimistic_ && (double)(unique + est1 + est2) < lmax_ * (double)cap_ &&
                               nb_next + est1 + est2 <= arena_cap_;
             // launch shape: a tight estimate (the grid strides over any excess)
             const u64 shape = (u64)((double)n * std::max(ratio_, 0.05) * 1.1) + 64;
             u32 sq_next = spec ? launch_expand(nb_next, 0, true, shape, undiscovered) : 0;
             if (!spec) publish_pending_slot();  // otherwise the enqueued level publishes this one
 
-            wait_publish(sq);  // lc_ = this level's counters
+            bool spec_ok = spec;
+            if (!wait_publish(sq, true)) {  // lc_ = this level's counters
+                // the level overflowed the probe limit: double the table, finish the level on it;
+                // the enqueued next level saw the error and expanded nothing
+                repair_level(lstart_[lstart_.size() - 2], n, undiscovered);
+                spec_ok = false;
+            }
             auto it = seq_launch_.find(sq);
             if (it != seq_launch_.end() && it->second < launch_frontier.size()) {
                 launch_frontier[it->second] = n;
                 launch_probes[it->second] = lc_.probes;
                 launch_cas[it->second] = lc_.cas;
             }
-            if (!account(lc_, spec ? " (next enqueued)" : "")) break;
-            sq = spec ? sq_next : launch_sync(n, undiscovered);
+            if (!account(lc_, spec_ok ? " (next enqueued)" : "")) break;
+            sq = spec_ok ? sq_next : launch_sync(n, undiscovered);
         }
         (void)hipStreamSynchronize(stream_);
         return order_dependent;
@@ -890,7 +1020,7 @@ class Engine final : public EngineBase {
     // the visited set and the arena are grown first if the level might not fit.
     u32 launch_sync(u64 n, u32 undiscovered) {
         const u64 d_eff = pessimistic_ ? D_ : std::min<u64>(D_, (u64)std::ceil(2.0 * ratio_ + 1.0));
-        while ((double)(unique + n * d_eff) > 0.8 * (double)cap_) grow_table();
+        while ((double)(unique + n * d_eff) > lmax_ * (double)cap_) grow_table();
         const u64 fbase = lstart_[lstart_.size() - 2];
         ensure_arena(fbase + n + n * d_eff, fbase + n);
         return launch_expand(fbase, (u32)n, false, n, undiscovered);
@@ -916,7 +1046,7 @@ class Engine final : public EngineBase {
     // One expand_fast launch over a whole level whose frontier starts at arena offset `fbase`:
     // n states (dev_n = 0), or the previous level's claims read on the device (dev_n = 1, `shape`
     // is then an estimate used only for the launch shape; the grid strides over any excess).
-    u32 launch_expand(u64 fbase, u32 n, bool dev_n, u64 shape, u32 undiscovered) {
+    u32 launch_expand(u64 fbase, u32 n, bool dev_n, u64 shape, u32 undiscovered, u32 flags = 0) {
         const u32 sq = next_seq();
         const u64 nbase = fbase + (dev_n ? 0 : n);  // start of the next level (dev_n: + n on the device)
         const u32 ncap = (u32)std::min<u64>(arena_cap_ - nbase, 0xffffffffu);
@@ -924,7 +1054,8 @@ class Engine final : public EngineBase {
         const u32 grid = std::min(expand_grid_cap(), std::max<u32>(1, blocks_for((shape + (1u << ppw_log2) - 1) >> ppw_log2, 4)));
         seq_launch_[sq] = launch_frontier.size();
         // a slotted launch: it counts into its own slot and is published by its successor
-        const SlotWork sw = slot_work(dev_n);
+        SlotWork sw = slot_work(dev_n);
+        sw.flags = flags;
         LevelCounters* lc = slot(slot_k_);
         const u32 svc = sw.pub || sw.zero ? 1u : 0u;  // the extra service workgroup (SlotWork)
         timed([&] {
@@ -979,7 +1110,7 @@ class Engine final : public EngineBase {
         const u64 d_eff = pessimistic_ ? D_ : std::min<u64>(D_, (u64)std::ceil(2.0 * ratio_ + 1.0));
         for (u64 lo = 0; lo < limit;) {
             // Chunk so the visited set stays under 80% load.
-            u64 head = (u64)(0.8 * (double)cap_) - std::min<u64>((u64)(0.8 * (double)cap_), unique + claims);
+            u64 head = (u64)(lmax_ * (double)cap_) - std::min<u64>((u64)(lmax_ * (double)cap_), unique + claims);
             u64 c = std::min<u64>(limit - lo, head / std::max<u64>(d_eff, 1));
             if (c < std::min<u64>(limit - lo, 1u << 16)) {
                 grow_table(fifo_ ? cand.p : nullptr, fifo_ ? limit * A : 0);
@@ -988,36 +1119,62 @@ class Engine final : public EngineBase {
             if (!fifo_) ensure_arena(nbase + claims + c * d_eff, nbase + claims);
             const u32 ulo = (u32)lo, uhi = (u32)(lo + c);
             const bool last = lo + c == limit;
-            const u32 sq = next_seq();
-            if (fifo_) {
-                timed([&] {
-                    expand_fifo<M><<<blocks_for(c, 256), 256, 0, stream_>>>(m_, cur(), ulo, uhi, (u32)limit, view(), cand.p,
-                                                                            A, level, lc_d_, hcd(sq), sq);
-                });
-            } else {
-                const u32 ncap = (u32)std::min<u64>(arena_cap_ - nbase, 0xffffffffu);
-                u64* next = arena_.p + nbase * W;
-                u32* npar = apar_.p + nbase;
-                const u32 ppw_log2 = ppw_env_ >= 0 ? (u32)ppw_env_ : ppw_for(c);
-                const u32 grid = std::min(expand_grid_cap(), blocks_for((c + (1u << ppw_log2) - 1) >> ppw_log2, 4));
-                timed([&] {
-                    auto launch = [&](auto kern) {
-                        kern<<<grid, 256, filt_log2_ ? (8u << filt_log2_) : 0u, stream_>>>(
-                            m_, cur(), ulo, uhi, view(), next, npar, ncap, lc_d_, undiscovered, hcd(sq), sq,
-                            last ? 1u : 0u, ppw_log2, filt_log2_, SlotWork{});
-                    };
-                    if (o_.counters) launch(expand_fast<M, 1, 0, true>);
-                    else switch (probe_batch_ * 10 + probe_load_) {
-                        case 11: launch(expand_fast<M, 1, 1>); break;
-                        case 12: launch(expand_fast<M, 1, 2>); break;
-                        case 13: launch(expand_fast<M, 1, 3>); break;
-                        case 20: launch(expand_fast<M, 2, 0>); break;
-                        case 21: launch(expand_fast<M, 2, 1>); break;
-                        default: launch(expand_fast<M, 1, 0>); break;
-                    }
-                });
+            // repair: the chunk's first pass overflowed the probe limit (see repair_level)
+            auto launch_chunk = [&](bool repair) {
+                const u32 sq = next_seq();
+                if (fifo_) {
+                    timed([&] {
+                        expand_fifo<M><<<blocks_for(c, 256), 256, 0, stream_>>>(m_, cur(), ulo, uhi, (u32)limit, view(), cand.p,
+                                                                                A, level, lc_d_, hcd(sq), sq, repair ? 0u : 1u);
+                    });
+                } else {
+                    const u32 ncap = (u32)std::min<u64>(arena_cap_ - nbase, 0xffffffffu);
+                    u64* next = arena_.p + nbase * W;
+                    u32* npar = apar_.p + nbase;
+                    const u32 ppw_log2 = ppw_env_ >= 0 ? (u32)ppw_env_ : ppw_for(c);
+                    const u32 grid = std::min(expand_grid_cap(), blocks_for((c + (1u << ppw_log2) - 1) >> ppw_log2, 4));
+                    SlotWork sw{};
+                    sw.flags = repair ? SLOT_REPAIR : 0u;
+                    timed([&] {
+                        auto launch = [&](auto kern) {
+                            kern<<<grid, 256, filt_log2_ ? (8u << filt_log2_) : 0u, stream_>>>(
+                                m_, cur(), ulo, uhi, view(), next, npar, ncap, lc_d_, undiscovered, hcd(sq), sq,
+                                last ? 1u : 0u, ppw_log2, filt_log2_, sw);
+                        };
+                        if (o_.counters) launch(expand_fast<M, 1, 0, true>);
+                        else switch (probe_batch_ * 10 + probe_load_) {
+                            case 11: launch(expand_fast<M, 1, 1>); break;
+                            case 12: launch(expand_fast<M, 1, 2>); break;
+                            case 13: launch(expand_fast<M, 1, 3>); break;
+                            case 20: launch(expand_fast<M, 2, 0>); break;
+                            case 21: launch(expand_fast<M, 2, 1>); break;
+                            default: launch(expand_fast<M, 1, 0>); break;
+                        }
+                    });
+                }
+                return sq;
+            };
+            if (!wait_publish(launch_chunk(false), true)) {
+                // Double the table (FIFO: the level's candidate slots move with it) and probe the
+                // chunk again: the missing states are claimed, nothing is counted twice. The
+                // counters continue from the failed pass (a last FAST chunk's publish reset them).
+                const HostCounters first = lc_;
+                u32 dmin[MAX_PROPS];
+                std::copy(first.disc, first.disc + MAX_PROPS, dmin);
+                for (int attempt = 0;; ++attempt) {
+                    if (attempt >= 8) throw Error(SR_ERR_CAPACITY, "visited set probe limit exceeded after 8 doublings");
+                    grow_table(fifo_ ? cand.p : nullptr, fifo_ ? limit * A : 0);
+                    stats.table_doublings++;
+                    SR_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(&lc_d_->claims), (int)lc_.claims, 1, stream_));
+                    SR_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(&lc_d_->err), 0, 1, stream_));
+                    const bool ok = wait_publish(launch_chunk(true), true);
+                    for (int p = 0; p < MAX_PROPS; ++p) dmin[p] = std::min(dmin[p], lc_.disc[p]);
+                    if (ok) break;
+                }
+                lc_.successors = std::max(lc_.successors, first.successors);
+                lc_.enabled = std::max(lc_.enabled, first.enabled);
+                std::copy(dmin, dmin + MAX_PROPS, lc_.disc);
             }
-            wait_publish(sq);
             claims = lc_.claims;
             lo += c;
         }
@@ -1104,6 +1261,8 @@ class Engine final : public EngineBase {
     LevelCounters* lc_d_ = nullptr;
     u64 cap_ = 0;
     DBuf<u64> keys_, meta_;      // visited set
+    double lmax_ = 0.8;          // growth threshold of the current table (max_load)
+    DBuf<u32> aux_;              // [0] rehash error bits, [1] max displacement (displacement_stats)
     DBuf<u64> arena_;            // BFS tree: every level's states in visit order
     DBuf<u32> apar_;             // parent rank (in the previous level) of each arena state
     DBuf<u32> aeb_;              // EventuallyBits of each arena state (models with eventually properties)

@@ -17,7 +17,10 @@
 // slot costs a 64-bit atomicCAS. A successor equal to its parent (a self-loop: 37% of 2pc's
 // successors) is a duplicate by construction and is counted without touching the table.
 #pragma once
+#include <algorithm>
+#include <cmath>
 #include <cstddef>
+#include <cstdlib>
 
 #include "models.hpp"
 
@@ -60,7 +63,36 @@ struct TableView {
     u32 qbits = 0;  // quotient mode: remainder bits per slot (0: fingerprint mode)
     u32 dbits = 0;  // quotient mode: displacement bits (64 - qbits)
     u32 bbits = 0;  // quotient mode: key bits B
+    u32 plimit = MAX_PROBE;  // probe limit: slots past home a probe may visit (quotient: 2^dbits - 2)
 };
+
+// The probe limit of an encoding: quotient mode stores 1 + the displacement in dbits bits.
+SR_HD u32 encoding_probe_limit(u32 qbits, u32 dbits) {
+    return qbits && dbits < 17 ? (1u << dbits) - 2 : (u32)MAX_PROBE;
+}
+
+// Longest linear-probe displacement the table can be expected to hold at load `alpha` with `slots`
+// slots: a run of L occupied slots starts at a given slot with probability ~exp(-L (alpha - 1 -
+// ln alpha)) under uniform hashing, so the longest of them is ~ln(slots) / (alpha - 1 - ln alpha)
+// (at increment_lock N=12's 0.61 load over 2^33 slots: ~220).
+inline double expected_max_displacement(double alpha, double slots) {
+    if (alpha <= 0) return 0;
+    if (alpha >= 1) return 1e300;
+    return std::log(std::max(2.0, slots)) / (alpha - 1.0 - std::log(alpha));
+}
+// The largest load at which that expectation stays within half the probe limit (the growth
+// threshold of a quotient-mode table, whose probe limit is set by its displacement bits), capped
+// at `cap_load`.
+inline double max_load_for(u32 plimit, double slots, double cap_load) {
+    if (plimit >= (u32)MAX_PROBE) return cap_load;
+    double lo = 0.0, hi = cap_load;
+    if (expected_max_displacement(hi, slots) <= plimit / 2.0) return hi;
+    for (int i = 0; i < 60; ++i) {
+        const double mid = 0.5 * (lo + hi);
+        (expected_max_displacement(mid, slots) <= plimit / 2.0 ? lo : hi) = mid;
+    }
+    return lo;
+}
 
 // Where a key's probe sequence starts, and the value its slot holds at displacement 0; at
 // displacement d the slot is (home + d) & mask and the value tag + d * step (step = 1 in quotient
@@ -104,8 +136,13 @@ SR_HD ProbeKey reprobe(const TableView& from, const TableView& to, u64 i, u64 v)
 // the model packs its states into a key (qkey) whose remainder fits a slot with >= 8 displacement
 // bits; min_table_cap keeps every table of such a model in that mode from the start (a
 // fingerprint cannot be turned back into a key when the table grows).
+// SR_DISP_LIMIT (tests) lowers every table's probe limit, to force the overflow path.
+inline u32 forced_probe_limit() {
+    const char* e = std::getenv("SR_DISP_LIMIT");
+    return e ? (u32)std::max(1, std::atoi(e)) : 0u;
+}
 template <class M>
-inline TableView make_table_view(const M& m, u64* keys, u64* meta, u64 cap) {
+inline TableView make_table_view(const M& m, u64* keys, u64* meta, u64 cap, bool natural = false) {
     TableView v{keys, meta, cap - 1};
     if constexpr (has_qkey<M>::value && M::W >= 2) {
         const u32 B = (u32)m.qkey_bits();
@@ -117,6 +154,8 @@ inline TableView make_table_view(const M& m, u64* keys, u64* meta, u64 cap) {
             v.bbits = B;
         }
     }
+    v.plimit = encoding_probe_limit(v.qbits, v.dbits);
+    if (!natural && forced_probe_limit()) v.plimit = std::min(v.plimit, forced_probe_limit());
     return v;
 }
 template <class M>
@@ -157,16 +196,20 @@ struct StatShard {
 struct LevelCounters {
     StatShard stat[NSHARD];
     u32 claims;            // new states inserted into the visited set (= next-frontier cursor)
-    u32 pad1[31];
+    u32 err;               // ErrBits; next to claims: a pipelined launch loads both with one load
+    u32 pad1[30];
     u32 ticket;            // groups of workgroups finished in this launch
     u32 pad2[31];
     u32 gticket[NSHARD][32];  // workgroups finished per group (blockIdx % NSHARD), one line each
-    u32 err;               // ErrBits
     u32 disc[MAX_PROPS];   // min rank of a discovering state in the frontier being produced
     u32 pad3[32];
     u32 prev_claims;       // claims of the last level (set by a resetting publish): the size of the
                            // frontier a pipelined launch expands, read on the device
+    u32 prev_err;          // always 0 (the err word a launch reading prev_claims sees)
 };
+static_assert(offsetof(LevelCounters, err) == offsetof(LevelCounters, claims) + 4, "claims/err pair");
+static_assert(offsetof(LevelCounters, prev_err) == offsetof(LevelCounters, prev_claims) + 4, "prev pair");
+static_assert(offsetof(LevelCounters, claims) % 8 == 0 && offsetof(LevelCounters, prev_claims) % 8 == 0, "u64 loads");
 
 // A workgroup's statistics (one thread): into its shard.
 __device__ __forceinline__ void add_stats(LevelCounters* lc, u32 succ, u32 en, u32 probes = 0, u32 cas = 0) {
@@ -324,12 +367,22 @@ __global__ void publish_kernel(LevelCounters* lc, HostCounters* h, u32 seq, u32 
 // it was published (by launch K-1 or by slot_publish_kernel) before launch K starts. When the
 // host waits for a level without having enqueued its successor, slot_publish_kernel publishes it.
 constexpr u32 SLOTS = 4;
+enum SlotFlags : u32 {
+    // Repair pass of a level whose first pass overflowed the visited set's probe limit (the table
+    // has been doubled since): every successor is probed again, the states still missing are
+    // claimed and appended after the ones the first pass appended; successors are not counted
+    // again (the first pass counted every one of them).
+    SLOT_REPAIR = 1,
+};
 struct SlotWork {
-    const u32* prev_n;          // frontier size = the previous level's claims (nullptr: `hi` is exact)
+    const u32* prev_n;          // frontier size = the previous level's claims (nullptr: `hi` is exact);
+                                // prev_n[1] is that level's err word: a launch behind a failed level
+                                // expands nothing
     const LevelCounters* pub;   // slot to publish (nullptr: none)
     HostCounters* hc;           // its host mirror
     u32 seq;                    // its launch's sequence number
     LevelCounters* zero;        // slot to reset (nullptr: none)
+    u32 flags = 0;              // SlotFlags
 };
 
 // One wave (lane = 0..63): publish sw.pub to sw.hc, then reset sw.zero.
@@ -385,7 +438,7 @@ template <int POL = 0>
 __device__ __forceinline__ u64 find_or_claim_from(const TableView& t, const ProbeKey& k, u64 cur, bool* is_new,
                                                   u32* err, u32* probes = nullptr, u32* cas = nullptr) {
     const u64 step = probe_step(t);
-    const int limit = step && t.dbits < 17 ? (int)((1u << t.dbits) - 2) : MAX_PROBE;
+    const int limit = (int)t.plimit;
     u64 i = k.home, key = k.tag;
     for (int probe = 0; probe < limit; ++probe) {
         if (cur == key) {
@@ -595,8 +648,11 @@ __global__ void __launch_bounds__(256) expand_fast(M m, const u64* __restrict__ 
     const u32 nblk = gridDim.x - (svc ? 1u : 0u);  // workgroups that expand parents
     if (sw.prev_n) {
         // Pipelined launch (enqueued before the host saw the previous level finish): the frontier
-        // is the previous level's claims, and the next level starts right after it.
-        const u32 nn = __hip_atomic_load(sw.prev_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // is the previous level's claims, and the next level starts right after it. Behind a level
+        // that failed (its err word, loaded with its claims) it expands nothing: the host repairs
+        // or restarts that level and its frontier is not final.
+        const u64 ce = __hip_atomic_load(reinterpret_cast<const u64*>(sw.prev_n), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const u32 nn = (ce >> 32) ? 0u : (u32)ce;
         hi = lo + nn;
         next += (u64)nn * W;
         next_par += nn;
@@ -797,8 +853,9 @@ __global__ void __launch_bounds__(256) expand_fast(M m, const u64* __restrict__ 
             if (threadIdx.x == 0) stage_n = 0;
         }
     }
-    u32 total_succ = block_sum(succ, scratch);
-    u32 total_enabled = block_sum(enabled, scratch);
+    const bool repair = (sw.flags & SLOT_REPAIR) != 0;  // successors were counted by the first pass
+    u32 total_succ = repair ? 0u : block_sum(succ, scratch);
+    u32 total_enabled = repair ? 0u : block_sum(enabled, scratch);
     u32 total_probes = STATS ? block_sum(probes, scratch) : 0u;
     u32 total_cas = STATS ? block_sum(cas, scratch) : 0u;
     const u32 n = min(stage_n, (u32)STAGE);
@@ -833,7 +890,7 @@ __global__ void __launch_bounds__(256) expand_fast(M m, const u64* __restrict__ 
 template <class M>
 __global__ void __launch_bounds__(256) expand_fifo(M m, const u64* __restrict__ frontier, u32 lo, u32 hi, u32 n,
                                                    TableView t, u32* __restrict__ cand, u32 A, u32 level,
-                                                   LevelCounters* lc, HostCounters* hc, u32 seq) {
+                                                   LevelCounters* lc, HostCounters* hc, u32 seq, u32 count_succ) {
     __shared__ u32 scratch[4];
     const u32 r = lo + blockIdx.x * blockDim.x + threadIdx.x;
     u32 succ = 0, claims = 0;
@@ -842,7 +899,7 @@ __global__ void __launch_bounds__(256) expand_fifo(M m, const u64* __restrict__ 
         load_state<M::W>(frontier, r, s);
         const u64 lvl = (u64)(level + 1) << META_SHIFT;
         for_each_successor(m, s, [&](int a, const u64* ns) {
-            ++succ;
+            succ += count_succ;  // 0 in the repair pass of a chunk that overflowed the probe limit
             if (same_state<M::W>(ns, s)) return;  // self-loop: the parent is visited already
             bool is_new;
             u64 slot = find_or_claim(t, probe_key(m, t, ns), &is_new, &lc->err);
@@ -1035,16 +1092,33 @@ __global__ void init_level_counters(LevelCounters* lc, LevelCounters* slots, u32
     }
 }
 
-// Rehash into a table of twice the capacity (keys and meta move together).
-__global__ void rehash(TableView from, u64 from_cap, TableView to, LevelCounters* lc) {
+// Rehash into a larger table (keys and meta move together); an entry that does not fit the new
+// table's probe limit sets ERR_TABLE_FULL in *err (the host then rehashes into a larger one).
+__global__ void rehash(TableView from, u64 from_cap, TableView to, u32* err) {
     u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= from_cap) return;
     u64 k = from.keys[i];
     if (!k) return;
     bool is_new;
-    u64 slot = find_or_claim(to, reprobe(from, to, i, k), &is_new, &lc->err);
+    u64 slot = find_or_claim(to, reprobe(from, to, i, k), &is_new, err);
     if (slot == ~0ull) return;
     if (to.meta) to.meta[slot] = from.meta[i];
+}
+
+// Longest linear-probe displacement over the occupied slots (sr_stats.max_displacement): quotient
+// mode stores 1 + the displacement in the low dbits; a fingerprint's home is fp & mask.
+__global__ void __launch_bounds__(256) table_max_disp(TableView t, u64 cap, u32* out) {
+    u32 best = 0;
+    const u64 dmask = t.qbits ? (1ull << t.dbits) - 1 : 0;
+    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < cap; i += (u64)gridDim.x * blockDim.x) {
+        const u64 v = t.keys[i];
+        if (!v) continue;
+        const u64 d = t.qbits ? (v & dmask) - 1 : (i - (v & t.mask)) & t.mask;
+        best = max(best, (u32)min<u64>(d, 0xffffffffull));
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) best = max(best, (u32)__shfl_xor((int)best, d, 64));
+    if ((threadIdx.x & 63) == 0 && best) atomicMax(out, best);
 }
 
 // After a rehash: candidate slot indices of the old table -> slots of the new one.

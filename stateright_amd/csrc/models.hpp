@@ -73,6 +73,21 @@ template <class M>
 struct has_self_loops<M, std::void_t<decltype(std::declval<const M&>().self_loops((const u64*)nullptr, (const u64*)nullptr,
                                                                                   (u64*)nullptr))>> : std::true_type {};
 
+// Init states (`Model::init_states`, src/lib.rs:163). A model writes its init states into a host
+// buffer of W words each; the engine sizes that buffer from the model's optional `init_count()`,
+// or for MAX_INIT_STATES states when the model has none (the documented bound of the GpuModel
+// concept, include/stateright_gpu_model.hpp). Every host-side caller goes through init_states_of.
+constexpr int MAX_INIT_STATES = 256;
+template <class M, class = void>
+struct has_init_count : std::false_type {};
+template <class M>
+struct has_init_count<M, std::void_t<decltype(std::declval<const M&>().init_count())>> : std::true_type {};
+template <class M>
+inline int init_capacity(const M& m) {
+    if constexpr (has_init_count<M>::value) return m.init_count() > 0 ? m.init_count() : 1;
+    else return MAX_INIT_STATES;
+}
+
 // The symmetry-reduced view of a model (the engine's opt-in canonical reduction): init states and
 // successors are replaced by their canonical representatives, so the visited set, the frontier and
 // the BFS tree hold one state per orbit. Everything else is the model's own.
@@ -498,12 +513,23 @@ struct IncrementLock {
     }
     int expectation(int) const { return ALWAYS; }
     const char* prop_name(int p) const { return p == 0 ? "fin" : "mutex"; }
-    // Exact key (quotient visited set): word 0 holds i, lock and threads 0..7 in its low 61 bits,
-    // word 1 threads 8.. : the state is the integer w0 | w1 << 61 below 2^(5 + 7n).
-    int qkey_bits() const { return 5 + 7 * n; }
+    // Exact key (quotient visited set), 5 + 6n bits: i and lock, then one 6-bit code per thread for
+    // its (t, pc) pair: pc while pc < 2 (t is still 0 there: it is set by Read, pc 1 -> 2), else
+    // 2 + 3t + (pc - 2) <= 49. Injective on every state whose threads hold t = 0 before their Read
+    // and pc <= 4, i.e. on every reachable state. Two bits per thread shorter than the packed
+    // words (5 + 7n): at N = 12 the key is 77 bits, so a table of 2^33 slots keeps 20 displacement
+    // bits per slot (a probe limit far beyond any run) where the packed words left 8 (254 slots).
+    int qkey_bits() const { return 5 + 6 * n; }
     SR_HD unsigned __int128 qkey(const u64* s) const {
-        if constexpr (W_ == 1) return s[0];
-        else return (unsigned __int128)s[0] | ((unsigned __int128)s[W_ - 1] << 61);
+        u64 lo = s[0] & 31, hi = 0;  // threads 0..8 in lo bits 5..58, threads 9.. in hi
+        for (int t = 0; t < n; ++t) {
+            const u64 f = getb(s, toff(t), 7);  // t | pc << 4
+            const u64 tv = f & 15, pc = f >> 4;
+            const u64 code = pc < 2 ? pc : 2 + 3 * tv + (pc - 2);
+            if (t < 9) lo |= code << (5 + 6 * t);
+            else hi |= code << (6 * (t - 9));
+        }
+        return (unsigned __int128)lo | ((unsigned __int128)hi << 59);
     }
     int describe_width() const { return 2 + 2 * n; }
     void describe(const u64* s, i64* d) const {

@@ -127,6 +127,15 @@ class OracleRun:
         flat = list(buf[:n])
         return [tuple(flat[i:i + self.width]) for i in range(0, n, self.width)]
 
+    def visits_array(self):
+        """The visits as an int64 numpy array (count x width), without Python tuples."""
+        import numpy as np
+        L = lib()
+        n = L.oracle_visits(self.h, None, 0)
+        out = np.empty(max(n, 1), dtype=np.int64)
+        L.oracle_visits(self.h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), n)
+        return out[:n].reshape(-1, self.width)
+
     def visit_paths(self):
         """Action ids of the path the reference's visitor receives at each pop, in visit order."""
         L = lib()

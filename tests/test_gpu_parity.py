@@ -60,6 +60,8 @@ def gpu(model, params, order, **kw):
         b = b.visitor(rec)
     if kw.get("target"):
         b = b.target_state_count(kw["target"])
+    if kw.get("counters"):
+        b = b.counters()
     c = b.spawn_bfs().join()
     return c, rec
 
@@ -294,3 +296,36 @@ def test_small_grid_strides(case, grid, monkeypatch):
         assert (c.unique_state_count(), c.state_count(), c.max_depth()) == \
             (o.unique_state_count, o.state_count, o.max_depth)
         assert sorted(c.discoveries()) == o.discovery_names()
+
+
+@pytest.mark.parametrize("pipe", ["1", "0"])
+@pytest.mark.parametrize("order", ["fifo", "fast"])
+@pytest.mark.parametrize("case", [(INCREMENT_LOCK, [9]), (TWO_PHASE, [7])], ids=ids)
+def test_probe_limit_overflow_doubles_the_table(case, order, pipe, monkeypatch):
+    # SR_DISP_LIMIT lowers the probe limit to a few slots, so levels overflow it. The engine doubles
+    # the visited set in the middle of the check (quotient mode: one more displacement bit) and
+    # finishes the level on it (repair pass: the missing successors are claimed, none is counted
+    # twice), instead of restarting the check; counts stay exact in both orders, with and without
+    # level pipelining, in quotient (increment_lock, 2 words) and fingerprint (2pc) mode.
+    monkeypatch.setenv("SR_DISP_LIMIT", "6")
+    monkeypatch.setenv("SR_PIPELINE", pipe)
+    model, params = case
+    o = oracle(model, params)
+    c, _ = gpu(model, params, order, counters=True)
+    assert (c.unique_state_count(), c.state_count(), c.max_depth()) == (o.unique_state_count, o.state_count, o.max_depth)
+    assert sorted(c.discoveries()) == o.discovery_names()
+    st = c.stats()
+    assert st["table_doublings"] > 0 and st["restarts"] == 0
+    assert st["displacement_limit"] == 6 and 0 < st["max_displacement"] < 6
+
+
+def test_displacement_stats_increment_lock_10():
+    # The quotient key of increment_lock (6 bits per thread) leaves a probe limit far above the
+    # longest run; counters() measures the longest displacement of the final table.
+    n = 10
+    expect = 1 + 4 * sum(math.factorial(n) // math.factorial(n - k) for k in range(1, n + 1))
+    c = sr.IncrementLock(n).checker().capacity_hint(expect).counters().spawn_bfs().join()
+    st = c.stats()
+    assert c.unique_state_count() == expect
+    assert st["displacement_limit"] >= 4094 and 0 < st["max_displacement"] < st["displacement_limit"] // 4
+    assert st["table_doublings"] == 0

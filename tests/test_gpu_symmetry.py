@@ -72,3 +72,28 @@ def test_partitioned_with_symmetry():
 def test_symmetry_requires_a_canonical_form():
     with pytest.raises(sr.CheckerError):
         sr.IncrementLock(3).checker().symmetry_canonical().spawn_bfs()
+
+
+@pytest.mark.parametrize("partitions", [1, 3])
+@pytest.mark.parametrize("n", [2, 3, 4, 5])
+def test_discoveries_replay_through_the_engine(n, partitions):
+    # The engine's own replay, chain and Explorer walk concrete states of the original model under
+    # the canonical reduction: assert_discovery(name, into_actions()) holds for every discovery
+    # (RmPrepare(0) then RmPrepare(1) is valid although the representative after the first step
+    # has RM 1 prepared), the fingerprint chain has one fingerprint per path state, and the
+    # Explorer's `Path::final_state` follows it to the discovered state.
+    b = sr.TwoPhaseSys(n).checker().symmetry_canonical().order("fast")
+    c = (b.partitions(partitions) if partitions > 1 else b).spawn_bfs().join()
+    found = c.discoveries()
+    assert found
+    for name, path in found.items():
+        c.assert_discovery(name, path.into_actions())
+        chain = c.discovery_fingerprints(name)
+        assert len(chain) == len(path) + 1
+        views = c.explore(chain)
+        assert views is not None  # the chain is a walk of concrete states
+        # the state the chain leads to is the path's last (concrete) state: its successors' views
+        # are those of the original model from there
+        for action, state, fp in views:
+            if state is not None:
+                assert len(state) == len(path.last_state())
