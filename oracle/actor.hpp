@@ -1,0 +1,706 @@
+// ORACLE — TEST INFRASTRUCTURE ONLY (see oracle.hpp).
+//
+// A generic restatement of `ActorModel` (src/actor/model.rs:176-327) over a system description
+// `Sys`, with the reference's actor-model fixtures on top of it:
+//   * ping-pong (src/actor/actor_test_util.rs:4-96), the goldens of src/actor/model.rs:515-734 and
+//     src/checker/explorer.rs:370-416;
+//   * the undeliverable-message and timer fixtures (src/actor/model.rs:698-734);
+//   * the ABD linearizable register (examples/linearizable-register.rs), golden 544 (:256, :278).
+//
+// Semantics kept exactly: init = the init network, then every actor's on_start in index order with
+// its commands processed (record_msg_out, then insert; timers); actions per envelope in network
+// order = Drop (lossy networks) then Deliver (dst within the actor list), then Timeout per set
+// timer; Deliver is None for an undeliverable envelope and for a no-op (state not touched, no
+// command), drops the envelope unless the network duplicates, records the message in; Timeout is
+// None only for a no-op that re-arms its timer, and clears the timer otherwise; `is_timer_set` is
+// a Vec that grows on demand, so its length is part of the state (model.rs:189-198).
+//
+// The network is a SET iterated in sorted order. The reference iterates a HashSet seeded by ahash,
+// so its action ORDER is not reproducible here; counts of full explorations do not depend on it
+// (early-exit actor configurations are parity unpinned).
+#pragma once
+#include "paxos.hpp"
+
+namespace oracle {
+namespace actor {
+
+using Id = u64;
+
+template <class Msg>
+struct Envelope {
+    Id src = 0, dst = 0;
+    Msg msg{};
+    auto key() const { return std::make_tuple(src, dst, msg.key()); }
+    bool operator<(const Envelope& o) const { return key() < o.key(); }
+    bool operator==(const Envelope& o) const { return key() == o.key(); }
+};
+
+// `Out` (src/actor.rs:163-201): the commands an actor emits, in order.
+template <class Msg>
+struct Out {
+    enum Kind { SEND, SET_TIMER, CANCEL_TIMER };
+    struct Cmd {
+        Kind kind;
+        Id dst;
+        Msg msg;
+    };
+    std::vector<Cmd> cmds;
+    void send(Id dst, const Msg& m) { cmds.push_back(Cmd{SEND, dst, m}); }
+    void broadcast(const std::vector<Id>& ids, const Msg& m) {
+        for (Id d : ids) send(d, m);
+    }
+    void set_timer() { cmds.push_back(Cmd{SET_TIMER, 0, Msg{}}); }
+    void cancel_timer() { cmds.push_back(Cmd{CANCEL_TIMER, 0, Msg{}}); }
+    bool empty() const { return cmds.empty(); }
+};
+
+// ActorModel<Sys>. Sys provides:
+//   using AState, Msg, Hist;  size_t actor_count();  bool lossy, duplicating;
+//   std::vector<Envelope<Msg>> init_network();  Hist init_history();
+//   AState on_start(Id, Out<Msg>&);
+//   bool on_msg(Id, AState&, Id src, const Msg&, Out<Msg>&)     (true: Cow::Owned)
+//   bool on_timeout(Id, AState&, Out<Msg>&)                      (true: Cow::Owned)
+//   std::optional<Hist> record_in / record_out(const Hist&, const Envelope<Msg>&)
+//   bool within_boundary(const State&);  properties;  hashing / description / Debug text.
+template <class Sys>
+struct ActorModel {
+    using AState = typename Sys::AState;
+    using Msg = typename Sys::Msg;
+    using Hist = typename Sys::Hist;
+    using Env = Envelope<Msg>;
+    struct State {
+        std::vector<AState> actor_states;
+        std::set<Env> network;  // `Network<Msg> = HashableHashSet<Envelope<Msg>>` (model.rs:69)
+        std::vector<bool> is_timer_set;
+        Hist history{};
+    };
+    enum Kind { DELIVER, DROP, TIMEOUT };
+    struct Action {
+        Kind kind;
+        Env env;  // Deliver / Drop
+        Id id;    // Timeout
+    };
+
+    Sys sys;
+
+    // process_commands (model.rs:176-202)
+    void process_commands(Id id, const Out<Msg>& out, State& s) const {
+        const size_t index = (size_t)id;
+        for (auto& c : out.cmds) {
+            switch (c.kind) {
+                case Out<Msg>::SEND: {
+                    const Env e{id, c.dst, c.msg};
+                    if (auto h = sys.record_out(s.history, e)) s.history = *h;
+                    s.network.insert(e);
+                    break;
+                }
+                case Out<Msg>::SET_TIMER:
+                    if (s.is_timer_set.size() <= index) s.is_timer_set.resize(index + 1, false);
+                    s.is_timer_set[index] = true;
+                    break;
+                case Out<Msg>::CANCEL_TIMER:
+                    if (index >= s.is_timer_set.size()) throw std::runtime_error("CancelTimer before any SetTimer (the reference panics)");
+                    s.is_timer_set[index] = false;
+                    break;
+            }
+        }
+    }
+
+    std::vector<State> init_states() const {  // model.rs:215-242
+        State s;
+        s.history = sys.init_history();
+        for (auto& e : sys.init_network()) s.network.insert(e);
+        for (size_t i = 0; i < sys.actor_count(); ++i) {
+            Out<Msg> out;
+            s.actor_states.push_back(sys.on_start((Id)i, out));
+            process_commands((Id)i, out, s);
+        }
+        return {s};
+    }
+
+    void actions(const State& s, std::vector<Action>& out) const {  // model.rs:238-257
+        for (auto& e : s.network) {
+            if (sys.lossy) out.push_back(Action{DROP, e, 0});
+            if (e.dst < s.actor_states.size()) out.push_back(Action{DELIVER, e, 0});
+        }
+        for (size_t i = 0; i < s.is_timer_set.size(); ++i)
+            if (s.is_timer_set[i]) out.push_back(Action{TIMEOUT, Env{}, (Id)i});
+    }
+
+    std::optional<State> next_state(const State& last, const Action& a) const {  // model.rs:259-327
+        switch (a.kind) {
+            case DROP: {
+                State s = last;
+                s.network.erase(a.env);
+                return s;
+            }
+            case DELIVER: {
+                const Env& e = a.env;
+                if (e.dst >= last.actor_states.size()) return std::nullopt;
+                AState st = last.actor_states[e.dst];
+                Out<Msg> out;
+                const bool owned = sys.on_msg(e.dst, st, e.src, e.msg, out);
+                if (!owned && out.empty()) return std::nullopt;  // is_no_op (src/actor.rs:232-234)
+                auto h = sys.record_in(last.history, e);
+                State s = last;
+                if (!sys.duplicating) s.network.erase(e);
+                if (owned) s.actor_states[e.dst] = st;
+                if (h) s.history = *h;
+                process_commands(e.dst, out, s);
+                return s;
+            }
+            case TIMEOUT: {
+                const size_t index = (size_t)a.id;
+                AState st = last.actor_states[index];
+                Out<Msg> out;
+                const bool owned = sys.on_timeout(a.id, st, out);
+                bool keep_timer = false;
+                for (auto& c : out.cmds) keep_timer |= c.kind == Out<Msg>::SET_TIMER;
+                if (!owned && out.empty() && keep_timer) return std::nullopt;
+                State s = last;
+                s.is_timer_set[index] = false;
+                if (owned) s.actor_states[index] = st;
+                process_commands(a.id, out, s);
+                return s;
+            }
+        }
+        return std::nullopt;
+    }
+
+    bool within_boundary(const State& s) const { return sys.within_boundary(s); }
+    std::vector<Property<ActorModel>> properties() const { return sys.template properties<ActorModel>(); }
+
+    // `impl Hash for ActorModelState` (model_state.rs:76-86): actor states, history, timers, network.
+    void hash_state(const State& s, Hasher& h) const {
+        h.write_usize(s.actor_states.size());
+        for (auto& a : s.actor_states) sys.hash_actor(a, h);
+        sys.hash_history(s.history, h);
+        h.write_usize(s.is_timer_set.size());
+        for (bool b : s.is_timer_set) h.write_bool(b);
+        h.write_usize(s.network.size());
+        for (auto& e : s.network) {
+            h.write_u64(e.src);
+            h.write_u64(e.dst);
+            sys.hash_msg(e.msg, h);
+        }
+    }
+
+    // Envelope code shared with the GPU encodings: (msg code * 128 + dst) * 16 + src.
+    i64 env_code(const Env& e) const { return (sys.msg_code(e.msg) * 128 + (i64)e.dst) * 16 + (i64)e.src; }
+    // Canonical description (shared with the GPU encodings): every actor's fields, the history's,
+    // the timer vector (length, bit mask), then the network as Sys::NET sorted envelope codes
+    // padded with -1.
+    std::vector<i64> describe(const State& s) const {
+        std::vector<i64> d;
+        for (size_t i = 0; i < s.actor_states.size(); ++i) sys.describe_actor((Id)i, s.actor_states[i], d);
+        sys.describe_history(s.history, d);
+        i64 mask = 0;
+        for (size_t i = 0; i < s.is_timer_set.size(); ++i) mask |= (i64)s.is_timer_set[i] << i;
+        d.push_back((i64)s.is_timer_set.size());
+        d.push_back(mask);
+        std::vector<i64> net;
+        for (auto& e : s.network) net.push_back(env_code(e));
+        std::sort(net.begin(), net.end());
+        if (net.size() > (size_t)Sys::NET) throw std::runtime_error("network larger than the description's capacity");
+        net.resize(Sys::NET, -1);
+        d.insert(d.end(), net.begin(), net.end());
+        return d;
+    }
+    // Action ids: Deliver = code * 4 + 1, Drop = code * 4 + 2, Timeout(i) = i * 4 + 3.
+    i64 action_id(const Action& a) const {
+        switch (a.kind) {
+            case DELIVER: return env_code(a.env) * 4 + 1;
+            case DROP: return env_code(a.env) * 4 + 2;
+            case TIMEOUT: return (i64)a.id * 4 + 3;
+        }
+        return 0;
+    }
+    // `Debug` of `ActorModelAction` (model.rs:42-51).
+    std::string format_action(const Action& a) const {
+        auto env = [&](const Env& e) {
+            return "src: Id(" + std::to_string(e.src) + "), dst: Id(" + std::to_string(e.dst) + "), msg: " + sys.format_msg(e.msg);
+        };
+        switch (a.kind) {
+            case DELIVER: return "Deliver { " + env(a.env) + " }";
+            case DROP: return "Drop(Envelope { " + env(a.env) + " })";
+            case TIMEOUT: return "Timeout(Id(" + std::to_string(a.id) + "))";
+        }
+        return "?";
+    }
+};
+
+// ---------------------------------------------------------------------------------------------
+// Ping-pong (src/actor/actor_test_util.rs:4-96).
+// ---------------------------------------------------------------------------------------------
+struct PingPongMsg {
+    bool pong = false;  // Ping(u32) | Pong(u32)
+    u32 v = 0;
+    auto key() const { return std::make_tuple(pong, v); }
+};
+
+struct PingPongSys {
+    static constexpr int NET = 16;
+    using AState = u32;  // count
+    using Msg = PingPongMsg;
+    using Hist = std::pair<u32, u32>;  // (#in, #out)
+    u32 max_nat = 1;
+    bool maintains_history = false;
+    bool lossy = false, duplicating = true;
+
+    size_t actor_count() const { return 2; }
+    std::vector<Envelope<Msg>> init_network() const { return {}; }
+    Hist init_history() const { return {0, 0}; }
+    AState on_start(Id id, Out<Msg>& o) const {  // actor 0 serves to actor 1
+        if (id == 0) o.send(1, Msg{false, 0});
+        return 0;
+    }
+    bool on_msg(Id, AState& s, Id src, const Msg& m, Out<Msg>& o) const {
+        if (m.pong && s == m.v) {
+            o.send(src, Msg{false, m.v + 1});
+            s += 1;
+            return true;
+        }
+        if (!m.pong && s == m.v) {
+            o.send(src, Msg{true, m.v});
+            s += 1;
+            return true;
+        }
+        return false;
+    }
+    bool on_timeout(Id, AState&, Out<Msg>&) const { return false; }
+    std::optional<Hist> record_in(const Hist& h, const Envelope<Msg>&) const {
+        if (!maintains_history) return std::nullopt;
+        return Hist{h.first + 1, h.second};
+    }
+    std::optional<Hist> record_out(const Hist& h, const Envelope<Msg>&) const {
+        if (!maintains_history) return std::nullopt;
+        return Hist{h.first, h.second + 1};
+    }
+    template <class State>
+    bool within_boundary(const State& s) const {
+        for (auto c : s.actor_states)
+            if (c > max_nat) return false;
+        return true;
+    }
+    template <class M>
+    std::vector<Property<M>> properties() const {
+        using P = Property<M>;
+        using S = typename M::State;
+        auto mx = [](const S& s) { return *std::max_element(s.actor_states.begin(), s.actor_states.end()); };
+        auto mn = [](const S& s) { return *std::min_element(s.actor_states.begin(), s.actor_states.end()); };
+        auto any_eq = [](const S& s, u32 v) {
+            return std::any_of(s.actor_states.begin(), s.actor_states.end(), [v](u32 c) { return c == v; });
+        };
+        return {
+            P::always("delta within 1", [mx, mn](const M&, const S& s) { return mx(s) - mn(s) <= 1; }),
+            P::sometimes("can reach max", [any_eq](const M& m, const S& s) { return any_eq(s, m.sys.max_nat); }),
+            P::eventually("must reach max", [any_eq](const M& m, const S& s) { return any_eq(s, m.sys.max_nat); }),
+            P::eventually("must exceed max", [any_eq](const M& m, const S& s) { return any_eq(s, m.sys.max_nat + 1); }),
+            P::always("#in <= #out", [](const M&, const S& s) { return s.history.first <= s.history.second; }),
+            P::eventually("#out <= #in + 1", [](const M&, const S& s) { return s.history.second <= s.history.first + 1; }),
+        };
+    }
+    void hash_actor(const AState& a, Hasher& h) const { h.write_u64(a); }
+    void hash_history(const Hist& x, Hasher& h) const {
+        h.write_u64(x.first);
+        h.write_u64(x.second);
+    }
+    void hash_msg(const Msg& m, Hasher& h) const {
+        h.write_bool(m.pong);
+        h.write_u64(m.v);
+    }
+    i64 msg_code(const Msg& m) const { return (i64)m.v * 2 + (m.pong ? 1 : 0); }
+    void describe_actor(Id, const AState& a, std::vector<i64>& d) const { d.push_back(a); }
+    void describe_history(const Hist& x, std::vector<i64>& d) const {
+        d.push_back(x.first);
+        d.push_back(x.second);
+    }
+    std::string format_msg(const Msg& m) const { return std::string(m.pong ? "Pong(" : "Ping(") + std::to_string(m.v) + ")"; }
+};
+
+// ---------------------------------------------------------------------------------------------
+// Unit-actor fixtures (src/actor/model.rs:698-734): kind 0 = handles_undeliverable_messages (an
+// `Actor for ()` and an init envelope to Id 99), kind 1 = resets_timer (an actor that sets its
+// timer on start and ignores every message).
+// ---------------------------------------------------------------------------------------------
+struct UnitMsg {
+    auto key() const { return 0; }
+};
+struct FixtureSys {
+    static constexpr int NET = 4;
+    using AState = u8;
+    using Msg = UnitMsg;
+    using Hist = u8;
+    int kind = 0;
+    bool lossy = false, duplicating = true;
+    size_t actor_count() const { return 1; }
+    std::vector<Envelope<Msg>> init_network() const {
+        if (kind == 0) return {Envelope<Msg>{0, 99, UnitMsg{}}};
+        return {};
+    }
+    Hist init_history() const { return 0; }
+    AState on_start(Id, Out<Msg>& o) const {
+        if (kind == 1) o.set_timer();
+        return 0;
+    }
+    bool on_msg(Id, AState&, Id, const Msg&, Out<Msg>&) const { return false; }
+    bool on_timeout(Id, AState&, Out<Msg>&) const { return false; }
+    std::optional<Hist> record_in(const Hist&, const Envelope<Msg>&) const { return std::nullopt; }
+    std::optional<Hist> record_out(const Hist&, const Envelope<Msg>&) const { return std::nullopt; }
+    template <class State>
+    bool within_boundary(const State&) const { return true; }
+    template <class M>
+    std::vector<Property<M>> properties() const {  // "force full traversal" (model.rs:706,730)
+        return {Property<M>::always("unused", [](const M&, const typename M::State&) { return true; })};
+    }
+    void hash_actor(const AState& a, Hasher& h) const { h.write_u8(a); }
+    void hash_history(const Hist& x, Hasher& h) const { h.write_u8(x); }
+    void hash_msg(const Msg&, Hasher& h) const { h.write_u8(0); }
+    i64 msg_code(const Msg&) const { return 0; }
+    void describe_actor(Id, const AState&, std::vector<i64>& d) const { d.push_back(0); }
+    void describe_history(const Hist&, std::vector<i64>&) const {}
+    std::string format_msg(const Msg&) const { return "()"; }
+};
+
+// ---------------------------------------------------------------------------------------------
+// ABD linearizable register (examples/linearizable-register.rs): AbdActor servers wrapped by
+// RegisterActor::Server, RegisterActor::Client clients with put_count 1 (src/actor/register.rs:
+// 119-217), a non-duplicating lossless network, a LinearizabilityTester<Id, Register<char>>
+// history recorded by RegisterMsg::record_{invocations,returns} (src/actor/register.rs:37-87).
+// ---------------------------------------------------------------------------------------------
+struct Seq {  // (LogicalClock, Id), ordered lexicographically
+    u64 clock = 0;
+    Id id = 0;
+    auto key() const { return std::make_tuple(clock, id); }
+    bool operator<(const Seq& o) const { return key() < o.key(); }
+    bool operator==(const Seq& o) const { return key() == o.key(); }
+};
+enum AbdKind : u8 { A_PUT, A_GET, A_PUTOK, A_GETOK, A_QUERY, A_ACKQUERY, A_RECORD, A_ACKRECORD };
+struct AbdMsg {
+    AbdKind kind = A_PUT;
+    u64 req = 0;
+    Seq seq;        // AckQuery / Record
+    char val = 0;   // Put / GetOk / AckQuery / Record
+    auto key() const { return std::make_tuple(kind, req, seq.key(), val); }
+};
+struct AbdPhase {
+    int phase = 0;  // 0 None, 1 Phase1, 2 Phase2
+    u64 request_id = 0;
+    Id requester = 0;
+    std::optional<char> write_or_read;  // Phase1 `write`, Phase2 `read`
+    std::map<Id, std::pair<Seq, char>> responses;  // Phase1
+    std::set<Id> acks;                              // Phase2
+    auto key() const { return std::make_tuple(phase, request_id, requester, write_or_read, responses.size(), acks.size()); }
+    bool operator==(const AbdPhase& o) const {
+        if (phase != o.phase) return false;
+        if (phase == 0) return true;
+        if (request_id != o.request_id || requester != o.requester || write_or_read != o.write_or_read) return false;
+        if (responses.size() != o.responses.size() || acks != o.acks) return false;
+        auto a = responses.begin(), b = o.responses.begin();
+        for (; a != responses.end(); ++a, ++b)
+            if (a->first != b->first || !(a->second.first == b->second.first) || a->second.second != b->second.second) return false;
+        return true;
+    }
+};
+struct AbdActorState {
+    bool server = true;
+    // server (AbdState)
+    Seq seq;
+    char val = 0;
+    AbdPhase phase;
+    // client (RegisterActorState::Client)
+    std::optional<u64> awaiting;
+    u64 op_count = 0;
+};
+
+struct AbdSys {
+    static constexpr int NET = 16;
+    using AState = AbdActorState;
+    using Msg = AbdMsg;
+    using Hist = paxos::History;
+    size_t client_count = 2, server_count = 2;
+    bool lossy = false, duplicating = false;  // `.duplicating_network(DuplicatingNetwork::No)`
+
+    size_t actor_count() const { return server_count + client_count; }
+    std::vector<Envelope<Msg>> init_network() const { return {}; }
+    Hist init_history() const { return Hist{}; }
+    std::vector<Id> peers(Id i) const {  // model_peers (model.rs:79-84)
+        std::vector<Id> p;
+        for (Id j = 0; j < server_count; ++j)
+            if (j != i) p.push_back(j);
+        return p;
+    }
+    size_t majority() const { return server_count / 2 + 1; }  // majority(peers.len() + 1)
+
+    AState on_start(Id id, Out<Msg>& o) const {
+        AState s;
+        if (id < server_count) {
+            s.server = true;
+            s.seq = Seq{0, id};  // AbdActor::on_start
+            return s;
+        }
+        // RegisterActor::Client::on_start, put_count 1 (register.rs:130-160)
+        s.server = false;
+        const u64 req = 1 * id;
+        o.send(id % server_count, Msg{A_PUT, req, {}, (char)('A' + (id - server_count))});
+        s.awaiting = req;
+        s.op_count = 1;
+        return s;
+    }
+    bool on_msg(Id id, AState& st, Id src, const Msg& m, Out<Msg>& o) const {
+        if (!st.server) {  // RegisterActor::Client::on_msg (register.rs:170-200)
+            if (!st.awaiting) return false;
+            if (m.kind == A_PUTOK && m.req == *st.awaiting) {
+                const u64 req = (st.op_count + 1) * id;
+                if (st.op_count < 1) o.send((id + st.op_count) % server_count, Msg{A_PUT, req, {}, (char)('Z' - (id - server_count))});
+                else o.send((id + st.op_count) % server_count, Msg{A_GET, req, {}, 0});
+                st.awaiting = req;
+                st.op_count += 1;
+                return true;
+            }
+            if (m.kind == A_GETOK && m.req == *st.awaiting) {
+                st.awaiting.reset();
+                st.op_count += 1;
+                return true;
+            }
+            return false;
+        }
+        // AbdActor::on_msg (examples/linearizable-register.rs:66-173)
+        switch (m.kind) {
+            case A_PUT:
+            case A_GET:
+                if (st.phase.phase != 0) return false;
+                o.broadcast(peers(id), Msg{A_QUERY, m.req, {}, 0});
+                st.phase = AbdPhase{};
+                st.phase.phase = 1;
+                st.phase.request_id = m.req;
+                st.phase.requester = src;
+                if (m.kind == A_PUT) st.phase.write_or_read = m.val;
+                st.phase.responses[id] = {st.seq, st.val};
+                return true;
+            case A_QUERY:
+                o.send(src, Msg{A_ACKQUERY, m.req, st.seq, st.val});
+                return false;
+            case A_ACKQUERY: {
+                if (!(st.phase.phase == 1 && st.phase.request_id == m.req)) return false;
+                st.phase.responses[src] = {m.seq, m.val};
+                if (st.phase.responses.size() == majority()) {
+                    // max_by_key(seq): sequencers are distinct
+                    auto best = st.phase.responses.begin();
+                    for (auto it = st.phase.responses.begin(); it != st.phase.responses.end(); ++it)
+                        if (best->second.first < it->second.first) best = it;
+                    Seq seq = best->second.first;
+                    char val;
+                    std::optional<char> read;
+                    if (st.phase.write_or_read) {
+                        seq = Seq{seq.clock + 1, id};
+                        val = *st.phase.write_or_read;
+                    } else {
+                        val = best->second.second;
+                        read = val;
+                    }
+                    o.broadcast(peers(id), Msg{A_RECORD, st.phase.request_id, seq, val});
+                    if (st.seq < seq) {
+                        st.seq = seq;
+                        st.val = val;
+                    }
+                    AbdPhase p2;
+                    p2.phase = 2;
+                    p2.request_id = st.phase.request_id;
+                    p2.requester = st.phase.requester;
+                    p2.write_or_read = read;
+                    p2.acks.insert(id);
+                    st.phase = p2;
+                }
+                return true;  // `state.to_mut()` before the quorum test
+            }
+            case A_RECORD:
+                o.send(src, Msg{A_ACKRECORD, m.req, {}, 0});
+                if (st.seq < m.seq) {
+                    st.seq = m.seq;
+                    st.val = m.val;
+                    return true;
+                }
+                return false;
+            case A_ACKRECORD: {
+                if (!(st.phase.phase == 2 && st.phase.request_id == m.req && !st.phase.acks.count(src))) return false;
+                st.phase.acks.insert(src);
+                if (st.phase.acks.size() == majority()) {
+                    if (st.phase.write_or_read) o.send(st.phase.requester, Msg{A_GETOK, st.phase.request_id, {}, *st.phase.write_or_read});
+                    else o.send(st.phase.requester, Msg{A_PUTOK, st.phase.request_id, {}, 0});
+                    st.phase = AbdPhase{};
+                }
+                return true;
+            }
+            default:
+                return false;
+        }
+    }
+    bool on_timeout(Id, AState&, Out<Msg>&) const { return false; }
+    // record_invocations / record_returns (src/actor/register.rs:37-87)
+    std::optional<Hist> record_out(const Hist& h, const Envelope<Msg>& e) const {
+        if (e.msg.kind == A_GET) {
+            Hist x = h;
+            x.on_invoke(e.src, paxos::Op{false, 0});
+            return x;
+        }
+        if (e.msg.kind == A_PUT) {
+            Hist x = h;
+            x.on_invoke(e.src, paxos::Op{true, e.msg.val});
+            return x;
+        }
+        return std::nullopt;
+    }
+    std::optional<Hist> record_in(const Hist& h, const Envelope<Msg>& e) const {
+        if (e.msg.kind == A_GETOK) {
+            Hist x = h;
+            x.on_return(e.dst, paxos::Ret{false, e.msg.val});
+            return x;
+        }
+        if (e.msg.kind == A_PUTOK) {
+            Hist x = h;
+            x.on_return(e.dst, paxos::Ret{true, 0});
+            return x;
+        }
+        return std::nullopt;
+    }
+    template <class State>
+    bool within_boundary(const State&) const { return true; }
+    template <class M>
+    std::vector<Property<M>> properties() const {  // examples/linearizable-register.rs:218-228
+        using P = Property<M>;
+        using S = typename M::State;
+        return {
+            P::always("linearizable", [](const M&, const S& s) { return s.history.linearizable(); }),
+            P::sometimes("value chosen", [](const M&, const S& s) {
+                for (auto& e : s.network)
+                    if (e.msg.kind == A_GETOK && e.msg.val != 0) return true;
+                return false;
+            }),
+        };
+    }
+    void hash_actor(const AState& a, Hasher& h) const {
+        h.write_bool(a.server);
+        if (a.server) {
+            h.write_u64(a.seq.clock);
+            h.write_u64(a.seq.id);
+            h.write_u64((u8)a.val);
+            h.write_u64((u64)a.phase.phase);
+            if (a.phase.phase) {
+                h.write_u64(a.phase.request_id);
+                h.write_u64(a.phase.requester);
+                h.write_bool(a.phase.write_or_read.has_value());
+                h.write_u64((u8)a.phase.write_or_read.value_or(0));
+                h.write_usize(a.phase.responses.size());
+                for (auto& [k, v] : a.phase.responses) {
+                    h.write_u64(k);
+                    h.write_u64(v.first.clock);
+                    h.write_u64(v.first.id);
+                    h.write_u64((u8)v.second);
+                }
+                h.write_usize(a.phase.acks.size());
+                for (auto k : a.phase.acks) h.write_u64(k);
+            }
+        } else {
+            h.write_bool(a.awaiting.has_value());
+            h.write_u64(a.awaiting.value_or(0));
+            h.write_u64(a.op_count);
+        }
+    }
+    void hash_history(const Hist& H, Hasher& h) const {
+        h.write_bool(H.valid);
+        for (auto& [t, cs] : H.by_thread) {
+            h.write_u64(t);
+            h.write_usize(cs.size());
+            for (auto& c : cs) {
+                h.write_usize(c.last.size());
+                for (auto& [k, v] : c.last) {
+                    h.write_u64(k);
+                    h.write_u64(v);
+                }
+                h.write_bool(c.op.write);
+                h.write_u64((u8)c.op.value);
+                h.write_bool(c.ret.write_ok);
+                h.write_u64((u8)c.ret.value);
+            }
+        }
+        h.write_u64(0xFFFF);
+        for (auto& [t, f] : H.in_flight) {
+            h.write_u64(t);
+            h.write_usize(f.last.size());
+            for (auto& [k, v] : f.last) {
+                h.write_u64(k);
+                h.write_u64(v);
+            }
+            h.write_bool(f.op.write);
+            h.write_u64((u8)f.op.value);
+        }
+    }
+    void hash_msg(const Msg& m, Hasher& h) const {
+        h.write_u64(m.kind);
+        h.write_u64(m.req);
+        h.write_u64(m.seq.clock);
+        h.write_u64(m.seq.id);
+        h.write_u64((u8)m.val);
+    }
+    // value code: '\0' 0, 'A'.. 1..
+    static i64 vcode(char c) { return c ? (i64)(c - 'A' + 1) : 0; }
+    i64 msg_code(const Msg& m) const {
+        return ((((i64)m.req * 8 + (i64)m.seq.clock) * 8 + (i64)m.seq.id) * 8 + vcode(m.val)) * 8 + (i64)m.kind;
+    }
+    // per actor: server [seq clock, seq id, val, phase, request id, requester, write/read (-1 None),
+    // response of server j (-1 absent, else clock*64 + id*8 + val) for j < server_count, acks mask];
+    // client [awaiting (-1 None), op_count, then zeros to the server width]
+    int actor_width() const { return 7 + (int)server_count + 1; }
+    void describe_actor(Id, const AState& a, std::vector<i64>& d) const {
+        const size_t o = d.size();
+        if (a.server) {
+            d.push_back((i64)a.seq.clock);
+            d.push_back((i64)a.seq.id);
+            d.push_back(vcode(a.val));
+            d.push_back(a.phase.phase);
+            d.push_back(a.phase.phase ? (i64)a.phase.request_id : 0);
+            d.push_back(a.phase.phase ? (i64)a.phase.requester : 0);
+            d.push_back(a.phase.phase && a.phase.write_or_read ? vcode(*a.phase.write_or_read) : -1);
+            for (Id j = 0; j < server_count; ++j) {
+                auto it = a.phase.responses.find(j);
+                d.push_back(a.phase.phase != 1 || it == a.phase.responses.end()
+                                ? -1 : (i64)it->second.first.clock * 64 + (i64)it->second.first.id * 8 + vcode(it->second.second));
+            }
+            i64 mask = 0;
+            if (a.phase.phase == 2)
+                for (auto k : a.phase.acks) mask |= 1ll << k;
+            d.push_back(mask);
+        } else {
+            d.push_back(a.awaiting ? (i64)*a.awaiting : -1);
+            d.push_back((i64)a.op_count);
+        }
+        d.resize(o + (size_t)actor_width(), 0);
+    }
+    void describe_history(const Hist&, std::vector<i64>&) const {}  // summarised by `linearizable`
+    std::string format_msg(const Msg& m) const {
+        auto ch = [](char c) {
+            if (!c) return std::string("'\\u{0}'");
+            return std::string("'") + c + "'";
+        };
+        auto seq = [](const Seq& s) { return "(" + std::to_string(s.clock) + ", Id(" + std::to_string(s.id) + "))"; };
+        switch (m.kind) {
+            case A_PUT: return "Put(" + std::to_string(m.req) + ", " + ch(m.val) + ")";
+            case A_GET: return "Get(" + std::to_string(m.req) + ")";
+            case A_PUTOK: return "PutOk(" + std::to_string(m.req) + ")";
+            case A_GETOK: return "GetOk(" + std::to_string(m.req) + ", " + ch(m.val) + ")";
+            case A_QUERY: return "Internal(Query(" + std::to_string(m.req) + "))";
+            case A_ACKQUERY: return "Internal(AckQuery(" + std::to_string(m.req) + ", " + seq(m.seq) + ", " + ch(m.val) + "))";
+            case A_RECORD: return "Internal(Record(" + std::to_string(m.req) + ", " + seq(m.seq) + ", " + ch(m.val) + "))";
+            case A_ACKRECORD: return "Internal(AckRecord(" + std::to_string(m.req) + "))";
+        }
+        return "?";
+    }
+};
+
+using PingPongModel = ActorModel<PingPongSys>;
+using FixtureModel = ActorModel<FixtureSys>;
+using AbdModel = ActorModel<AbdSys>;
+
+}  // namespace actor
+}  // namespace oracle

@@ -3,6 +3,7 @@
 
 #include "models.hpp"
 #include "paxos.hpp"
+#include "actor.hpp"
 #include "dfs.hpp"
 
 using namespace oracle;
@@ -12,7 +13,8 @@ namespace {
 thread_local std::string g_last_error;
 
 // Model ids are shared with include/stateright_gpu.h (SR_MODEL_*).
-enum ModelId { LINEAR_EQUATION = 1, BINARY_CLOCK = 2, TWO_PHASE = 3, INCREMENT = 4, INCREMENT_LOCK = 5, DGRAPH = 6, PAXOS = 7, SYM_TOY = 8 };
+enum ModelId { LINEAR_EQUATION = 1, BINARY_CLOCK = 2, TWO_PHASE = 3, INCREMENT = 4, INCREMENT_LOCK = 5, DGRAPH = 6, PAXOS = 7, SYM_TOY = 8,
+               PINGPONG = 9, ACTOR_FIXTURE = 10, ABD = 11 };
 
 struct HandleBase {
     virtual ~HandleBase() = default;
@@ -149,6 +151,25 @@ auto with_model(int model, const i64* p, int np, F&& f) {
         case DGRAPH: return f(make_dgraph(p, np));
         case PAXOS: return f(paxos::PaxosModel{(size_t)p[0], 3});
         case SYM_TOY: return f(SymToy{});
+        case PINGPONG: {  // (max_nat, lossy, duplicating, maintains_history)
+            actor::PingPongModel m;
+            m.sys.max_nat = (u32)p[0];
+            m.sys.lossy = np > 1 && p[1];
+            m.sys.duplicating = np > 2 ? p[2] != 0 : true;
+            m.sys.maintains_history = np > 3 && p[3];
+            return f(m);
+        }
+        case ACTOR_FIXTURE: {  // (kind: 0 undeliverable, 1 timer)
+            actor::FixtureModel m;
+            m.sys.kind = (int)p[0];
+            return f(m);
+        }
+        case ABD: {  // (client_count, server_count)
+            actor::AbdModel m;
+            m.sys.client_count = (size_t)p[0];
+            m.sys.server_count = np > 1 ? (size_t)p[1] : 2;
+            return f(m);
+        }
     }
     throw std::runtime_error("unknown model id " + std::to_string(model));
 }

@@ -9,7 +9,9 @@ property evaluation) runs as hand-written HIP kernels for gfx950 behind the C AB
 include/stateright_gpu.h; this package is the host-side mirror of the reference API.
 """
 from .checker import CheckerBuilder, CheckerError, Expectation, GpuBfsChecker, Path, PathRecorder, StateRecorder
-from .models import BinaryClock, DGraph, Increment, IncrementLock, LinearEquation, Paxos, TwoPhaseSys
+from .models import (AbdRegister, ActorFixture, BinaryClock, DGraph, Increment, IncrementLock, LinearEquation, Paxos,
+                     PingPong, TwoPhaseSys)
 
 __all__ = ["CheckerBuilder", "CheckerError", "Expectation", "GpuBfsChecker", "Path", "PathRecorder", "StateRecorder",
-           "BinaryClock", "Increment", "IncrementLock", "LinearEquation", "TwoPhaseSys"]
+           "AbdRegister", "ActorFixture", "BinaryClock", "DGraph", "Increment", "IncrementLock", "LinearEquation", "Paxos",
+           "PingPong", "TwoPhaseSys"]

@@ -4,6 +4,7 @@
 #include "engine.hpp"
 #include "dgraph.hpp"
 #include "paxos.hpp"
+#include "actor.hpp"
 
 namespace sr {
 
@@ -50,6 +51,29 @@ static std::unique_ptr<EngineBase> make_model_engine(int model, const i64* p, in
             return std::make_unique<E<Paxos>>(Paxos::make((int)p[0], o.device), o, args...);
         case SR_MODEL_DGRAPH:
             return std::make_unique<E<DGraph>>(DGraph::make(p, np, o.device), o, args...);
+        case SR_MODEL_PINGPONG: {
+            need(1);
+            if (p[0] < 0 || p[0] > 7) throw Error(SR_ERR_UNSUPPORTED, "ping-pong: max_nat must be in 0..=7 (16 network slots)");
+            PingPong m;
+            m.max_nat = (u32)p[0];
+            m.lossy = np > 1 && p[1] != 0;
+            m.duplicating = np > 2 ? p[2] != 0 : true;
+            m.maintains_history = np > 3 && p[3] != 0;
+            return std::make_unique<E<PingPong>>(m, o, args...);
+        }
+        case SR_MODEL_ACTOR_FIXTURE: {
+            need(1);
+            if (p[0] < 0 || p[0] > 1) throw Error(SR_ERR_ARG, "actor fixture: kind 0 (undeliverable) or 1 (timer)");
+            ActorFixture m;
+            m.kind = (int)p[0];
+            return std::make_unique<E<ActorFixture>>(m, o, args...);
+        }
+        case SR_MODEL_ABD: {
+            need(1);
+            AbdRegister m;
+            static_cast<act::AbdSys&>(m) = act::AbdSys::make((int)p[0], np > 1 ? (int)p[1] : 2, o.device);
+            return std::make_unique<E<AbdRegister>>(m, o, args...);
+        }
     }
     throw Error(SR_ERR_ARG, "unknown model id " + std::to_string(model));
 }

@@ -142,3 +142,50 @@ class DGraph(_Model):
             p.append(len(path))
             p.extend(path)
         return p
+
+
+class PingPong(_Model):
+    """The reference's ping-pong actor fixture `PingPongCfg { max_nat, maintains_history }
+    .into_model()` (src/actor/actor_test_util.rs:4-96) with `.lossy_network(..)` and
+    `.duplicating_network(..)` (src/actor/model.rs:52-66; the reference defaults to a lossless
+    duplicating network). Action ids: Deliver = envelope code * 4 + 1, Drop = code * 4 + 2
+    (stateright_amd/csrc/actor.hpp)."""
+    MODEL_ID = N.SR_MODEL_PINGPONG
+
+    def __init__(self, max_nat, maintains_history=False, lossy=False, duplicating=True):
+        self.max_nat, self.maintains_history = max_nat, maintains_history
+        self.lossy, self.duplicating = lossy, duplicating
+
+    def lossy_network(self, on=True):
+        return PingPong(self.max_nat, self.maintains_history, on, self.duplicating)
+
+    def duplicating_network(self, on=True):
+        return PingPong(self.max_nat, self.maintains_history, self.lossy, on)
+
+    def params(self):
+        return [self.max_nat, int(self.lossy), int(self.duplicating), int(self.maintains_history)]
+
+
+class ActorFixture(_Model):
+    """The reference's one-actor fixtures (src/actor/model.rs:697-733): kind 0 =
+    `handles_undeliverable_messages` (an init envelope to Id 99), kind 1 = `resets_timer`."""
+    MODEL_ID = N.SR_MODEL_ACTOR_FIXTURE
+
+    def __init__(self, kind):
+        self.kind = kind
+
+    def params(self):
+        return [self.kind]
+
+
+class AbdRegister(_Model):
+    """The ABD linearizable register `AbdModelCfg { client_count, server_count }.into_model()`
+    (examples/linearizable-register.rs:192-229): AbdActor servers, RegisterActor clients, a
+    non-duplicating network and a linearizability history."""
+    MODEL_ID = N.SR_MODEL_ABD
+
+    def __init__(self, client_count=2, server_count=2):
+        self.client_count, self.server_count = client_count, server_count
+
+    def params(self):
+        return [self.client_count, self.server_count]

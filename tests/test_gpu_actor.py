@@ -1,0 +1,158 @@
+"""ActorModel on the GPU (stateright_amd/csrc/actor.hpp): the reference's actor goldens
+(src/actor/model.rs:515-734, src/checker/explorer.rs:370-416, examples/linearizable-register.rs:
+236-279) through the C ABI, and parity with the CPU oracle's generic ActorModel restatement
+(oracle/actor.hpp, pinned by the same goldens in tests/test_oracle_actor.py): counts, discoveries,
+and in FIFO order the exact visit order and discovery paths (the oracle iterates the network set
+in sorted order, as the GPU encoding does; the reference's HashSet order is parity unpinned)."""
+import json
+import urllib.request
+
+import pytest
+
+from actor_golden import (ABD, ABD_VALUE_CHOSEN_NAMES, ABD_VALUE_CHOSEN_PATH, ACTOR_FIXTURE, PINGPONG, PINGPONG_14,
+                          PINGPONG_DROP_FIRST_PING, pingpong_params)
+from oracle_lib import OracleRun
+
+pytestmark = pytest.mark.gpu
+sr = pytest.importorskip("stateright_amd")
+
+
+def model(mid, params):
+    if mid == PINGPONG:
+        return sr.PingPong(params[0], maintains_history=bool(params[3]), lossy=bool(params[1]),
+                           duplicating=bool(params[2]))
+    if mid == ACTOR_FIXTURE:
+        return sr.ActorFixture(params[0])
+    return sr.AbdRegister(*params)
+
+
+CASES = [
+    (PINGPONG, pingpong_params(1, lossy=True)),
+    (PINGPONG, pingpong_params(5, lossy=True)),
+    (PINGPONG, pingpong_params(5, lossy=False, duplicating=False)),
+    (PINGPONG, pingpong_params(5, lossy=False)),
+    (PINGPONG, pingpong_params(2, lossy=False, duplicating=False, maintains_history=True)),
+    (PINGPONG, pingpong_params(3, lossy=True, duplicating=False, maintains_history=True)),
+    (PINGPONG, pingpong_params(7, lossy=True)),
+    (ACTOR_FIXTURE, [0]),
+    (ACTOR_FIXTURE, [1]),
+    (ABD, [1, 2]),
+    (ABD, [2, 2]),
+    (ABD, [1, 3]),
+    (ABD, [3, 2]),
+]
+
+
+def ids(c):
+    return {PINGPONG: "pingpong", ACTOR_FIXTURE: "fixture", ABD: "abd"}[c[0]] + "-" + "-".join(map(str, c[1]))
+
+
+_oracle = {}
+
+
+def oracle(mid, params, **kw):
+    key = (mid, tuple(params), tuple(sorted(kw.items())))
+    if key not in _oracle:
+        _oracle[key] = OracleRun(mid, params, **kw)
+    return _oracle[key]
+
+
+@pytest.mark.parametrize("order", ["fifo", "fast", "auto"])
+@pytest.mark.parametrize("case", CASES, ids=ids)
+def test_counts_match_oracle(case, order):
+    mid, params = case
+    o = oracle(mid, params)
+    c = model(mid, params).checker().order(order).spawn_bfs().join()
+    assert (c.unique_state_count(), c.state_count(), c.max_depth()) == (o.unique_state_count, o.state_count, o.max_depth)
+    assert sorted(c.discoveries()) == o.discovery_names()
+    assert c.is_done() == o.is_done
+
+
+@pytest.mark.parametrize("case", CASES, ids=ids)
+def test_fifo_visits_and_paths_identical(case):
+    mid, params = case
+    o = oracle(mid, params, record_visits=True)
+    rec = sr.StateRecorder()
+    c = model(mid, params).checker().order("fifo").visitor(rec).spawn_bfs().join()
+    assert rec.states == o.visits()
+    for name in o.discovery_names():
+        assert c.discovery(name).action_ids == o.discovery_actions(name)
+        assert c.discovery(name).states == o.discovery_states(name)
+
+
+def test_pingpong_visits_expected_states():
+    # src/actor/model.rs:515-610
+    rec = sr.StateRecorder()
+    c = sr.PingPong(1).lossy_network().checker().visitor(rec).spawn_bfs().join()
+    assert c.unique_state_count() == 14
+    assert len(rec.states) == 14 and set(rec.states) == PINGPONG_14
+
+
+def test_pingpong_lossy_duplicating():
+    # src/actor/model.rs:612-642: 4 094 states, delta within 1 holds, and losing the first Ping is a
+    # counterexample of "must reach max" (never reached, ends at a terminal state)
+    c = sr.PingPong(5).lossy_network().checker().spawn_bfs().join()
+    assert c.unique_state_count() == 4_094
+    c.assert_no_discovery("delta within 1")
+    c.assert_discovery("must reach max", PINGPONG_DROP_FIRST_PING)
+    assert c.action_name(PINGPONG_DROP_FIRST_PING[0]) == "Drop(Envelope { src: Id(0), dst: Id(1), msg: Ping(0) })"
+
+
+def test_pingpong_perfect_delivery():
+    # src/actor/model.rs:644-656 and 673-694
+    c = sr.PingPong(5).duplicating_network(False).checker().spawn_bfs().join()
+    assert c.unique_state_count() == 11
+    c.assert_no_discovery("must reach max")
+    assert c.discovery("must exceed max").last_state()[:2] == (5, 5)
+
+
+def test_pingpong_can_reach_max():
+    # src/actor/model.rs:658-671
+    c = sr.PingPong(5).checker().spawn_bfs().join()
+    assert c.unique_state_count() == 11
+    assert c.discovery("can reach max").last_state()[:2] == (4, 5)
+
+
+def test_actor_fixtures():
+    # src/actor/model.rs:697-707 (undeliverable: 1 state), 709-733 (timer: 2 states)
+    assert sr.ActorFixture(0).checker().spawn_bfs().join().unique_state_count() == 1
+    rec = sr.StateRecorder()
+    assert sr.ActorFixture(1).checker().visitor(rec).spawn_bfs().join().unique_state_count() == 2
+    assert [s[1:3] for s in rec.states] == [(1, 1), (1, 0)]  # is_timer_set [true], then [false]
+
+
+def test_abd_linearizable_register():
+    # examples/linearizable-register.rs:236-258
+    for order in ("fifo", "fast", "auto"):
+        c = sr.AbdRegister(2, 2).checker().order(order).spawn_bfs().join()
+        c.assert_properties()
+        c.assert_discovery("value chosen", ABD_VALUE_CHOSEN_PATH)
+        assert c.unique_state_count() == 544
+    assert [c.action_name(a) for a in ABD_VALUE_CHOSEN_PATH] == ABD_VALUE_CHOSEN_NAMES
+
+
+def test_explorer_status_pingpong():
+    # src/checker/explorer.rs:370-416 (smoke_test_status) over the served routes
+    ex = sr.PingPong(2, maintains_history=True).duplicating_network(False).checker().serve(("127.0.0.1", 0), block=False)
+    try:
+        ex.checker.join()
+        with urllib.request.urlopen(ex.url + "/.status", timeout=30) as r:
+            st = json.loads(r.read())
+        assert st["done"] is True
+        assert (st["state_count"], st["unique_state_count"]) == (5, 5)
+        found = {(exp, name): enc is not None for exp, name, enc in st["properties"]}
+        assert found == {("Always", "delta within 1"): False, ("Sometimes", "can reach max"): True,
+                         ("Eventually", "must reach max"): False, ("Eventually", "must exceed max"): True,
+                         ("Always", "#in <= #out"): False, ("Eventually", "#out <= #in + 1"): False}
+        assert st["recent_path"].startswith("[")
+    finally:
+        ex.shutdown()
+
+
+def test_partitioned_actor_models():
+    # the partitioned search over 3 virtual partitions (FAST order; no `eventually` properties)
+    for mid, params in [(ABD, [2, 2]), (ABD, [3, 2])]:
+        o = oracle(mid, params)
+        c = model(mid, params).checker().partitions(3).spawn_bfs().join()
+        assert (c.unique_state_count(), c.state_count(), c.max_depth()) == (o.unique_state_count, o.state_count, o.max_depth)
+        assert sorted(c.discoveries()) == o.discovery_names()
