@@ -43,11 +43,13 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-# Random-access ceilings of the visited set on MI355X, measured by scripts/microbench_random.hip
-# (profiles/r01_microbench_random_access.txt, table 64 MB-2 GB): the 80/20 load/CAS probe mix and
-# random 64-bit atomicCAS.
-PROBE_MIX_PEAK = 49.0e9
-RANDOM_CAS_PEAK = 26.9e9
+# Uniform random-access rates into a 256 MiB table (scripts/microbench_random.hip,
+# profiles/r01_microbench_random_access.txt): reported beside the kernel's probe and claim rates
+# for context only. They are NOT ceilings of the kernel (its probes hit L2 29% of the time and its
+# linear-probe steps stay in a line), so they enter no fraction; the memory-side bounds are the
+# PMC-measured request ceilings of profiles/pmc_ceiling.json.
+UNIFORM_LOAD_RATE = 55.6e9
+UNIFORM_CAS_RATE = 26.7e9
 BIG_LEVEL_MS = 0.1  # levels whose expand launch takes >= 100 us count as "big"
 
 
@@ -169,18 +171,29 @@ def cpu_baseline(args, n):
     }
 
 
-def pmc_traffic(n, world):
-    """Beyond-L2 bytes per expand launch from the committed rocprofv3 PMC passes of this bench
-    (scripts/pmc_traffic.sh -> profiles/pmc_traffic.json), or None if not measured for this config."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+def pmc_files(label, world):
+    """The committed rocprofv3 PMC measurements of this configuration's expand kernel and the
+    measured memory-side request ceilings (scripts/gpu_roofline.sh -> profiles/pmc_traffic.json,
+    profiles/pmc_ceiling.json), or (None, None, reason): both files must carry the source digest of
+    the engine being benchmarked (stateright_amd.build.source_digest), so a measurement of other
+    sources is never reported."""
+    from stateright_amd.build import source_digest
+    if world != 1:
+        return None, None, "PMC files are single-GPU measurements"
+    digest = source_digest()
     try:
-        with open(path) as f:
-            d = json.load(f)
-        if d.get("rm_count") == n and d.get("n_gpus", 1) == world:
-            return d["bytes_per_launch"], d.get("atomics_per_launch")
-    except (OSError, ValueError, KeyError):
-        pass
-    return None, None
+        with open(os.path.join(ROOT, "profiles", "pmc_traffic.json")) as f:
+            traffic = json.load(f)
+        with open(os.path.join(ROOT, "profiles", "pmc_ceiling.json")) as f:
+            ceiling = json.load(f)
+    except (OSError, ValueError):
+        return None, None, "no PMC files"
+    if traffic.get("source_digest") != digest or ceiling.get("source_digest") != digest:
+        return None, None, f"PMC files measured on other sources ({traffic.get('source_digest')} != {digest})"
+    cfg = traffic.get("configs", {}).get(label)
+    if not cfg:
+        return None, None, f"no PMC measurement of {label}"
+    return cfg, ceiling, traffic.get("source_digest")
 
 
 def measure_config4(args, world, comm, dev, barrier):
@@ -391,29 +404,35 @@ def main():
         alg_bytes /= world  # this rank's share of the check's algorithmic bytes
     kernel_s = kernel_ms * 1e-3
     achieved_gbps = alg_bytes / kernel_s / 1e9 if kernel_ms else 0.0
-    traffic, atomics = pmc_traffic(n, world) if args.model == "2pc" and not partitioned else (None, None)
+    pmc, ceiling, pmc_note = pmc_files(label, world) if not partitioned else (None, None, "partitioned run")
     launch_s = avg_launch_ms * 1e-3
     probe_rate = probes / kernel_s if kernel_s and probes else None
     cas_rate = cas / kernel_s if kernel_s and cas else None
+    # Fractions of bounds the kernel cannot exceed: algorithmic bytes against HBM's 8 TB/s, and
+    # (when a PMC measurement of these sources exists) its memory-side read / write / atomic
+    # requests per second against the largest rates the random-access microbenchmark reached.
     fracs = {"hbm_bytes": achieved_gbps / HBM_PEAK_GBPS}
-    if probe_rate:
-        fracs["probe_rate"] = probe_rate / PROBE_MIX_PEAK
-    if cas_rate:
-        fracs["cas_rate"] = cas_rate / RANDOM_CAS_PEAK
-    # The big levels alone (launches >= BIG_LEVEL_MS of the profiled check): their probes and CAS
-    # claims (counting pass, same levels in the same order) per second of their event time, against
-    # the random-transaction mix ceiling. The whole-check rates above are diluted by small levels,
-    # which are latency-bound.
+    ea = None
+    if pmc and launch_s:
+        ea = {"read_req_per_s": pmc["ea_read_req_per_launch"] / launch_s,
+              "write_req_per_s": pmc["ea_write_req_per_launch"] / launch_s,
+              "atomic_req_per_s": pmc["ea_atomic_req_per_launch"] / launch_s,
+              "read_req_peak": ceiling["ea_read_req_per_s"], "write_req_peak": ceiling["ea_write_req_per_s"],
+              "atomic_req_peak": ceiling["ea_atomic_req_per_s"]}
+        fracs["ea_read_requests"] = ea["read_req_per_s"] / ceiling["ea_read_req_per_s"]
+        fracs["ea_write_requests"] = ea["write_req_per_s"] / ceiling["ea_write_req_per_s"]
+        fracs["ea_atomic_requests"] = ea["atomic_req_per_s"] / ceiling["ea_atomic_req_per_s"]
+        fracs["hbm_traffic"] = pmc["bytes_per_launch"] / launch_s / 1e9 / HBM_PEAK_GBPS
+    traffic = pmc["bytes_per_launch"] if pmc else None
+    # The big levels alone (launches >= BIG_LEVEL_MS of the profiled check): probes and CAS claims
+    # per second of their event time (context: the whole-check rates are diluted by small levels).
     big_rate = None
     if prof and len(per_launch) == len(prof):
         bi = [i for i, (ms, _) in enumerate(prof) if ms >= BIG_LEVEL_MS]
         bt = sum(prof[i][0] for i in bi) * 1e-3
         bp, bc = sum(per_launch[i][0] for i in bi), sum(per_launch[i][1] for i in bi)
         if bt > 0 and bp:
-            big_rate = {"launches": len(bi), "probe_rate": bp / bt, "cas_rate": bc / bt,
-                        "transactions_per_s": (bp + bc) / bt, "peak": PROBE_MIX_PEAK,
-                        "frac": (bp + bc) / bt / PROBE_MIX_PEAK}
-            fracs["big_level_transactions"] = big_rate["frac"]
+            big_rate = {"launches": len(bi), "probe_rate": bp / bt, "cas_rate": bc / bt}
     # Per-level split of the last profiled check: big levels, small levels, and the span between
     # launches (level boundaries: dispatch, ramp/drain, host planning).
     big = sum(ms for ms, _ in prof if ms >= BIG_LEVEL_MS)
@@ -445,11 +464,10 @@ def main():
         },
         "state_count_per_sec": float(final_state_count) * (1 if partitioned else world) * args.steps / elapsed,
         "roofline": {
-            # HBM-side, but by random transactions (8-byte probes and CAS claims that each move a
-            # memory line), not by bytes: `limiter` names the largest measured fraction
+            # HBM-side: random visited-set probes and claims (8-byte accesses that each move a
+            # memory line) and streamed frontiers. `limiter` names the largest fraction of a bound
+            # the kernel cannot exceed.
             "bound": "hbm",
-            "bound_detail": "random HBM transactions (visited-set probes + CAS claims) against the "
-                            "microbenchmarked 49 G/s mix ceiling; bytes/s against 8 TB/s is `frac`",
             "limiter": max(fracs, key=fracs.get),
             "fractions": fracs,
             "kernel": ("expand_route" if partitioned else "expand_fast") +
@@ -459,16 +477,17 @@ def main():
             "unit": "GB/s",
             "frac": achieved_gbps / HBM_PEAK_GBPS,
             "traffic": traffic,
-            # the random-transaction view: visited-set probes and claims per second of kernel time
-            # (device counters), against the microbenchmarked ceilings
+            "traffic_gbps": traffic / launch_s / 1e9 if traffic and launch_s else None,
+            "memory_side_requests": ea,
+            "pmc": pmc_note,
+            # context: visited-set probes and claims per second of kernel time (device counters)
+            # beside the uniform random-access rates of one 256 MiB table
             "probe_rate": probe_rate,
-            "probe_peak": PROBE_MIX_PEAK if probe_rate else None,
             "cas_rate": cas_rate,
-            "cas_peak": RANDOM_CAS_PEAK if cas_rate else None,
+            "uniform_load_rate": UNIFORM_LOAD_RATE,
+            "uniform_cas_rate": UNIFORM_CAS_RATE,
             "probes_per_step": probes / args.steps,
             "big_levels": big_rate,
-            "traffic_gbps": traffic / launch_s / 1e9 if traffic and launch_s else None,
-            "atomics_per_s": atomics / launch_s if atomics and launch_s else None,
             "avg_launch_ms": avg_launch_ms,
             "launches_per_step": launches / args.steps,
             "algorithmic_bytes_per_step": alg_bytes / args.steps,

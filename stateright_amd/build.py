@@ -7,7 +7,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 SRC = os.path.join(HERE, "csrc", "engine.hip")
 CSRC = [os.path.join(HERE, "csrc", f) for f in ("engine.hip", "engine.hpp", "kernels.hpp", "kernels_dist.hpp",
-                                                 "dist.hpp", "models.hpp", "device.hpp", "paxos.hpp", "dgraph.hpp")]
+                                                 "dist.hpp", "models.hpp", "device.hpp", "paxos.hpp", "dgraph.hpp",
+                                                 "actor.hpp")]
 HEADERS = [os.path.join(ROOT, "include", f) for f in ("stateright_gpu.h", "stateright_gpu_model.hpp")]
 OUT = os.path.join(HERE, "libstateright_gpu.so")
 PLUGINS = {"sliding_puzzle": os.path.join(ROOT, "examples", "plugins", "sliding_puzzle.hip")}
@@ -41,3 +42,14 @@ def build(force=False, verbose=False, plugins=True):
 
 if __name__ == "__main__":
     print(build(force=True, verbose=True))
+
+
+def source_digest():
+    """sha256 (16 hex digits) of the engine's sources (CSRC + HEADERS): measurement files under
+    profiles/ are stamped with it, and bench.py ignores a file measured on other sources."""
+    import hashlib
+    h = hashlib.sha256()
+    for path in sorted(CSRC + HEADERS):
+        with open(path, "rb") as f:
+            h.update(os.path.basename(path).encode() + b"\0" + f.read())
+    return h.hexdigest()[:16]

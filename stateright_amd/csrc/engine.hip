@@ -754,3 +754,25 @@ void sr_gpu_bfs_free(sr_bfs* b) {
 }
 
 }  // extern "C"
+
+#if SR_TIMELINE
+// ---- diagnostic build only (SR_TIMELINE=1): expand_fast's per-workgroup timeline ----
+static u64* g_timeline_host_ptr = nullptr;
+extern "C" int64_t sr_timeline_reset(int32_t device) {
+    const size_t words = (size_t)TL_LAUNCHES * TL_BLOCKS * TL_STAMPS;
+    if (hipSetDevice(device) != hipSuccess) return SR_ERR_HIP;
+    if (!g_timeline_host_ptr) {
+        if (hipMalloc(&g_timeline_host_ptr, words * 8) != hipSuccess) return SR_ERR_HIP;
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_timeline), &g_timeline_host_ptr, sizeof(u64*)) != hipSuccess) return SR_ERR_HIP;
+    }
+    if (hipMemset(g_timeline_host_ptr, 0, words * 8) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return SR_ERR_HIP;
+    return (int64_t)words;
+}
+extern "C" int64_t sr_timeline_fetch(int32_t device, uint64_t* out, int64_t cap) {
+    const size_t words = (size_t)TL_LAUNCHES * TL_BLOCKS * TL_STAMPS;
+    if (!g_timeline_host_ptr || hipSetDevice(device) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return SR_ERR_HIP;
+    if (out && hipMemcpy(out, g_timeline_host_ptr, std::min<size_t>(words, (size_t)cap) * 8, hipMemcpyDeviceToHost) != hipSuccess)
+        return SR_ERR_HIP;
+    return (int64_t)words;
+}
+#endif

@@ -594,6 +594,30 @@ __device__ __forceinline__ u32 select_bit(u64 m, u32 k) {
     return pos;
 }
 
+// Diagnostic build only (SR_TIMELINE=1, scripts/build_timeline.sh): expand_fast's lane 0 of wave 0
+// stamps s_memrealtime (a 100 MHz clock shared by every CU) at each link of its workgroup's chain
+// of dependent round trips, after draining its memory counters, into g_timeline[launch seq % 64]
+// [block][stamp]; scripts/timeline.py turns them into the per-level breakdown. The production
+// library is built with SR_TIMELINE=0 and contains none of it.
+#ifndef SR_TIMELINE
+#define SR_TIMELINE 0
+#endif
+constexpr u32 TL_STAMPS = 16, TL_BLOCKS = 2048, TL_LAUNCHES = 64;
+#if SR_TIMELINE
+__device__ u64* g_timeline;
+#define SR_TL(k)                                                            \
+    do {                                                                    \
+        if (tl_on) {                                                        \
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");     \
+            tl_ts[k] = __builtin_amdgcn_s_memrealtime();                    \
+        }                                                                   \
+    } while (0)
+#else
+#define SR_TL(k) \
+    do {         \
+    } while (0)
+#endif
+
 // FAST order: expand parents [lo, hi) of the frontier.
 //
 // Load-balanced over SUCCESSORS: each wave loads 64 parents, counts their enabled actions, and
@@ -640,9 +664,31 @@ __global__ void __launch_bounds__(256) expand_fast(M m, const u64* __restrict__ 
     // The previous level's publish and the slot reset (SlotWork) run in one extra workgroup, the
     // last of the grid: in a small level any workgroup that expands parents is on the critical
     // path, and the publish waits for its host stores to be acknowledged.
+#if SR_TIMELINE
+    // stamps: 0 entry, 1 frontier size known, 2 first parents loaded, 3 first successor map, 4 first
+    // probes returned, 5 first claims done, 6 chunks done, 7 stage reserved, 8 stage written,
+    // 9 exit (service workgroup: 0 entry, 9 exit)
+    const bool tl_on = threadIdx.x == 0 && blockIdx.x < TL_BLOCKS && g_timeline;
+    u64 tl_ts[TL_STAMPS];
+#pragma unroll
+    for (u32 k = 0; k < TL_STAMPS; ++k) tl_ts[k] = 0;
+    bool tl_first_chunk = true, tl_first_round = true;
+    auto tl_store = [&]() {
+        if (!tl_on) return;
+        u64* t = g_timeline + ((u64)(seq % TL_LAUNCHES) * TL_BLOCKS + blockIdx.x) * TL_STAMPS;
+#pragma unroll
+        for (u32 k = 0; k < TL_STAMPS; ++k) t[k] = tl_ts[k];
+        t[TL_STAMPS - 1] = (u64)gridDim.x << 32 | (u64)(hi - lo);
+    };
+#endif
+    SR_TL(0);
     const bool svc = sw.pub || sw.zero;
     if (svc && blockIdx.x == gridDim.x - 1) {
         if (threadIdx.x < 64) slot_service<M::NPROPS>(sw, threadIdx.x);
+        SR_TL(9);
+#if SR_TIMELINE
+        tl_store();
+#endif
         return;
     }
     const u32 nblk = gridDim.x - (svc ? 1u : 0u);  // workgroups that expand parents
@@ -658,6 +704,7 @@ __global__ void __launch_bounds__(256) expand_fast(M m, const u64* __restrict__ 
         next_par += nn;
         next_cap = next_cap > nn ? next_cap - nn : 0u;
     }
+    SR_TL(1);
     // Each wave takes ppw = 2^ppw_log2 <= 64 parents (small levels use fewer parents per wave so
     // that their successors spread over more waves: shorter per-lane probe chains). The grid
     // strides over chunks of 4 waves (a pipelined launch is sized from an estimate of the frontier).
@@ -695,6 +742,9 @@ __global__ void __launch_bounds__(256) expand_fast(M m, const u64* __restrict__ 
         for (int i = 0; i < MW; ++i) mk[i] = 0;
         if (lane < ppw && r < hi) {
             m.enabled(s, mk);
+#if SR_TIMELINE
+            if (tl_first_chunk) SR_TL(2);
+#endif
             if constexpr (has_self_loops<M>::value) {
                 // self-loops are counted here and never generated (has_self_loops)
                 u64 sl[MW];
@@ -709,6 +759,9 @@ __global__ void __launch_bounds__(256) expand_fast(M m, const u64* __restrict__ 
             for (int i = 0; i < W; ++i) pst[wid][lane * W + i] = s[i];
 #pragma unroll
             for (int i = 0; i < MW; ++i) cnt += __popcll(mk[i]);
+#if SR_TIMELINE
+            if (tl_first_chunk) SR_TL(10);
+#endif
         }
         // wave-inclusive scan of the counts
         u32 incl = cnt;
@@ -720,6 +773,9 @@ __global__ void __launch_bounds__(256) expand_fast(M m, const u64* __restrict__ 
         u32 nidx = incl - cnt;  // this parent's next successor index (its entries are [excl, incl))
         const u32 total = __shfl(incl, 63, 64);
         if (lane == 0) enabled += total;
+#if SR_TIMELINE
+        if (tl_first_chunk) SR_TL(11);
+#endif
 
         for (u32 w0 = 0; w0 < total; w0 += MAPCAP) {
         const u32 wend = min(total, w0 + MAPCAP);
@@ -733,7 +789,14 @@ __global__ void __launch_bounds__(256) expand_fast(M m, const u64* __restrict__ 
             smap[wid][nidx - w0] = (u16)((u32)lane | a << 6);
             ++nidx;
         }
+#if SR_TIMELINE
+        if (tl_first_chunk) SR_TL(12);
+#endif
         wave_lds_sync();  // pst and the map are the wave's own: no workgroup barrier
+#if SR_TIMELINE
+        if (tl_first_chunk) SR_TL(3);
+        tl_first_chunk = false;
+#endif
 
         for (u32 it = w0; it < wend; it += 64 * PB) {
             u64 ns[PB][W], cur[PB];
@@ -779,6 +842,9 @@ __global__ void __launch_bounds__(256) expand_fast(M m, const u64* __restrict__ 
                 cur[j] = ok[j] ? probe_load<POL>(&t.keys[pk[j].home]) : 0;
                 if constexpr (STATS) probes += ok[j];
             }
+#if SR_TIMELINE
+            if (tl_first_round) SR_TL(4);
+#endif
             bool nw[PB];
 #pragma unroll
             for (int j = 0; j < PB; ++j) {
@@ -789,6 +855,10 @@ __global__ void __launch_bounds__(256) expand_fast(M m, const u64* __restrict__ 
                 find_or_claim_from<POL>(t, pk[j], cur[j], &nw[j], &lc->err, STATS ? &probes : nullptr,
                                         STATS ? &cas : nullptr);
             }
+#if SR_TIMELINE
+            if (tl_first_round) SR_TL(5);
+            tl_first_round = false;
+#endif
             // Append the new states of this round, aggregated per wave: one LDS atomic reserves the
             // wave's span of the stage; what does not fit goes straight to the next frontier with
             // ONE global atomic for the wave (never one per state).
@@ -853,6 +923,7 @@ __global__ void __launch_bounds__(256) expand_fast(M m, const u64* __restrict__ 
             if (threadIdx.x == 0) stage_n = 0;
         }
     }
+    SR_TL(6);
     const bool repair = (sw.flags & SLOT_REPAIR) != 0;  // successors were counted by the first pass
     u32 total_succ = repair ? 0u : block_sum(succ, scratch);
     u32 total_enabled = repair ? 0u : block_sum(enabled, scratch);
@@ -863,6 +934,7 @@ __global__ void __launch_bounds__(256) expand_fast(M m, const u64* __restrict__ 
         base = n ? atomicAdd(&lc->claims, n) : 0;
         add_stats(lc, total_succ, total_enabled, total_probes, total_cas);
     }
+    SR_TL(7);
     __syncthreads();
     for (u32 i = threadIdx.x; i < n; i += blockDim.x) {
         u32 pos = base + i;
@@ -879,7 +951,12 @@ __global__ void __launch_bounds__(256) expand_fast(M m, const u64* __restrict__ 
     }
     };
     level(frontier, lo, hi, next, next_par, next_cap, lc, undiscovered);
+    SR_TL(8);
     if (hc) publish<M::NPROPS>(lc, hc, seq, reset != 0, nullptr);  // a slotted launch is published by its successor
+    SR_TL(9);
+#if SR_TIMELINE
+    tl_store();
+#endif
 }
 
 // FIFO order, pass 1: insert-or-find every successor and record (level, parent rank, slot) in
