@@ -576,6 +576,26 @@ __device__ __forceinline__ u32 block_sum(u32 v, u32* scratch) {
     return t;
 }
 
+// Sums of a and b over the workgroup, returned to every thread (one LDS round for both).
+__device__ __forceinline__ void block_sum2(u32 a, u32 b, u32* scratch, u32& ta, u32& tb) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        a += __shfl_xor(a, d, 64);
+        b += __shfl_xor(b, d, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        scratch[2 * (threadIdx.x >> 6)] = a;
+        scratch[2 * (threadIdx.x >> 6) + 1] = b;
+    }
+    __syncthreads();
+    ta = tb = 0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
+        ta += scratch[2 * w];
+        tb += scratch[2 * w + 1];
+    }
+    __syncthreads();
+}
+
 // k-th set bit (0-based) of a 64-bit mask with popcount(m) > k.
 __device__ __forceinline__ u32 select_bit(u64 m, u32 k) {
     // the half first, then five steps on 32 bits (u64 shifts and masks cost two VALU each)
@@ -658,7 +678,7 @@ __global__ void __launch_bounds__(256) expand_fast(M m, const u64* __restrict__ 
     constexpr u32 MAPCAP = 1024;
     static_assert(MW * 64 <= 1024, "action ids must fit 10 bits");
     __shared__ u16 smap[4][MAPCAP];
-    __shared__ u32 stage_n, base, scratch[4];
+    __shared__ u32 stage_n, base, scratch[8];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     if (threadIdx.x == 0) stage_n = 0;
     // The previous level's publish and the slot reset (SlotWork) run in one extra workgroup, the
@@ -692,6 +712,19 @@ __global__ void __launch_bounds__(256) expand_fast(M m, const u64* __restrict__ 
         return;
     }
     const u32 nblk = gridDim.x - (svc ? 1u : 0u);  // workgroups that expand parents
+    // Each wave takes ppw = 2^ppw_log2 <= 64 parents (small levels use fewer parents per wave so
+    // that their successors spread over more waves: shorter per-lane probe chains). The grid
+    // strides over chunks of 4 waves (a pipelined launch is sized from an estimate of the frontier).
+    ppw_log2 = min(ppw_log2, PPW_LOG2_MAX);
+    const u32 ppw = 1u << ppw_log2;
+    const u64 chunk = (u64)(blockDim.x >> 6) << ppw_log2;
+    // The wave's first parents. A pipelined launch issues their load before it knows the frontier
+    // size (any row below next_cap is inside the arena; rows past the frontier are never used), so
+    // the two round trips overlap instead of following each other.
+    const u64 r_first = lo + (u64)blockIdx.x * chunk + ((u64)wid << ppw_log2) + lane;
+    u64 first[W];
+    const bool spec_first = sw.prev_n && lane < (int)ppw && r_first < next_cap;
+    if (spec_first) load_state<W>(frontier, r_first, first);
     if (sw.prev_n) {
         // Pipelined launch (enqueued before the host saw the previous level finish): the frontier
         // is the previous level's claims, and the next level starts right after it. Behind a level
@@ -705,12 +738,6 @@ __global__ void __launch_bounds__(256) expand_fast(M m, const u64* __restrict__ 
         next_cap = next_cap > nn ? next_cap - nn : 0u;
     }
     SR_TL(1);
-    // Each wave takes ppw = 2^ppw_log2 <= 64 parents (small levels use fewer parents per wave so
-    // that their successors spread over more waves: shorter per-lane probe chains). The grid
-    // strides over chunks of 4 waves (a pipelined launch is sized from an estimate of the frontier).
-    ppw_log2 = min(ppw_log2, PPW_LOG2_MAX);
-    const u32 ppw = 1u << ppw_log2;
-    const u64 chunk = (u64)(blockDim.x >> 6) << ppw_log2;
     const u32 fmask = filt_log2 ? (1u << filt_log2) - 1 : 0;
     if (lo + (u64)blockIdx.x * chunk < hi)  // blocks past the frontier only take their ticket
         for (u32 i = threadIdx.x; i < (fmask ? fmask + 1 : 0u); i += blockDim.x) filt[i] = 0;
@@ -722,9 +749,11 @@ __global__ void __launch_bounds__(256) expand_fast(M m, const u64* __restrict__ 
     // chunk's probes instead of stalling the chunk start.
     const u64 cstride = (u64)nblk * chunk;
     u64 nxt[W];
-    {
-        const u64 r0 = lo + (u64)blockIdx.x * chunk + ((u64)wid << ppw_log2) + lane;
-        if (lane < (int)ppw && r0 < hi) load_state<W>(frontier, r0, nxt);
+    if (spec_first) {
+#pragma unroll
+        for (int i = 0; i < W; ++i) nxt[i] = first[i];
+    } else if (lane < (int)ppw && r_first < hi) {
+        load_state<W>(frontier, r_first, nxt);
     }
     for (u64 c0 = lo + (u64)blockIdx.x * chunk; c0 < hi; c0 += cstride) {
         const u32 wave0 = (u32)(c0 + ((u64)wid << ppw_log2));  // first parent of the wave
@@ -779,6 +808,28 @@ __global__ void __launch_bounds__(256) expand_fast(M m, const u64* __restrict__ 
 
         for (u32 w0 = 0; w0 < total; w0 += MAPCAP) {
         const u32 wend = min(total, w0 + MAPCAP);
+        if (MW <= 2 && ppw <= 8) {
+            // Few parents per wave (small levels): the 64 lanes fill the map together, entry j
+            // from parent p (the last whose exclusive offset is <= j) and its (j - offset)-th
+            // enabled slot, instead of every parent lane writing its own successors one by one
+            // (up to ~20 dependent iterations for a wave that is alone on its CU).
+            const u32 excl = incl - cnt;
+            for (u32 j0 = w0; j0 < wend; j0 += 64) {
+                const u32 j = j0 + (u32)lane;
+                u32 p = 0;
+#pragma unroll
+                for (int q = 1; q < 8; ++q) {
+                    const u32 ex = (u32)__shfl((int)excl, q, 64);
+                    if ((u32)q < ppw && ex <= j) p = (u32)q;
+                }
+                const u32 k = j - (u32)__shfl((int)excl, (int)p, 64);
+                const u64 m0 = __shfl(mk[0], (int)p, 64);
+                const u64 m1 = MW > 1 ? __shfl(mk[MW > 1 ? 1 : 0], (int)p, 64) : 0ull;
+                const u32 c0 = (u32)__popcll(m0);
+                const u32 a = k < c0 ? select_bit(m0, k) : 64u + select_bit(m1, k - c0);
+                if (j < wend) smap[wid][j - w0] = (u16)(p | a << 6);
+            }
+        } else
         // this window's entries: each parent lane writes its successors with index in [w0, wend)
         while (nidx < wend && nidx < incl) {
             u32 a = 0;
@@ -925,13 +976,18 @@ __global__ void __launch_bounds__(256) expand_fast(M m, const u64* __restrict__ 
     }
     SR_TL(6);
     const bool repair = (sw.flags & SLOT_REPAIR) != 0;  // successors were counted by the first pass
-    u32 total_succ = repair ? 0u : block_sum(succ, scratch);
-    u32 total_enabled = repair ? 0u : block_sum(enabled, scratch);
+    // The stage's span of the next frontier is reserved first; the round trip of that atomic
+    // overlaps the block's reduction of its statistics (both sums in one pass).
+    __syncthreads();  // the stage's fill is final
+    const u32 n = min(stage_n, (u32)STAGE);
+    u32 my_base = 0;
+    if (threadIdx.x == 0 && n) my_base = atomicAdd(&lc->claims, n);
+    u32 total_succ, total_enabled;
+    block_sum2(repair ? 0u : succ, repair ? 0u : enabled, scratch, total_succ, total_enabled);
     u32 total_probes = STATS ? block_sum(probes, scratch) : 0u;
     u32 total_cas = STATS ? block_sum(cas, scratch) : 0u;
-    const u32 n = min(stage_n, (u32)STAGE);
     if (threadIdx.x == 0) {
-        base = n ? atomicAdd(&lc->claims, n) : 0;
+        base = my_base;
         add_stats(lc, total_succ, total_enabled, total_probes, total_cas);
     }
     SR_TL(7);
