@@ -12,8 +12,12 @@ N > 1: one process per GPU. If WORLD_SIZE is not set, this script starts
 `python -m torch.distributed.run --nproc-per-node N ... bench.py ...` as a CHILD process (before
 anything touches the GPU) and exits with its status; under the launcher every rank checks
 WORLD_SIZE == N. The ranks partition ONE check: the visited set and the frontier
-are hash-partitioned by fingerprint owner; after a few replicated head levels, every BFS level does
-ONE RCCL all-to-all of fixed-capacity buckets whose headers carry every rank's row.
+are hash-partitioned by fingerprint owner; after a few replicated head levels, every BFS level is
+exchanged DIRECTLY: each rank's expand kernel stores its records into the owners' receive buffers
+through IPC-mapped peer pointers and raises a per-level flag there, and each owner's stream waits
+for the flags on the device (no collective and no host step per level). SR_DIRECT=0, or a failed
+one-off probe of the peer path, falls back to ONE RCCL all-to-all of fixed-capacity buckets per
+level (whose headers carry every rank's row). DESIGN.md §6.
 The workload stays 2pc N=9 at every N ("scaling": "strong"); value = unique states of the check /
 max-over-ranks time. At N > 1 the line also carries `replicas`: the whole node's throughput on
 independent full checks (one per GPU and step, weak scaling). `--mode replicas` makes that the
@@ -196,9 +200,16 @@ def pmc_files(label, world):
     return cfg, ceiling, traffic.get("source_digest")
 
 
+def exchange_label(st):
+    """How a partitioned check's levels exchanged their records (sr_stats.pipelined)."""
+    return {2: "direct exchange: peer stores + device flags per level",
+            1: "RCCL all-to-all per level", 0: "synchronous: all-gather + exchange per level"}.get(st["pipelined"], "?")
+
+
 def measure_config4(args, world, comm, dev, barrier):
     """BASELINE.json configs[3]: 2pc N=11 (366 993 408 unique states, 34 levels) partitioned over
-    the `world` GPUs (one process each, RCCL all-to-all per level), or on the one GPU at N=1."""
+    the `world` GPUs (one process each; the direct exchange, or RCCL all-to-all with SR_DIRECT=0),
+    or on the one GPU at N=1."""
     from stateright_amd import TwoPhaseSys
     n = 11
     want = 6 ** n + 4 ** n + 2 ** n
@@ -224,7 +235,7 @@ def measure_config4(args, world, comm, dev, barrier):
         el = comm.allreduce([el], "max")[0]
     st = c.stats()
     return {"workload": f"2pc N={n} spawn_bfs, full check per step ({want} unique states; BASELINE configs[3])",
-            "parallelism": f"partitioned{world} (RCCL all-to-all per level)" if world > 1 else "1 GPU",
+            "parallelism": f"partitioned{world} ({exchange_label(st)})" if world > 1 else "1 GPU",
             "n_gpus": world, "steps": args.config4_steps, "ms_per_step": el / args.config4_steps * 1e3,
             "value": want * args.config4_steps / el, "unit": "unique states/s",
             "restarts": st["restarts"], "head_levels": st["head_levels"], "records_routed": st["records_routed"]}
@@ -456,7 +467,7 @@ def main():
             "model": args.model,
             "rm_count": n if args.model == "2pc" else None,
             "order": "fast" if partitioned else args.order,
-            "parallelism": (f"partitioned{world} (RCCL all-to-all per level)" if partitioned else
+            "parallelism": (f"partitioned{world} ({exchange_label(st)})" if partitioned else
                             f"replicas{world}" if world > 1 else "1 GPU"),
             "world_size": world,
             "comm": comm.kind() if comm is not None else None,

@@ -123,7 +123,9 @@ typedef struct sr_stats {
     uint32_t words_per_state;
     uint32_t order_used;         /* enum sr_order actually used for the reported counts          */
     uint32_t restarts;           /* capacity restarts of this check (larger buffers / synchronous) */
-    uint32_t pipelined;          /* partitioned search: 1 = levels pipelined, no host wait inside */
+    uint32_t pipelined;          /* partitioned search: 1 = levels pipelined, no host wait inside;
+                                    2 = pipelined with the direct exchange (records stored into the
+                                    owners' buffers through peer pointers, device flags per level) */
     uint64_t records_routed;     /* partitioned search: successor records sent between partitions (all ranks) */
     uint64_t head_levels;        /* partitioned search: levels run replicated before partitioning */
     uint64_t probes;             /* visited-set slots loaded by the expand kernels (first probe + linear steps) */

@@ -32,11 +32,30 @@ def _hipcc(src, out, deps, force, verbose):
     return out
 
 
+# The cross-process check of the direct exchange's IPC path (run by tests/test_gpu_partitioned.py):
+# an executable built from the same engine headers.
+IPC_SELFTEST_SRC = os.path.join(ROOT, "scripts", "ipc_selftest.hip")
+IPC_SELFTEST = os.path.join(ROOT, "scripts", "ipc_selftest")
+
+
+def _hipcc_exe(src, out, deps, force, verbose):
+    if not force and os.path.exists(out) and all(os.path.getmtime(out) >= os.path.getmtime(d) for d in deps):
+        return out
+    cmd = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-I", os.path.join(ROOT, "include"),
+           "-o", out + ".tmp", src, "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.check_call(cmd)
+    os.replace(out + ".tmp", out)
+    return out
+
+
 def build(force=False, verbose=False, plugins=True):
     _hipcc(SRC, OUT, CSRC + HEADERS, force, verbose)
     if plugins:
         for name, src in PLUGINS.items():
             _hipcc(src, plugin_path(name), CSRC + HEADERS + [src], force, verbose)
+        _hipcc_exe(IPC_SELFTEST_SRC, IPC_SELFTEST, CSRC + HEADERS + [IPC_SELFTEST_SRC], force, verbose)
     return OUT
 
 

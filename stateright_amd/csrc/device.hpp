@@ -62,6 +62,7 @@ class DevicePool {
     }
     void release_all(int dev) {
         std::lock_guard<std::mutex> g(mu_);
+        ++epoch_[dev];  // blocks may come back at the same addresses: peers' IPC mappings are stale
         for (auto& [k, v] : free_)
             if (k.first == dev) {
                 for (void* p : v) (void)hipFree(p);
@@ -76,9 +77,16 @@ class DevicePool {
         return r;
     }
 
+    // Incremented whenever blocks of `dev` are returned to the driver (direct exchange: PeerBlob).
+    uint64_t epoch(int dev) {
+        std::lock_guard<std::mutex> g(mu_);
+        return epoch_[dev];
+    }
+
   private:
     std::mutex mu_;
     std::map<std::pair<int, size_t>, std::vector<void*>> free_;
+    std::map<int, uint64_t> epoch_;
 };
 
 // RAII device buffer backed by the pool.

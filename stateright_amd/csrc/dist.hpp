@@ -34,6 +34,8 @@
 #include <condition_variable>
 #include <memory>
 #include <mutex>
+#include <set>
+#include <tuple>
 
 #include "kernels_dist.hpp"
 
@@ -66,6 +68,15 @@ __global__ void reduce_rows(const u64* in, u32 rows, u64 n, u32 op, u64* out) {
 //   broadcast    count words of root's buf to every rank's buf
 //   all_reduce   element-wise min / max / sum of count u64 words
 enum class RedOp { Min, Max, Sum };
+
+// A device buffer as another rank can name it (direct exchange): its address in the exporting
+// process, the hipMalloc allocation around it, and an IPC handle of that allocation.
+struct PeerBlob {
+    u64 ptr = 0, base = 0, size = 0;
+    u64 epoch = 0;  // the exporter's DevicePool epoch: a re-hipMalloc'd block at the same address differs
+    hipIpcMemHandle_t handle{};
+};
+
 struct Comm {
     int rank = 0, world = 1, device = 0;
     virtual ~Comm() = default;
@@ -85,12 +96,145 @@ struct Comm {
         all_reduce(one.p, 1, RedOp::Sum, s);
         SR_HIP(hipStreamSynchronize(s));
     }
+
+    // ---- direct exchange (peer pointers) ----
+    // Whether this transport can give every rank a pointer to every other rank's buffers
+    // (SR_DIRECT=0 turns the direct exchange off; RCCL's all-to-all is then the exchange).
+    virtual bool peer_capable() const { return false; }
+    // Collective: every rank's `bytes` bytes of `mine`, rank-major, into `all` (host memory).
+    virtual void share(const void* mine, size_t bytes, void* all, hipStream_t s) = 0;
+    // This rank's buffer `p` as a blob, and rank q's blob as an address usable by this rank's kernels.
+    virtual PeerBlob export_buf(void* p) const {
+        PeerBlob b;
+        b.ptr = reinterpret_cast<u64>(p);
+        return b;
+    }
+    virtual u64* map(int q, const PeerBlob& b) {
+        (void)q;
+        return reinterpret_cast<u64*>(b.ptr);
+    }
+    // Collective: the address of every rank's buffer `mine` as seen by this rank (out[q]).
+    void peer_addresses(void* mine, std::vector<u64*>& out, hipStream_t s) {
+        const PeerBlob b = export_buf(mine);
+        std::vector<PeerBlob> all(world);
+        share(&b, sizeof(b), all.data(), s);
+        out.resize(world);
+        for (int q = 0; q < world; ++q) out[q] = q == rank ? static_cast<u64*>(mine) : map(q, all[q]);
+    }
+    // Checked once per communicator (collective, on first use): a flag round trip between every
+    // pair of ranks through the direct path, with a bounded wait. Every rank gets the same answer.
+    int direct_ok = -1;
+    bool probe_direct(hipStream_t s);
+};
+
+inline bool direct_env_on() {
+    const char* e = std::getenv("SR_DIRECT");
+    return !(e && std::atoi(e) == 0);
+}
+// peer_wait's bound in ticks of the 100 MHz real-time counter (SR_PEER_TIMEOUT_MS, default 20 s)
+inline u64 peer_timeout_ticks() {
+    const char* e = std::getenv("SR_PEER_TIMEOUT_MS");
+    const u64 ms = e && std::atoll(e) > 0 ? (u64)std::atoll(e) : 20000;
+    return ms * 100000ull;
+}
+
+inline bool Comm::probe_direct(hipStream_t s) {
+    if (direct_ok >= 0) return direct_ok == 1;
+    // Every rank reaches every collective below, whatever failed on it: a local failure becomes
+    // a vote, never a skipped collective (which would leave the other ranks waiting in it).
+    auto agree = [&](u64 vote) {
+        DBuf<u64> v;
+        v.alloc(device, 1);
+        SR_HIP(hipMemcpyAsync(v.p, &vote, 8, hipMemcpyHostToDevice, s));
+        all_reduce(v.p, 1, RedOp::Min, s);
+        SR_HIP(hipMemcpyAsync(&vote, v.p, 8, hipMemcpyDeviceToHost, s));
+        SR_HIP(hipStreamSynchronize(s));
+        return vote == 1;
+    };
+    direct_ok = 0;
+    if (!agree(peer_capable() ? 1 : 0)) return false;
+    DBuf<u32> flags;
+    flags.alloc(device, world);
+    DBuf<u32*> ftab;
+    ftab.alloc(device, world);
+    DBuf<u64> lcbuf;  // a LevelCounters for the wait's error bit
+    lcbuf.alloc(device, (sizeof(LevelCounters) + 7) / 8);
+    SR_HIP(hipMemsetAsync(flags.p, 0, world * 4, s));
+    SR_HIP(hipMemsetAsync(lcbuf.p, 0, sizeof(LevelCounters), s));
+    SR_HIP(hipStreamSynchronize(s));
+    u64 ok = 1;
+    PeerBlob b;
+    try {
+        b = export_buf(flags.p);
+    } catch (const Error&) {
+        ok = 0;
+        b = PeerBlob{};
+    }
+    std::vector<PeerBlob> all(world);
+    share(&b, sizeof(b), all.data(), s);  // collective: every rank's flags are zero from here on
+    std::vector<u32*> ft(world);
+    for (int q = 0; q < world && ok; ++q) {
+        if (!all[q].ptr) ok = 0;  // that rank could not export
+        try {
+            if (ok) ft[q] = (q == rank ? flags.p : reinterpret_cast<u32*>(map(q, all[q]))) + rank;
+        } catch (const Error&) {
+            ok = 0;
+        }
+    }
+    if (!agree(ok)) return false;
+    SR_HIP(hipMemcpyAsync(ftab.p, ft.data(), world * sizeof(u32*), hipMemcpyHostToDevice, s));
+    peer_signal<<<1, 64, 0, s>>>(ftab.p, (u32)world, 7u);
+    auto* lc = reinterpret_cast<LevelCounters*>(lcbuf.p);
+    peer_wait<<<1, 64, 0, s>>>(flags.p, (u32)world, 7u, lc, 100000000ull);  // 1 s
+    SR_HIP(hipGetLastError());
+    u32 err = 0;
+    SR_HIP(hipMemcpyAsync(&err, &lc->err, 4, hipMemcpyDeviceToHost, s));
+    SR_HIP(hipStreamSynchronize(s));
+    if (err) flags.p = nullptr;  // a late peer store may still land: never reuse the block
+    direct_ok = agree(err == 0 ? 1 : 0) ? 1 : 0;
+    return direct_ok == 1;
+}
+
+// IPC export and mapping of pool buffers (the direct exchange across processes; also used by the
+// standalone cross-process check scripts/ipc_selftest.hip). A blob names the hipMalloc allocation
+// around a buffer; a process opens each (peer, allocation) once and keeps the mapping.
+struct IpcMaps {
+    static PeerBlob export_of(int device, void* p) {
+        PeerBlob b;
+        b.ptr = reinterpret_cast<u64>(p);
+        hipDeviceptr_t base = nullptr;
+        size_t size = 0;
+        SR_HIP(hipMemGetAddressRange(&base, &size, reinterpret_cast<hipDeviceptr_t>(p)));
+        b.base = reinterpret_cast<u64>(base);
+        b.size = size;
+        b.epoch = DevicePool::get().epoch(device);
+        SR_HIP(hipIpcGetMemHandle(&b.handle, reinterpret_cast<void*>(base)));
+        return b;
+    }
+    u64* open(int device, int q, const PeerBlob& b) {
+        const auto key = std::make_tuple(q, b.base, b.size, b.epoch);
+        auto it = opened.find(key);
+        if (it == opened.end()) {
+            void* m = nullptr;
+            SR_HIP(hipSetDevice(device));
+            SR_HIP(hipIpcOpenMemHandle(&m, b.handle, hipIpcMemLazyEnablePeerAccess));
+            it = opened.emplace(key, m).first;
+        }
+        return reinterpret_cast<u64*>(static_cast<char*>(it->second) + (b.ptr - b.base));
+    }
+    void close() {
+        for (auto& [k, m] : opened) (void)hipIpcCloseMemHandle(m);
+        opened.clear();
+    }
+    ~IpcMaps() { close(); }
+    std::map<std::tuple<int, u64, u64, u64>, void*> opened;
 };
 
 // One process per GPU over RCCL (xGMI).
 struct RcclComm final : Comm {
     ncclComm_t nccl = nullptr;
     ~RcclComm() override {
+        ipc.close();
         if (nccl) (void)ncclCommDestroy(nccl);
     }
     const char* kind() const override { return "rccl"; }
@@ -125,6 +269,25 @@ struct RcclComm final : Comm {
         const ncclRedOp_t o = op == RedOp::Min ? ncclMin : op == RedOp::Max ? ncclMax : ncclSum;
         SR_NCCL(ncclAllReduce(buf, buf, count, ncclUint64, o, nccl, s));
     }
+
+    // Direct exchange across processes: buffers travel as IPC handles of their hipMalloc
+    // allocation (the DevicePool hands out whole allocations), opened once per (peer, allocation).
+    bool peer_capable() const override { return direct_env_on(); }
+    void share(const void* mine, size_t bytes, void* all, hipStream_t s) override {
+        const u64 words = (bytes + 7) / 8;
+        DBuf<u64> d;
+        d.alloc(device, words * world);
+        SR_HIP(hipMemcpyAsync(d.p + (u64)rank * words, mine, bytes, hipMemcpyHostToDevice, s));
+        SR_NCCL(ncclAllGather(d.p + (u64)rank * words, d.p, words, ncclUint64, nccl, s));
+        std::vector<u64> h(words * world);
+        SR_HIP(hipMemcpyAsync(h.data(), d.p, words * world * 8, hipMemcpyDeviceToHost, s));
+        SR_HIP(hipStreamSynchronize(s));
+        for (int q = 0; q < world; ++q)
+            std::memcpy(static_cast<char*>(all) + (size_t)q * bytes, h.data() + (u64)q * words, bytes);
+    }
+    PeerBlob export_buf(void* p) const override { return IpcMaps::export_of(device, p); }
+    u64* map(int q, const PeerBlob& b) override { return ipc.open(device, q, b); }
+    IpcMaps ipc;  // peers' allocations opened in this process
 };
 
 // Ranks that are threads of ONE process (each with its own driver thread, stream and device).
@@ -135,7 +298,7 @@ struct RcclComm final : Comm {
 // ordered with HIP events across the ranks' streams. This runs the partitioned engine's real
 // multi-rank code (rank-local partitions, every collective in its order) on one GPU.
 struct LocalGroup {
-    explicit LocalGroup(int w) : world(w), slots(w), ready(w, nullptr), done(w, nullptr) {}
+    explicit LocalGroup(int w) : world(w), slots(w), ready(w, nullptr), done(w, nullptr), devices(w, 0) {}
     ~LocalGroup() {
         for (auto e : ready)
             if (e) (void)hipEventDestroy(e);
@@ -153,6 +316,7 @@ struct LocalGroup {
     const int world;
     std::vector<Slot> slots;
     std::vector<hipEvent_t> ready, done;
+    std::vector<int> devices;  // each rank's device
     std::mutex mu;
     std::condition_variable cv;
     int arrived = 0;
@@ -192,7 +356,7 @@ struct LocalComm final : Comm {
     const char* kind() const override { return "local"; }
     int nranks() const override { return g->world; }
 
-    enum Op { A2A = 1, AGATHER, EXCH, BCAST, RMIN, RMAX, RSUM };
+    enum Op { A2A = 1, AGATHER, EXCH, BCAST, RMIN, RMAX, RSUM, SHARE };
 
     // Phase 1: publish this rank's call and a "ready" event (its inputs are written once the
     // stream reaches it); every rank checks that all ranks issued the same call, then orders its
@@ -281,6 +445,38 @@ struct LocalComm final : Comm {
         SR_HIP(hipGetLastError());
         SR_HIP(hipStreamSynchronize(s));  // `all` returns to the pool at scope exit
     }
+
+    // Direct exchange between threads of one process: raw device pointers (peer access enabled
+    // when the ranks sit on different devices). share() first finishes this rank's stream, so a
+    // rank that shares a buffer it just cleared has cleared it before any peer can write to it.
+    bool peer_capable() const override { return direct_env_on(); }
+    void share(const void* mine, size_t bytes, void* all, hipStream_t s) override {
+        SR_HIP(hipStreamSynchronize(s));
+        auto& sl = g->slots[rank];
+        sl.op = SHARE;
+        sl.count = bytes;
+        sl.send = static_cast<const u64*>(mine);
+        sl.root = 0;
+        sync("share");
+        for (int q = 0; q < world; ++q) {
+            if (g->slots[q].op != SHARE || g->slots[q].count != bytes)
+                throw Error(SR_ERR_HIP, "local collective mismatch in share: rank " + std::to_string(q));
+            std::memcpy(static_cast<char*>(all) + (size_t)q * bytes, g->slots[q].send, bytes);
+        }
+        sync("share done");
+    }
+    u64* map(int q, const PeerBlob& b) override {
+        const int pd = g->devices[q];
+        if (pd != device && !peer_enabled.count(pd)) {
+            SR_HIP(hipSetDevice(device));
+            const hipError_t e = hipDeviceEnablePeerAccess(pd, 0);
+            if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) SR_HIP(e);
+            (void)hipGetLastError();
+            peer_enabled.insert(pd);
+        }
+        return reinterpret_cast<u64*>(b.ptr);
+    }
+    std::set<int> peer_enabled;
 };
 
 // Per-device resources of the partitioned engine, pooled across checks like the single-GPU
@@ -362,6 +558,9 @@ class DistEngine final : public EngineBase {
         DBuf<u32> sendc;                 // [T] records per destination (device)
         DBuf<u64> recv;
         u64 recv_cap = 0;
+        DBuf<u64> drecv[2];              // direct exchange: receive buffers by level parity, [T][S]
+        u64 drecv_words = 0;
+        DBuf<u64*> ptab[2];              // direct exchange: every owner's drecv[parity] + DIST_HDR
         LevelCounters* lc = nullptr;
         DistCtl* ctl = nullptr;          // device: frontier size + its discoveries (next level's input)
         HostCounters* hc = nullptr;      // pinned host (root level only)
@@ -752,7 +951,7 @@ class DistEngine final : public EngineBase {
                 expand_route<M, 1><<<grid, 256, route_lds(), stream_>>>(
                     m_, p.arena.p, p.apar.p, nb, p.arena_cap, p.view(), p.id, T_, p.send.p, (u32)p.bucket_cap,
                     p.sendc.p, p.lc, p.ctl, undiscovered, row, ppw_log2, filt_log2_, p.bucket_cap * REC, 0u,
-                    p.sent_mask ? p.sent.p : nullptr, p.sent_mask, rstage_recs());
+                    p.sent_mask ? p.sent.p : nullptr, p.sent_mask, rstage_recs(), nullptr, nullptr, 0u, self_rec());
                 SR_HIP(hipGetLastError());
                 if (o_.profile) SR_HIP(hipEventRecord(event(2 * stats.expand_launches + 1), stream_));
                 stats.expand_launches++;
@@ -1032,15 +1231,20 @@ class DistEngine final : public EngineBase {
     void lag_enqueue(u32 level, u64 C, u32 undiscovered, const std::vector<u64>& n_plan) {
         const u64 S = lag_S(C);
         const size_t RW = T_ + 6 + M::NPROPS;
-        bool sync = false;
-        for (auto& p : parts_) {
-            if (p.send_words < S * T_ || p.recv_words < S * T_) {
-                if (!sync) SR_HIP(hipStreamSynchronize(stream_));  // in-flight levels use the old buffers
-                sync = true;
-                const u64 words = std::max<u64>(S * T_, p.send_words * 2);
-                p.send.alloc(o_.device, words);
-                p.recv.alloc(o_.device, words);
-                p.send_words = p.recv_words = words;
+        const u32 par = xlev_ & 1, fseq = ++xlev_;
+        if (direct_) {
+            direct_buffers(S);
+        } else {
+            bool sync = false;
+            for (auto& p : parts_) {
+                if (p.send_words < S * T_ || p.recv_words < S * T_) {
+                    if (!sync) SR_HIP(hipStreamSynchronize(stream_));  // in-flight levels use the old buffers
+                    sync = true;
+                    const u64 words = std::max<u64>(S * T_, p.send_words * 2);
+                    p.send.alloc(o_.device, words);
+                    p.recv.alloc(o_.device, words);
+                    p.send_words = p.recv_words = words;
+                }
             }
         }
         for (auto& p : parts_) {
@@ -1049,14 +1253,22 @@ class DistEngine final : public EngineBase {
             const u32 grid = (u32)std::min<u64>(std::max<u64>(1, blocks_for(n_plan[p.id], 4u << ppw_log2)), route_grid_cap());
             u64* row = comm_ ? rows_mine_.p : rows_all_.p + (u64)p.id * RW;
             expand_route<M, 1><<<grid, 256, route_lds(), stream_>>>(
-                m_, p.arena.p, p.apar.p, 0, p.arena_cap, p.view(), p.id, T_, p.send.p + DIST_HDR, (u32)C, p.sendc.p,
-                p.lc, p.ctl, undiscovered, row, ppw_log2, filt_log2_, S, 1u, p.sent_mask ? p.sent.p : nullptr,
-                p.sent_mask, rstage_recs());
+                m_, p.arena.p, p.apar.p, 0, p.arena_cap, p.view(), p.id, T_, direct_ ? nullptr : p.send.p + DIST_HDR,
+                (u32)C, p.sendc.p, p.lc, p.ctl, undiscovered, row, ppw_log2, filt_log2_, S, 1u,
+                p.sent_mask ? p.sent.p : nullptr, p.sent_mask, rstage_recs(), direct_ ? p.ptab[par].p : nullptr,
+                dflags_ ? ftab_.p : nullptr, fseq, self_rec());
             SR_HIP(hipGetLastError());
             if (o_.profile) SR_HIP(hipEventRecord(event(2 * stats.expand_launches + 1), stream_));
             stats.expand_launches++;
         }
-        if (comm_) {
+        if (direct_) {
+            // the records are in the owners' buffers already; ranks on their own streams wait for
+            // every source's flag (virtual partitions share this stream: the routes ran before)
+            if (dflags_) {
+                peer_wait<<<1, 64, 0, stream_>>>(flags_.p, T_, fseq, parts_[0].lc, peer_timeout_);
+                SR_HIP(hipGetLastError());
+            }
+        } else if (comm_) {
             comm_->all_to_all(parts_[0].send.p, parts_[0].recv.p, S, stream_);
         } else {
             for (auto& dst : parts_)
@@ -1070,11 +1282,60 @@ class DistEngine final : public EngineBase {
             auto& r = ctx_->parts[p.res];
             // four records per thread on the large grid (insert_grid), one otherwise
             auto kern = ig > INSERT_GRID_MAX && W <= 2 ? insert_recv_lag<M, 4> : insert_recv_lag<M, 1>;
-            kern<<<ig, 256, 0, stream_>>>(m_, p.recv.p, S, (u32)C, p.id, T_, p.view(), p.arena.p, p.apar.p, p.arena_cap, p.lc,
-                                          undiscovered, p.ctl, r.pub_dev[p.seq & 1], p.seq);
+            kern<<<ig, 256, 0, stream_>>>(m_, direct_ ? p.drecv[par].p : p.recv.p, S, (u32)C, p.id, T_, p.view(),
+                                          p.arena.p, p.apar.p, p.arena_cap, p.lc, undiscovered, p.ctl,
+                                          r.pub_dev[p.seq & 1], p.seq);
             SR_HIP(hipGetLastError());
         }
         (void)level;
+    }
+
+    // Direct exchange: receive buffers of T slots of S words for both level parities, and every
+    // partition's table of the owners' buffers. They grow (doubling) when a level needs larger
+    // slots; every rank takes that decision at the same level (the plan is the same everywhere), and
+    // first waits until no level is in flight ANYWHERE (a collective barrier: peers may still be
+    // storing into the old buffers), then shares the new buffers' addresses.
+    void direct_buffers(u64 S) {
+        bool grow = false;
+        for (auto& p : parts_) grow |= p.drecv_words < S * T_;
+        if (!grow) return;
+        if (comm_) comm_->barrier(stream_);
+        else SR_HIP(hipStreamSynchronize(stream_));
+        for (auto& p : parts_) {
+            const u64 words = std::max<u64>(S * T_, p.drecv_words * 2);
+            for (int k = 0; k < 2; ++k) p.drecv[k].alloc(o_.device, words);
+            p.drecv_words = words;
+        }
+        for (int k = 0; k < 2; ++k) {
+            std::vector<u64*> owners(T_);
+            if (comm_) {
+                comm_->peer_addresses(parts_[0].drecv[k].p, owners, stream_);
+            } else {
+                for (auto& q : parts_) owners[q.id] = q.drecv[k].p;
+            }
+            for (auto& o : owners) o += DIST_HDR;
+            for (auto& p : parts_) {
+                if (p.ptab[k].n < T_) p.ptab[k].alloc(o_.device, T_);
+                SR_HIP(hipMemcpyAsync(p.ptab[k].p, owners.data(), T_ * sizeof(u64*), hipMemcpyHostToDevice, stream_));
+            }
+        }
+        SR_HIP(hipStreamSynchronize(stream_));  // the host tables may go
+        direct_grows_++;
+    }
+
+    // Direct exchange with device flags (ranks on their own streams): this rank's flag words, zero
+    // before any peer may store into them (the share is collective and follows the clear on every
+    // rank), and the table of this rank's word in every owner's flags.
+    void direct_flags() {
+        flags_.alloc(o_.device, T_);
+        SR_HIP(hipMemsetAsync(flags_.p, 0, T_ * 4, stream_));
+        std::vector<u64*> owners;
+        comm_->peer_addresses(flags_.p, owners, stream_);
+        std::vector<u32*> ft(T_);
+        for (u32 q = 0; q < T_; ++q) ft[q] = reinterpret_cast<u32*>(owners[q]) + comm_->rank;
+        ftab_.alloc(o_.device, T_);
+        SR_HIP(hipMemcpyAsync(ftab_.p, ft.data(), T_ * sizeof(u32*), hipMemcpyHostToDevice, stream_));
+        SR_HIP(hipStreamSynchronize(stream_));
     }
 
     // Waits for partition p's publish of the level tagged `seq`.
@@ -1101,6 +1362,12 @@ class DistEngine final : public EngineBase {
     void lag_loop(u64& unique_total, u32& undiscovered) {
         const size_t RW = T_ + 6 + M::NPROPS;
         for (auto& p : parts_) ctx_->ensure_pub(p.res, RW * T_);
+        // the exchange of this check's levels (every rank decides the same: probe_direct is collective)
+        direct_ = direct_env_on() && (comm_ ? comm_->probe_direct(stream_) : T_ > 1);
+        dflags_ = direct_ && comm_ != nullptr;
+        xlev_ = 0;
+        stats.pipelined = direct_ ? 2u : 1u;
+        if (dflags_) direct_flags();
         const u64 cmin = lag_cmin_;
         glob_prev_ = 0;
         // What the plan knows (the same on every rank): exact frontier sizes up to the last rows
@@ -1197,6 +1464,8 @@ class DistEngine final : public EngineBase {
             // one level later, the receiver's) error bit is in these rows on every rank.
             if (glob_err & ERR_TABLE_FULL) throw Error(SR_ERR_CAPACITY, "visited set probe limit exceeded");
             if (glob_err & ERR_FRONTIER_OVERFLOW) throw Error(SR_ERR_CAPACITY, "frontier or send bucket overflow");
+            if (glob_err & ERR_PEER_TIMEOUT)
+                throw Error(SR_ERR_HIP, "direct exchange: a source's records did not arrive within SR_PEER_TIMEOUT_MS");
             for (u32 q = 0; q < T_; ++q) {
                 u64 r = 0;
                 for (u32 s2 = 0; s2 < T_; ++s2) r += all[s2 * RW + q];
@@ -1459,10 +1728,14 @@ class DistEngine final : public EngineBase {
     }
     double rec_ratio_ = 4.0;  // remote records per parent, last level
     // Records staged per chunk in LDS (none with one partition), and expand_route's dynamic LDS.
-    u32 rstage_recs() const { return T_ > 1 ? rstage_words_ / REC : 0u; }
+    u32 rstage_recs() const { return T_ > 1 ? rstage_words() / REC : 0u; }
+    // expand_route turns local successors into records to itself from this many partitions on
+    // (SR_SELF_RECORDS_MIN; 0 = never): its rounds then wait on no visited-set probe
+    u32 self_rec() const { return self_rec_min_ && T_ >= self_rec_min_ ? 1u : 0u; }
+    u32 self_rec_min_ = std::getenv("SR_SELF_RECORDS_MIN") ? (u32)std::atoi(std::getenv("SR_SELF_RECORDS_MIN")) : 5u;
     size_t route_lds() const {
         return (filt_log2_ ? (8u << filt_log2_) : 0u) + (size_t)rstage_recs() * (REC * 8 + 2 + 1) +
-               (size_t)route_local_stage(T_, W) * (W * 8 + 4);
+               (size_t)route_local_stage(T_, W, self_rec()) * (W * 8 + 4);
     }
     // expand_route's grid: two device residencies at its LDS footprint (expand_fast's rule); the
     // kernel strides over further parents. SR_ROUTE_GRID_MAX > 0 overrides it.
@@ -1496,11 +1769,23 @@ class DistEngine final : public EngineBase {
                                                                : (8ull << 20);
     u32 insert_grid_big_ = std::getenv("SR_INSERT_GRID") && std::atoi(std::getenv("SR_INSERT_GRID")) > 0
                                ? (u32)std::atoi(std::getenv("SR_INSERT_GRID")) : 4096u;
-    u32 rstage_words_ = std::getenv("SR_RSTAGE_WORDS") ? (u32)std::atoi(std::getenv("SR_RSTAGE_WORDS")) : 1024;
+    // record stage of expand_route (words): twice as large with self records (no local stage, and a
+    // chunk of 4 x 32 parents then fits: 2pc N=11 at T = 8 routes in 41 instead of 69 ms per check)
+    // (0 = that default; SR_RSTAGE_WORDS overrides)
+    u32 rstage_words_ = std::getenv("SR_RSTAGE_WORDS") ? (u32)std::atoi(std::getenv("SR_RSTAGE_WORDS")) : 0u;
+    u32 rstage_words() const { return rstage_words_ ? rstage_words_ : self_rec() ? 2048u : 1024u; }
     int route_ppw_env_ = std::getenv("SR_ROUTE_PPW_LOG2") ? std::atoi(std::getenv("SR_ROUTE_PPW_LOG2")) : -1;
     bool trace_ = std::getenv("SR_DIST_TRACE") != nullptr;
     Clock::time_point t_trace_ = Clock::now();
     u64 arena_grows_ = 0;
+    // direct exchange (lag_loop): on for this check, with device flags (comm ranks), pipelined
+    // levels enqueued (buffer parity and flag sequence), flags / flag table, buffer growths
+    bool direct_ = false, dflags_ = false;
+    u32 xlev_ = 0;
+    DBuf<u32> flags_;
+    DBuf<u32*> ftab_;
+    u64 peer_timeout_ = peer_timeout_ticks();
+    u64 direct_grows_ = 0;
     std::vector<u64> rows_;
     std::vector<std::vector<u64>> paths_;  // per property: the discovery path's states (gather_paths)
     bool paths_ready_ = false;

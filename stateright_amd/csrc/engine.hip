@@ -588,6 +588,7 @@ int32_t sr_dist_local_group(int32_t world, const int32_t* devices, sr_dist** out
             c->world = world;
             c->device = devices ? devices[r] : 0;
             c->g = g;
+            g->devices[r] = c->device;
             auto d = std::make_unique<sr_dist>();
             d->c = std::move(c);
             out[r] = d.release();

@@ -45,7 +45,7 @@ constexpr int MAX_PARTS = 64;  // visited-set partitions (one per GPU, or virtua
 #define SR_WIDE_STAGE_WORDS 2048
 #endif
 
-enum ErrBits { ERR_TABLE_FULL = 1, ERR_FRONTIER_OVERFLOW = 2 };
+enum ErrBits { ERR_TABLE_FULL = 1, ERR_FRONTIER_OVERFLOW = 2, ERR_PEER_TIMEOUT = 4 };
 
 // Two slot encodings ("Visited set"):
 //  * fingerprint mode (qbits == 0): a slot holds the 64-bit fingerprint. Exact for one-word states

@@ -62,21 +62,63 @@ __device__ __forceinline__ bool last_workgroup(LevelCounters* lc) {
 }
 
 // Pipelined mode: the last workgroup of a launch, told to every thread of that workgroup.
-__device__ __forceinline__ bool last_block(LevelCounters* lc) {
+// `sysrel`: the workgroup's stores went (also) to another device's memory (direct exchange), so
+// they are released at system scope before the ticket, and the last workgroup acquires them.
+__device__ __forceinline__ bool last_block(LevelCounters* lc, bool sysrel = false) {
     __shared__ u32 is_last;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (threadIdx.x == 0) is_last = take_ticket(lc);
+    if (threadIdx.x == 0) {
+        if (sysrel) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        is_last = take_ticket(lc);
+        if (sysrel && is_last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    }
     __syncthreads();
     return is_last != 0;
+}
+
+// Direct exchange: the records of a level are stored by the SOURCE's expand_route
+// straight into slot `source` of every owner's receive buffer (a peer pointer: the same device, a
+// peer device in this process, or another process's memory through IPC), and its last workgroup
+// then stores the level's flag sequence number into every owner's flag word for that source. The
+// owner waits for every source's flag with this one-wave kernel before its insert (a spinning
+// insert grid could starve the sources' expand grids of the same device), then acquires at system
+// scope. A flag is a monotonic sequence number, so a source that is already a level ahead also
+// satisfies the wait (its next level writes the other buffer parity). Bounded: after `timeout`
+// ticks of the 100 MHz real-time counter the wait gives up and sets ERR_PEER_TIMEOUT, which
+// reaches every rank through the next level's rows.
+__global__ void peer_wait(const u32* flags, u32 nparts, u32 seq, LevelCounters* lc, u64 timeout) {
+    const u32 q = threadIdx.x;
+    bool ok = q >= nparts;
+    const u64 t0 = __builtin_amdgcn_s_memrealtime();
+    while (!ok) {
+        const u32 v = __hip_atomic_load(&flags[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if ((int)(v - seq) >= 0) {
+            ok = true;
+            break;
+        }
+        if (__builtin_amdgcn_s_memrealtime() - t0 > timeout) break;
+        __builtin_amdgcn_s_sleep(2);
+    }
+    if (!ok) atomicOr(&lc->err, (u32)ERR_PEER_TIMEOUT);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+}
+
+// Direct exchange, one-off check of a transport (sr_dist probe): rank `me` stores `seq` into flag
+// word `me` of every rank's flag array (ftab[q]) after a system-scope release.
+__global__ void peer_signal(u32* const* ftab, u32 nparts, u32 seq) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    for (u32 q = threadIdx.x; q < nparts; q += blockDim.x)
+        __hip_atomic_store(ftab[q], seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Local new states expand_route stages per chunk (states of W words): a partition keeps ~1/T of its
 // new states (a growth level of 2pc makes ~3 per parent, 768 per 256-parent chunk), so the stage
 // shrinks with T and leaves its LDS to the record stage: LDS per block sets residency, and the
 // probes of this kernel are latency-bound.
-__host__ __device__ __forceinline__ u32 route_local_stage(u32 nparts, int W) {
-    return (nparts <= 1 ? 1024u : nparts == 2 ? 512u : 256u) / (u32)W;
+// With self records (below) nothing is inserted locally: no stage.
+__host__ __device__ __forceinline__ u32 route_local_stage(u32 nparts, int W, u32 self_rec) {
+    return self_rec ? 0u : (nparts <= 1 ? 1024u : nparts == 2 ? 512u : 256u) / (u32)W;
 }
 
 // Expands the frontier of this partition (its size n is read from ctl). Same structure as
@@ -98,14 +140,26 @@ __global__ void __launch_bounds__(256) expand_route(M m, u64* __restrict__ arena
                                                     u64* __restrict__ send, u32 bucket_cap, u32* send_counts,
                                                     LevelCounters* lc, DistCtl* ctl, u32 undiscovered, u64* row,
                                                     u32 ppw_log2, u32 filt_log2, u64 bucket_stride, u32 lag,
-                                                    u64* __restrict__ sent, u64 sent_mask, u32 rs) {
+                                                    u64* __restrict__ sent, u64 sent_mask, u32 rs,
+                                                    u64* const* ptab, u32* const* ftab, u32 fseq, u32 self_rec) {
+    // self_rec: successors owned by this partition become records too (to its own slot), so this
+    // kernel probes nothing and has no global round trip per round of successors: with many
+    // partitions 1/T of the lanes probed and the whole wave waited for them. The insert kernel
+    // then probes every successor, with its batched probes.
+    // Destinations. Exchanged buckets (ptab == nullptr): owner q's records go to this partition's
+    // own send bucket q, send + q * bucket_stride. Direct exchange: straight into slot my_part of
+    // owner q's receive buffer, ptab[q] + my_part * bucket_stride (both past the header; the row
+    // goes into the HDR words before it), and with ftab the level's flag to every owner at the end.
     constexpr int W = M::W, MW = M::MW, REC = W;
+    __shared__ u64* sdst[MAX_PARTS];
+    for (u32 q = threadIdx.x; q < nparts; q += blockDim.x)
+        sdst[q] = ptab ? ptab[q] + (u64)my_part * bucket_stride : send + (u64)q * bucket_stride;
     // Dynamic LDS: [filter: 2^filt_log2 fingerprints][record stage: rs x REC words][local stage:
     // ls x W words][its parents' frontier ranks: ls u32][record ranks: rs u16][record owners: rs u8].
     // rs (records staged per chunk, all owners) is chosen on the host: 0 with one partition, so the
     // one-partition launch keeps expand_fast's occupancy; ls = route_local_stage(nparts).
     extern __shared__ u64 dyn[];
-    const u32 RSTAGE = rs, STAGE = route_local_stage(nparts, W);
+    const u32 RSTAGE = rs, STAGE = route_local_stage(nparts, W, self_rec);
     u64* filt = dyn;
     u64* rstage = dyn + (filt_log2 ? (1u << filt_log2) : 0u);
     u64* stage = rstage + (u64)rs * REC;
@@ -130,7 +184,8 @@ __global__ void __launch_bounds__(256) expand_route(M m, u64* __restrict__ arena
     const u64 gid_base = ((u64)my_part << GID_SHIFT) + nb;
     const u32 ppw = 1u << ppw_log2;
     const u32 fmask = filt_log2 ? (1u << filt_log2) - 1 : 0;
-    if (threadIdx.x == 0) stage_n = rstage_n = 0;
+    __shared__ u32 sent_any;  // this workgroup stored records (direct exchange: release them)
+    if (threadIdx.x == 0) stage_n = rstage_n = sent_any = 0;
     for (u32 q = threadIdx.x; q < nparts; q += blockDim.x) ocnt[q] = 0;
     for (u32 i = threadIdx.x; i < (fmask ? fmask + 1 : 0u); i += blockDim.x) filt[i] = 0;
 
@@ -227,7 +282,7 @@ __global__ void __launch_bounds__(256) expand_route(M m, u64* __restrict__ arena
                     }
                 }
                 own[j] = ok[j] ? owner_of(key[j], nparts) : my_part;
-                rem[j] = ok[j] && own[j] != my_part;
+                rem[j] = ok[j] && (self_rec || own[j] != my_part);
             }
             // One memory round trip per round: a local successor's visited-set probe and a remote
             // one's sent-cache lookup are issued together (the lookup used to be resolved before
@@ -310,6 +365,7 @@ __global__ void __launch_bounds__(256) expand_route(M m, u64* __restrict__ arena
                 }
                 // overflow (rare): per-wave reservations, owner by owner
                 u64 om = __ballot(rem[j] && rbelow >= rin);
+                if (om && lane == 0) sent_any = 1;
                 while (om) {
                     const int leader = __builtin_ctzll(om);
                     const u32 q = __shfl(own[j], leader, 64);
@@ -322,7 +378,7 @@ __global__ void __launch_bounds__(256) expand_route(M m, u64* __restrict__ arena
                     if (mine) {
                         const u32 pos = gb + __popcll(qm & lanes_below);
                         if (pos < bucket_cap) {
-                            u64* rec = &send[(u64)q * bucket_stride + (u64)pos * REC];
+                            u64* rec = sdst[q] + (u64)pos * REC;
 #pragma unroll
                             for (int x = 0; x < W; ++x) rec[x] = ns[j][x];
                         } else {
@@ -340,6 +396,7 @@ __global__ void __launch_bounds__(256) expand_route(M m, u64* __restrict__ arena
         __syncthreads();
         const u32 nl = min(stage_n, (u32)STAGE);
         const u32 nr = min(rstage_n, RSTAGE);
+        if (nr && threadIdx.x == 0) sent_any = 1;
         for (u32 i = threadIdx.x; i < nr; i += blockDim.x) rrank[i] = (u16)atomicAdd(&ocnt[rown[i]], 1u);
         if (threadIdx.x == 0 && nl) base = atomicAdd(&lc->claims, nl);
         __syncthreads();
@@ -367,14 +424,14 @@ __global__ void __launch_bounds__(256) expand_route(M m, u64* __restrict__ arena
             const u32 rr = i / REC, x = i - rr * REC;
             const u32 q = rown[rr];
             const u32 pos = obase[q] + rrank[rr];
-            if (pos < bucket_cap) send[(u64)q * bucket_stride + (u64)pos * REC + x] = rstage[rr * REC + x];
+            if (pos < bucket_cap) sdst[q][(u64)pos * REC + x] = rstage[rr * REC + x];
             else if (x == 0) atomicOr(&lc->err, (u32)ERR_FRONTIER_OVERFLOW);
         }
     }
     u32 total_succ = block_sum(succ, scratch);
     u32 total_enabled = block_sum(enabled, scratch);
     if (threadIdx.x == 0) add_stats(lc, total_succ, total_enabled);
-    if (!last_block(lc)) return;
+    if (!last_block(lc, ftab != nullptr && sent_any)) return;
     // The row, one word per thread (every source word is a round trip to the coherence point: one
     // thread loading them in turn was the floor of a small level), staged in LDS for the headers.
     __shared__ u64 srow[MAX_PARTS + 6 + MAX_PROPS];
@@ -403,9 +460,18 @@ __global__ void __launch_bounds__(256) expand_route(M m, u64* __restrict__ arena
     if (lag)  // the row travels in the header of every bucket (and so reaches every rank)
         for (u32 i = threadIdx.x; i < nparts * rw; i += blockDim.x) {
             const u32 q = i / rw, w = i - q * rw;
-            send[(u64)q * bucket_stride - DIST_HDR + w] = srow[w];
+            (sdst[q] - DIST_HDR)[w] = srow[w];
         }
     if (threadIdx.x < 64) reset_stats_tickets(lc, threadIdx.x, true);
+    if (!ftab) return;
+    // direct exchange: the headers (and, before the ticket, every workgroup's records) reach the
+    // owners before their flags
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    __syncthreads();
+    for (u32 q = threadIdx.x; q < nparts; q += blockDim.x)
+        __hip_atomic_store(ftab[q], fseq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Inserts received records [0, total) (record g at rec_at(g)), grid-strided over the workgroups:

@@ -51,11 +51,18 @@ def close(comms, checkers):
         c.close()
 
 
+@pytest.mark.parametrize("direct", ["1", "0"], ids=["direct", "alltoall"])
 @pytest.mark.parametrize("world", [2, 3])
 @pytest.mark.parametrize("case", [(TWO_PHASE, [3]), (TWO_PHASE, [5]), (TWO_PHASE, [7]), (INCREMENT_LOCK, [7]),
                                   (LINEAR_EQUATION, [2, 4, 7])],
                          ids=lambda c: f"{c[0]}-{'-'.join(map(str, c[1]))}")
-def test_ranks_match_oracle(case, world):
+def test_ranks_match_oracle(case, world, direct, monkeypatch):
+    # direct: every rank stores its records straight into the owners' receive buffers and raises
+    # a per-level flag there; the owners' streams wait for the flags on the device (no collective
+    # per level). alltoall: the collective exchange of buckets (SR_DIRECT=0).
+    monkeypatch.setenv("SR_DIRECT", direct)
+    if direct == "1":  # every level partitioned (the replicated head would explore the small cases)
+        monkeypatch.setenv("SR_HEAD_MAX", "0")
     model, params = case
     o = oracle(model, params)
     comms, cs = run_ranks(model, params, world)
@@ -64,6 +71,7 @@ def test_ranks_match_oracle(case, world):
         for ch in cs:  # every rank reports the global counts
             assert (ch.unique_state_count(), ch.state_count(), ch.max_depth()) == \
                 (o.unique_state_count, o.state_count, o.max_depth)
+            assert ch.stats()["pipelined"] == (2 if direct == "1" else 1)
         # discovery paths from ONE rank alone (no collective after join), valid on the CPU model
         last = cs[-1]
         assert sorted(last.discoveries()) == o.discovery_names()
@@ -98,7 +106,8 @@ def test_ranks_protocol_modes(sync, head, monkeypatch):
         for ch in cs:
             assert (ch.unique_state_count(), ch.state_count(), ch.max_depth()) == \
                 (o.unique_state_count, o.state_count, o.max_depth)
-            assert ch.stats()["pipelined"] == (0 if sync else 1)
+            # (2pc N=6 fits the 65536-state head entirely: no partitioned level is exchanged)
+            assert ch.stats()["pipelined"] == (0 if sync else 2 if head == "0" else 1)
         assert sorted(cs[1].discoveries()) == o.discovery_names()
     finally:
         close(comms, cs)
@@ -142,9 +151,11 @@ def test_ranks_overflow_restart_is_collective():
         close(comms, cs)
 
 
-@pytest.mark.parametrize("world", [2, 8])
-def test_ranks_bench_config(world):
-    # BASELINE config 3 (2pc N=9) on `world` ranks: closed forms, pipelined, no restart
+@pytest.mark.parametrize("world,direct", [(2, "1"), (8, "1"), (8, "0")])
+def test_ranks_bench_config(world, direct, monkeypatch):
+    # BASELINE config 3 (2pc N=9) on `world` ranks: closed forms, pipelined, no restart; the direct
+    # exchange (default) and the collective all-to-all
+    monkeypatch.setenv("SR_DIRECT", direct)
     n = 9
     want = 6 ** n + 4 ** n + 2 ** n
     comms, cs = run_ranks(TWO_PHASE, [n], world, hint=want)
@@ -154,7 +165,7 @@ def test_ranks_bench_config(world):
             assert 3 * ch.state_count() == 4 * n * 6 ** n + 3 * (n + 1) * 4 ** n + 3 * n * 2 ** n + 6
             assert ch.max_depth() == 3 * n + 1
             st = ch.stats()
-            assert st["pipelined"] == 1 and st["restarts"] == 0, st
+            assert st["pipelined"] == (2 if direct == "1" else 1) and st["restarts"] == 0, st
         assert sorted(cs[0].discoveries()) == ["abort agreement", "commit agreement"]
     finally:
         close(comms, cs)

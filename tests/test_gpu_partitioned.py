@@ -90,15 +90,35 @@ def test_partitioned_restart_on_overflow():
     assert c.unique_state_count() == expect
 
 
-def test_rccl_single_rank():
+@pytest.mark.parametrize("direct", ["1", "0"])
+def test_rccl_single_rank(direct, monkeypatch):
+    # the RCCL communicator's code path with one rank: the direct exchange (its flag protocol with
+    # this rank as the only source and owner), or RCCL's all-to-all (SR_DIRECT=0)
+    monkeypatch.setenv("SR_DIRECT", direct)
     from stateright_amd.distributed import Communicator
     comm = Communicator(0, 1, Communicator.unique_id(), 0)
     c = sr.TwoPhaseSys(6).checker().comm(comm).spawn_bfs().join()
-    o = oracle(TWO_PHASE, [6]) if False else OracleRun(TWO_PHASE, [6])
+    o = oracle(TWO_PHASE, [6])
     assert (c.unique_state_count(), c.state_count(), c.max_depth()) == (o.unique_state_count, o.state_count, o.max_depth)
     assert sorted(c.discoveries()) == o.discovery_names()
+    assert c.stats()["pipelined"] == (2 if direct == "1" else 1)
     del c
     comm.close()
+
+
+@pytest.mark.parametrize("parts", [2, 3, 8])
+@pytest.mark.parametrize("case", [(TWO_PHASE, [5]), (TWO_PHASE, [7]), (INCREMENT_LOCK, [7]), (LINEAR_EQUATION, [2, 4, 7])],
+                         ids=ids)
+def test_exchange_by_copies_matches_oracle(case, parts, monkeypatch):
+    # SR_DIRECT=0: the buckets of every partition are exchanged by device copies (the all-to-all's
+    # stand-in) instead of being stored straight into the owners' receive buffers
+    monkeypatch.setenv("SR_DIRECT", "0")
+    model, params = case
+    o = oracle(model, params)
+    c = MODELS[model](params).checker().partitions(parts).spawn_bfs().join()
+    assert (c.unique_state_count(), c.state_count(), c.max_depth()) == (o.unique_state_count, o.state_count, o.max_depth)
+    assert sorted(c.discoveries()) == o.discovery_names()
+    assert c.stats()["pipelined"] == 1
 
 
 @pytest.mark.parametrize("parts", [2, 4, 8])
@@ -111,7 +131,7 @@ def test_pipelined_plan_holds_on_bench_config(parts):
     c = sr.TwoPhaseSys(n).checker().partitions(parts).capacity_hint(want).spawn_bfs().join()
     st = c.stats()
     assert c.unique_state_count() == want
-    assert st["pipelined"] == 1 and st["restarts"] == 0, st
+    assert st["pipelined"] == (2 if parts > 1 else 1) and st["restarts"] == 0, st
 
 
 @pytest.mark.parametrize("sync", [False, True])
@@ -120,10 +140,11 @@ def test_pipelined_and_synchronous_agree(sync, monkeypatch):
         monkeypatch.setenv("SR_DIST_SYNC", "1")
     else:
         monkeypatch.delenv("SR_DIST_SYNC", raising=False)
+    monkeypatch.setenv("SR_HEAD_MAX", "0")  # every level partitioned (the head would explore it all)
     o = oracle(INCREMENT_LOCK, [7])
     c = sr.IncrementLock(7).checker().partitions(3).spawn_bfs().join()
     assert (c.unique_state_count(), c.state_count(), c.max_depth()) == (o.unique_state_count, o.state_count, o.max_depth)
-    assert c.stats()["pipelined"] == (0 if sync else 1)
+    assert c.stats()["pipelined"] == (0 if sync else 2)
 
 
 @pytest.mark.parametrize("head", ["0", "64", "65536"])
@@ -148,3 +169,17 @@ def test_replicated_head_counts_and_paths(case, head, monkeypatch):
         assert len(path) == len(o.discovery_actions(name))  # a shortest path, as BFS reports
     if head == "0":
         assert c.stats()["head_levels"] == 0
+
+
+def test_ipc_direct_exchange_across_processes():
+    # The direct exchange across processes (one process per GPU under the bench) rests on IPC
+    # handles of pool buffers, stores into another process's memory from every workgroup of a
+    # kernel, and a flag raised after a system-scope release: scripts/ipc_selftest runs exactly that
+    # between two processes on this GPU, each checking every word the other stored.
+    import os
+    import subprocess
+    from stateright_amd import build
+    assert os.path.exists(build.IPC_SELFTEST), "built by __graft_entry__.build()"
+    r = subprocess.run([build.IPC_SELFTEST, str(1 << 20)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "ipc selftest ok" in r.stdout and r.stdout.count(": 0 wrong") == 2, r.stdout
