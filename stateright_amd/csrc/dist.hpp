@@ -79,6 +79,12 @@ struct PeerBlob {
 
 struct Comm {
     int rank = 0, world = 1, device = 0;
+    // process-unique identity (pooled per-device resources remember which communicator they served)
+    const u64 uid = next_uid();
+    static u64 next_uid() {
+        static std::atomic<u64> n{1};
+        return n++;
+    }
     virtual ~Comm() = default;
     virtual const char* kind() const = 0;
     virtual int nranks() const = 0;  // ranks the transport itself reports (RCCL: ncclCommCount)
@@ -493,7 +499,24 @@ struct DistContext {
         LagPub* pub[2] = {nullptr, nullptr};      // pipelined mode: pinned, slot = seq & 1
         LagPub* pub_dev[2] = {nullptr, nullptr};
         size_t pub_words = 0;
+        // direct exchange: receive buffers by level parity ([T][S] words), and the table of every
+        // owner's buffer of that parity (+ DIST_HDR). Kept across checks, like the streams.
+        DBuf<u64> drecv[2];
+        u64 drecv_words = 0;
+        DBuf<u64*> ptab[2];
     };
+    // Direct exchange state kept across the checks of one communicator (or one set of virtual
+    // partitions): the flag words of this rank, the table of its word in every owner's flags, and
+    // the flag sequence number of the last level (monotonic: flags are never cleared between
+    // checks, so a check costs no collective set-up once the addresses are shared).
+    struct Direct {
+        u64 comm_uid = 0;  // the communicator served (0: virtual partitions)
+        u32 T = 0;         // partitions
+        bool valid = false;
+        u32 fseq = 0;
+        DBuf<u32> flags;
+        DBuf<u32*> ftab;
+    } dx;
     static constexpr size_t ROW_WORDS = (size_t)MAX_PARTS * (MAX_PARTS + 6 + MAX_PROPS);
     int dev = 0;
     hipStream_t stream = nullptr;
@@ -519,7 +542,7 @@ struct DistContext {
             SR_HIP(hipHostMalloc(&r.hc, sizeof(HostCounters), hipHostMallocCoherent | hipHostMallocMapped));
             SR_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&r.hc_dev), r.hc, 0));
             std::memset(r.hc, 0, sizeof(HostCounters));
-            parts.push_back(r);
+            parts.push_back(std::move(r));
         }
     }
     // pinned publish slots of partition i holding `words` row words
@@ -558,9 +581,6 @@ class DistEngine final : public EngineBase {
         DBuf<u32> sendc;                 // [T] records per destination (device)
         DBuf<u64> recv;
         u64 recv_cap = 0;
-        DBuf<u64> drecv[2];              // direct exchange: receive buffers by level parity, [T][S]
-        u64 drecv_words = 0;
-        DBuf<u64*> ptab[2];              // direct exchange: every owner's drecv[parity] + DIST_HDR
         LevelCounters* lc = nullptr;
         DistCtl* ctl = nullptr;          // device: frontier size + its discoveries (next level's input)
         HostCounters* hc = nullptr;      // pinned host (root level only)
@@ -1231,7 +1251,7 @@ class DistEngine final : public EngineBase {
     void lag_enqueue(u32 level, u64 C, u32 undiscovered, const std::vector<u64>& n_plan) {
         const u64 S = lag_S(C);
         const size_t RW = T_ + 6 + M::NPROPS;
-        const u32 par = xlev_ & 1, fseq = ++xlev_;
+        const u32 fseq = direct_ ? ++ctx_->dx.fseq : 0, par = fseq & 1;
         if (direct_) {
             direct_buffers(S);
         } else {
@@ -1255,8 +1275,8 @@ class DistEngine final : public EngineBase {
             expand_route<M, 1><<<grid, 256, route_lds(), stream_>>>(
                 m_, p.arena.p, p.apar.p, 0, p.arena_cap, p.view(), p.id, T_, direct_ ? nullptr : p.send.p + DIST_HDR,
                 (u32)C, p.sendc.p, p.lc, p.ctl, undiscovered, row, ppw_log2, filt_log2_, S, 1u,
-                p.sent_mask ? p.sent.p : nullptr, p.sent_mask, rstage_recs(), direct_ ? p.ptab[par].p : nullptr,
-                dflags_ ? ftab_.p : nullptr, fseq, self_rec());
+                p.sent_mask ? p.sent.p : nullptr, p.sent_mask, rstage_recs(), direct_ ? ctx_->parts[p.res].ptab[par].p : nullptr,
+                dflags_ ? ctx_->dx.ftab.p : nullptr, fseq, self_rec());
             SR_HIP(hipGetLastError());
             if (o_.profile) SR_HIP(hipEventRecord(event(2 * stats.expand_launches + 1), stream_));
             stats.expand_launches++;
@@ -1265,7 +1285,7 @@ class DistEngine final : public EngineBase {
             // the records are in the owners' buffers already; ranks on their own streams wait for
             // every source's flag (virtual partitions share this stream: the routes ran before)
             if (dflags_) {
-                peer_wait<<<1, 64, 0, stream_>>>(flags_.p, T_, fseq, parts_[0].lc, peer_timeout_);
+                peer_wait<<<1, 64, 0, stream_>>>(ctx_->dx.flags.p, T_, fseq, parts_[0].lc, peer_timeout_);
                 SR_HIP(hipGetLastError());
             }
         } else if (comm_) {
@@ -1282,7 +1302,7 @@ class DistEngine final : public EngineBase {
             auto& r = ctx_->parts[p.res];
             // four records per thread on the large grid (insert_grid), one otherwise
             auto kern = ig > INSERT_GRID_MAX && W <= 2 ? insert_recv_lag<M, 4> : insert_recv_lag<M, 1>;
-            kern<<<ig, 256, 0, stream_>>>(m_, direct_ ? p.drecv[par].p : p.recv.p, S, (u32)C, p.id, T_, p.view(),
+            kern<<<ig, 256, 0, stream_>>>(m_, direct_ ? r.drecv[par].p : p.recv.p, S, (u32)C, p.id, T_, p.view(),
                                           p.arena.p, p.apar.p, p.arena_cap, p.lc, undiscovered, p.ctl,
                                           r.pub_dev[p.seq & 1], p.seq);
             SR_HIP(hipGetLastError());
@@ -1296,46 +1316,72 @@ class DistEngine final : public EngineBase {
     // first waits until no level is in flight ANYWHERE (a collective barrier: peers may still be
     // storing into the old buffers), then shares the new buffers' addresses.
     void direct_buffers(u64 S) {
+        auto R = [&](Part& p) -> DistContext::PartRes& { return ctx_->parts[p.res]; };
         bool grow = false;
-        for (auto& p : parts_) grow |= p.drecv_words < S * T_;
+        for (auto& p : parts_) grow |= R(p).drecv_words < S * T_;
         if (!grow) return;
         if (comm_) comm_->barrier(stream_);
         else SR_HIP(hipStreamSynchronize(stream_));
         for (auto& p : parts_) {
-            const u64 words = std::max<u64>(S * T_, p.drecv_words * 2);
-            for (int k = 0; k < 2; ++k) p.drecv[k].alloc(o_.device, words);
-            p.drecv_words = words;
+            const u64 words = std::max<u64>(S * T_, R(p).drecv_words * 2);
+            for (int k = 0; k < 2; ++k) R(p).drecv[k].alloc(o_.device, words);
+            R(p).drecv_words = words;
         }
         for (int k = 0; k < 2; ++k) {
             std::vector<u64*> owners(T_);
             if (comm_) {
-                comm_->peer_addresses(parts_[0].drecv[k].p, owners, stream_);
+                comm_->peer_addresses(R(parts_[0]).drecv[k].p, owners, stream_);
             } else {
-                for (auto& q : parts_) owners[q.id] = q.drecv[k].p;
+                for (auto& q : parts_) owners[q.id] = R(q).drecv[k].p;
             }
             for (auto& o : owners) o += DIST_HDR;
             for (auto& p : parts_) {
-                if (p.ptab[k].n < T_) p.ptab[k].alloc(o_.device, T_);
-                SR_HIP(hipMemcpyAsync(p.ptab[k].p, owners.data(), T_ * sizeof(u64*), hipMemcpyHostToDevice, stream_));
+                if (R(p).ptab[k].n < T_) R(p).ptab[k].alloc(o_.device, T_);
+                SR_HIP(hipMemcpyAsync(R(p).ptab[k].p, owners.data(), T_ * sizeof(u64*), hipMemcpyHostToDevice, stream_));
             }
         }
         SR_HIP(hipStreamSynchronize(stream_));  // the host tables may go
         direct_grows_++;
     }
 
-    // Direct exchange with device flags (ranks on their own streams): this rank's flag words, zero
-    // before any peer may store into them (the share is collective and follows the clear on every
-    // rank), and the table of this rank's word in every owner's flags.
-    void direct_flags() {
-        flags_.alloc(o_.device, T_);
-        SR_HIP(hipMemsetAsync(flags_.p, 0, T_ * 4, stream_));
-        std::vector<u64*> owners;
-        comm_->peer_addresses(flags_.p, owners, stream_);
-        std::vector<u32*> ft(T_);
-        for (u32 q = 0; q < T_; ++q) ft[q] = reinterpret_cast<u32*>(owners[q]) + comm_->rank;
-        ftab_.alloc(o_.device, T_);
-        SR_HIP(hipMemcpyAsync(ftab_.p, ft.data(), T_ * sizeof(u32*), hipMemcpyHostToDevice, stream_));
-        SR_HIP(hipStreamSynchronize(stream_));
+    // The direct exchange's state at the start of a check (lag_loop). It is kept in the pooled
+    // context across checks; a check reuses it only if EVERY rank holds it for this communicator
+    // with the same flag sequence number (one small collective), and otherwise every rank sets it
+    // up again: its flag words cleared before any peer may store into them (the address share is
+    // collective and follows the clear on every rank), the table of this rank's word in every
+    // owner's flags, and receive buffers grown (and shared) at the first level.
+    void direct_setup() {
+        auto& d = ctx_->dx;
+        const u64 uid = comm_ ? comm_->uid : 0;
+        bool reuse = d.valid && d.comm_uid == uid && d.T == T_;
+        if (comm_) {
+            u64 v[3] = {reuse ? 1ull : 0ull, (u64)d.fseq, ~(u64)d.fseq};
+            DBuf<u64> dv;
+            dv.alloc(o_.device, 3);
+            SR_HIP(hipMemcpyAsync(dv.p, v, sizeof(v), hipMemcpyHostToDevice, stream_));
+            comm_->all_reduce(dv.p, 3, RedOp::Min, stream_);
+            SR_HIP(hipMemcpyAsync(v, dv.p, sizeof(v), hipMemcpyDeviceToHost, stream_));
+            SR_HIP(hipStreamSynchronize(stream_));
+            reuse = v[0] == 1 && v[1] == ~v[2];  // everyone holds it, at one sequence number
+        }
+        if (reuse) return;
+        d.valid = false;
+        for (auto& p : parts_) ctx_->parts[p.res].drecv_words = 0;  // grown and shared at level one
+        d.comm_uid = uid;
+        d.T = T_;
+        d.fseq = 0;
+        if (comm_) {
+            d.flags.alloc(o_.device, T_);
+            SR_HIP(hipMemsetAsync(d.flags.p, 0, T_ * 4, stream_));
+            std::vector<u64*> owners;
+            comm_->peer_addresses(d.flags.p, owners, stream_);
+            std::vector<u32*> ft(T_);
+            for (u32 q = 0; q < T_; ++q) ft[q] = reinterpret_cast<u32*>(owners[q]) + comm_->rank;
+            d.ftab.alloc(o_.device, T_);
+            SR_HIP(hipMemcpyAsync(d.ftab.p, ft.data(), T_ * sizeof(u32*), hipMemcpyHostToDevice, stream_));
+            SR_HIP(hipStreamSynchronize(stream_));
+        }
+        d.valid = true;
     }
 
     // Waits for partition p's publish of the level tagged `seq`.
@@ -1365,9 +1411,8 @@ class DistEngine final : public EngineBase {
         // the exchange of this check's levels (every rank decides the same: probe_direct is collective)
         direct_ = direct_env_on() && (comm_ ? comm_->probe_direct(stream_) : T_ > 1);
         dflags_ = direct_ && comm_ != nullptr;
-        xlev_ = 0;
         stats.pipelined = direct_ ? 2u : 1u;
-        if (dflags_) direct_flags();
+        if (direct_) direct_setup();
         const u64 cmin = lag_cmin_;
         glob_prev_ = 0;
         // What the plan knows (the same on every rank): exact frontier sizes up to the last rows
@@ -1464,8 +1509,10 @@ class DistEngine final : public EngineBase {
             // one level later, the receiver's) error bit is in these rows on every rank.
             if (glob_err & ERR_TABLE_FULL) throw Error(SR_ERR_CAPACITY, "visited set probe limit exceeded");
             if (glob_err & ERR_FRONTIER_OVERFLOW) throw Error(SR_ERR_CAPACITY, "frontier or send bucket overflow");
-            if (glob_err & ERR_PEER_TIMEOUT)
+            if (glob_err & ERR_PEER_TIMEOUT) {
+                ctx_->dx.valid = false;
                 throw Error(SR_ERR_HIP, "direct exchange: a source's records did not arrive within SR_PEER_TIMEOUT_MS");
+            }
             for (u32 q = 0; q < T_; ++q) {
                 u64 r = 0;
                 for (u32 s2 = 0; s2 < T_; ++s2) r += all[s2 * RW + q];
@@ -1778,12 +1825,9 @@ class DistEngine final : public EngineBase {
     bool trace_ = std::getenv("SR_DIST_TRACE") != nullptr;
     Clock::time_point t_trace_ = Clock::now();
     u64 arena_grows_ = 0;
-    // direct exchange (lag_loop): on for this check, with device flags (comm ranks), pipelined
-    // levels enqueued (buffer parity and flag sequence), flags / flag table, buffer growths
+    // direct exchange (lag_loop): on for this check, with device flags (comm ranks); buffer growths
+    // (the flags, buffers and tables live in the pooled context: DistContext::Direct)
     bool direct_ = false, dflags_ = false;
-    u32 xlev_ = 0;
-    DBuf<u32> flags_;
-    DBuf<u32*> ftab_;
     u64 peer_timeout_ = peer_timeout_ticks();
     u64 direct_grows_ = 0;
     std::vector<u64> rows_;

@@ -185,3 +185,26 @@ def test_config4_2pc11_partitioned_8_full_size():
     for name, path in c.discoveries().items():
         r = replay(TWO_PHASE, [n], path.action_ids, n_props=3)
         assert r is not None and r[1][["abort agreement", "commit agreement", "consistent"].index(name)] == 1
+
+
+def test_direct_state_reused_across_checks(monkeypatch):
+    # The direct exchange keeps its flag words, receive buffers and address tables in the pooled
+    # per-device context across the checks of one communicator (flags are monotonic sequence
+    # numbers, never cleared). Consecutive checks of different sizes on the same ranks: the second
+    # grows the buffers, the third reuses them; every count equals the oracle's.
+    monkeypatch.setenv("SR_HEAD_MAX", "0")
+    comms = Communicator.local_group(3)
+    try:
+        for model, params in [(TWO_PHASE, [4]), (TWO_PHASE, [7]), (INCREMENT_LOCK, [6]), (TWO_PHASE, [5])]:
+            o = oracle(model, params)
+            cs = [MODELS[model](params).checker().comm(c).spawn_bfs() for c in comms]
+            for ch in cs:
+                ch.join()
+            for ch in cs:
+                assert (ch.unique_state_count(), ch.state_count(), ch.max_depth()) == \
+                    (o.unique_state_count, o.state_count, o.max_depth)
+                assert ch.stats()["pipelined"] == 2
+            cs.clear()
+    finally:
+        for c in comms:
+            c.close()

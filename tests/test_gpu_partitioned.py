@@ -183,3 +183,12 @@ def test_ipc_direct_exchange_across_processes():
     r = subprocess.run([build.IPC_SELFTEST, str(1 << 20)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "ipc selftest ok" in r.stdout and r.stdout.count(": 0 wrong") == 2, r.stdout
+
+
+def test_direct_virtual_partitions_change_between_checks():
+    # Virtual partitions share the pooled context's direct-exchange buffers: a different partition
+    # count between checks sets them up again, the same count reuses them.
+    for parts, n in [(8, 5), (2, 6), (8, 7), (8, 5)]:
+        o = oracle(TWO_PHASE, [n])
+        c = sr.TwoPhaseSys(n).checker().partitions(parts).spawn_bfs().join()
+        assert (c.unique_state_count(), c.state_count(), c.max_depth()) == (o.unique_state_count, o.state_count, o.max_depth)
