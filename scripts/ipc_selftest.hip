@@ -112,7 +112,10 @@ int main(int argc, char** argv) {
         pid[r] = fork();  // before any HIP call in this process
         if (pid[r] == 0) {
             close(sv[1 - r]);
-            std::_Exit(run(r, sv[r], n));
+            const int rc = run(r, sv[r], n);
+            std::fflush(stdout);  // _Exit skips the stdio flush (stdout is a pipe under the test)
+            std::fflush(stderr);
+            std::_Exit(rc);
         }
     }
     close(sv[0]);

@@ -107,6 +107,8 @@ struct Comm {
     // Whether this transport can give every rank a pointer to every other rank's buffers
     // (SR_DIRECT=0 turns the direct exchange off; RCCL's all-to-all is then the exchange).
     virtual bool peer_capable() const { return false; }
+    // Every rank on its own device (the direct exchange's wait may then run inside the insert grid).
+    virtual bool distinct_devices() const { return false; }
     // Collective: every rank's `bytes` bytes of `mine`, rank-major, into `all` (host memory).
     virtual void share(const void* mine, size_t bytes, void* all, hipStream_t s) = 0;
     // This rank's buffer `p` as a blob, and rank q's blob as an address usable by this rank's kernels.
@@ -279,6 +281,7 @@ struct RcclComm final : Comm {
     // Direct exchange across processes: buffers travel as IPC handles of their hipMalloc
     // allocation (the DevicePool hands out whole allocations), opened once per (peer, allocation).
     bool peer_capable() const override { return direct_env_on(); }
+    bool distinct_devices() const override { return true; }  // RCCL refuses two ranks on one GPU
     void share(const void* mine, size_t bytes, void* all, hipStream_t s) override {
         const u64 words = (bytes + 7) / 8;
         DBuf<u64> d;
@@ -456,6 +459,10 @@ struct LocalComm final : Comm {
     // when the ranks sit on different devices). share() first finishes this rank's stream, so a
     // rank that shares a buffer it just cleared has cleared it before any peer can write to it.
     bool peer_capable() const override { return direct_env_on(); }
+    bool distinct_devices() const override {
+        std::set<int> d(g->devices.begin(), g->devices.end());
+        return (int)d.size() == world;
+    }
     void share(const void* mine, size_t bytes, void* all, hipStream_t s) override {
         SR_HIP(hipStreamSynchronize(s));
         auto& sl = g->slots[rank];
@@ -513,7 +520,10 @@ struct DistContext {
         u64 comm_uid = 0;  // the communicator served (0: virtual partitions)
         u32 T = 0;         // partitions
         bool valid = false;
+        u64 gen = 0;       // set-up generation (agreed by the ranks of the communicator)
         u32 fseq = 0;
+        u32 fseq_start = 0;  // diagnostics: the sequence number this check started from, and how
+        bool reused = false;
         DBuf<u32> flags;
         DBuf<u32*> ftab;
     } dx;
@@ -1284,7 +1294,7 @@ class DistEngine final : public EngineBase {
         if (direct_) {
             // the records are in the owners' buffers already; ranks on their own streams wait for
             // every source's flag (virtual partitions share this stream: the routes ran before)
-            if (dflags_) {
+            if (dflags_ && !fused_wait_) {
                 peer_wait<<<1, 64, 0, stream_>>>(ctx_->dx.flags.p, T_, fseq, parts_[0].lc, peer_timeout_);
                 SR_HIP(hipGetLastError());
             }
@@ -1304,7 +1314,8 @@ class DistEngine final : public EngineBase {
             auto kern = ig > INSERT_GRID_MAX && W <= 2 ? insert_recv_lag<M, 4> : insert_recv_lag<M, 1>;
             kern<<<ig, 256, 0, stream_>>>(m_, direct_ ? r.drecv[par].p : p.recv.p, S, (u32)C, p.id, T_, p.view(),
                                           p.arena.p, p.apar.p, p.arena_cap, p.lc, undiscovered, p.ctl,
-                                          r.pub_dev[p.seq & 1], p.seq);
+                                          r.pub_dev[p.seq & 1], p.seq, dflags_ && fused_wait_ ? ctx_->dx.flags.p : nullptr,
+                                          fseq, peer_timeout_);
             SR_HIP(hipGetLastError());
         }
         (void)level;
@@ -1354,19 +1365,32 @@ class DistEngine final : public EngineBase {
         auto& d = ctx_->dx;
         const u64 uid = comm_ ? comm_->uid : 0;
         bool reuse = d.valid && d.comm_uid == uid && d.T == T_;
+        u64 gen = d.gen + 1;
         if (comm_) {
-            u64 v[3] = {reuse ? 1ull : 0ull, (u64)d.fseq, ~(u64)d.fseq};
+            // min over the ranks of: held, sequence number, ~sequence number, set-up generation and
+            // ~generation. A rank may be handed another pooled context than last time, holding the
+            // state of an OLDER set-up of this communicator (its peers' addresses stale): the
+            // generation, agreed at every set-up, tells it apart even when the sequence numbers match.
+            u64 v[5] = {reuse ? 1ull : 0ull, (u64)d.fseq, ~(u64)d.fseq, d.gen, ~d.gen};
             DBuf<u64> dv;
-            dv.alloc(o_.device, 3);
+            dv.alloc(o_.device, 5);
             SR_HIP(hipMemcpyAsync(dv.p, v, sizeof(v), hipMemcpyHostToDevice, stream_));
-            comm_->all_reduce(dv.p, 3, RedOp::Min, stream_);
+            comm_->all_reduce(dv.p, 5, RedOp::Min, stream_);
             SR_HIP(hipMemcpyAsync(v, dv.p, sizeof(v), hipMemcpyDeviceToHost, stream_));
             SR_HIP(hipStreamSynchronize(stream_));
-            reuse = v[0] == 1 && v[1] == ~v[2];  // everyone holds it, at one sequence number
+            reuse = v[0] == 1 && v[1] == ~v[2] && v[3] == ~v[4];  // everyone holds the same set-up
+            gen = ~v[4] + 1;  // a new set-up's generation: past every rank's
         }
+        if (trace_)
+            std::fprintf(stderr, "[sr-direct] rank %d: %s (uid %llu/%llu, T %u, fseq %u, gen %llu, ctx %p)\n",
+                         comm_ ? comm_->rank : 0, reuse ? "reuse" : "set up", (unsigned long long)d.comm_uid,
+                         (unsigned long long)uid, d.T, d.fseq, (unsigned long long)d.gen, (void*)ctx_);
+        d.fseq_start = d.fseq;
+        d.reused = reuse;
         if (reuse) return;
         d.valid = false;
         for (auto& p : parts_) ctx_->parts[p.res].drecv_words = 0;  // grown and shared at level one
+        d.gen = gen;
         d.comm_uid = uid;
         d.T = T_;
         d.fseq = 0;
@@ -1411,6 +1435,7 @@ class DistEngine final : public EngineBase {
         // the exchange of this check's levels (every rank decides the same: probe_direct is collective)
         direct_ = direct_env_on() && (comm_ ? comm_->probe_direct(stream_) : T_ > 1);
         dflags_ = direct_ && comm_ != nullptr;
+        fused_wait_ = dflags_ && comm_->distinct_devices() && fused_env_on();
         stats.pipelined = direct_ ? 2u : 1u;
         if (direct_) direct_setup();
         const u64 cmin = lag_cmin_;
@@ -1510,8 +1535,19 @@ class DistEngine final : public EngineBase {
             if (glob_err & ERR_TABLE_FULL) throw Error(SR_ERR_CAPACITY, "visited set probe limit exceeded");
             if (glob_err & ERR_FRONTIER_OVERFLOW) throw Error(SR_ERR_CAPACITY, "frontier or send bucket overflow");
             if (glob_err & ERR_PEER_TIMEOUT) {
-                ctx_->dx.valid = false;
-                throw Error(SR_ERR_HIP, "direct exchange: a source's records did not arrive within SR_PEER_TIMEOUT_MS");
+                auto& d = ctx_->dx;
+                d.valid = false;
+                std::string fl;
+                if (d.flags.p) {  // what this rank's flag words hold against the last sequence enqueued
+                    std::vector<u32> f(T_);
+                    SR_HIP(hipStreamSynchronize(stream_));
+                    SR_HIP(hipMemcpy(f.data(), d.flags.p, T_ * 4, hipMemcpyDeviceToHost));
+                    for (u32 q = 0; q < T_; ++q) fl += (q ? "," : "") + std::to_string(f[q]);
+                }
+                throw Error(SR_ERR_HIP, "direct exchange: a source's records did not arrive within SR_PEER_TIMEOUT_MS "
+                                        "(level " + std::to_string(level) + ", rank " + std::to_string(comm_ ? comm_->rank : 0) +
+                                        ", last sequence " + std::to_string(d.fseq) + ", flags [" + fl + "], check started at " +
+                                        std::to_string(d.fseq_start) + (d.reused ? " reusing" : " after set-up") + ")");
             }
             for (u32 q = 0; q < T_; ++q) {
                 u64 r = 0;
@@ -1828,6 +1864,11 @@ class DistEngine final : public EngineBase {
     // direct exchange (lag_loop): on for this check, with device flags (comm ranks); buffer growths
     // (the flags, buffers and tables live in the pooled context: DistContext::Direct)
     bool direct_ = false, dflags_ = false;
+    bool fused_wait_ = false;  // the insert grid polls the flags itself (ranks on distinct devices)
+    static bool fused_env_on() {
+        const char* e = std::getenv("SR_FUSED_WAIT");
+        return !(e && std::atoi(e) == 0);
+    }
     u64 peer_timeout_ = peer_timeout_ticks();
     u64 direct_grows_ = 0;
     std::vector<u64> rows_;

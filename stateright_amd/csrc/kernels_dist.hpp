@@ -619,12 +619,38 @@ template <class M, int IPB = 1>
 __global__ void __launch_bounds__(256) insert_recv_lag(M m, const u64* __restrict__ recv, u64 S, u32 C, u32 me,
                                                        u32 nparts, TableView t, u64* __restrict__ arena,
                                                        u64* __restrict__ apar, u64 arena_cap, LevelCounters* lc,
-                                                       u32 undiscovered, DistCtl* ctl, LagPub* pub, u32 seq) {
+                                                       u32 undiscovered, DistCtl* ctl, LagPub* pub, u32 seq,
+                                                       const u32* wflags, u32 wseq, u64 wtimeout) {
     constexpr int W = M::W, REC = W;
     constexpr u32 STAGE = 1024 / W;
     __shared__ u64 stage[STAGE * W];
     __shared__ u32 qoff[MAX_PARTS + 1];  // exclusive prefix of the received counts per source
     __shared__ u32 stage_n, base;
+    if (wflags) {
+        // Direct exchange with every rank on its own device: peer_wait's poll is this grid's first
+        // step (no launch of its own), one source flag per lane of wave 0, then one acquire per
+        // workgroup before any record or header is read. Bounded like peer_wait. (Ranks that share
+        // a device keep the separate one-wave wait: a spinning insert grid could hold the CUs a
+        // source's expand grid needs.)
+        if (threadIdx.x < nparts) {
+            const u64 t0 = __builtin_amdgcn_s_memrealtime();
+            bool ok = false;
+            for (;;) {
+                const u32 v = __hip_atomic_load(&wflags[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                if ((int)(v - wseq) >= 0) {
+                    ok = true;
+                    break;
+                }
+                if (__builtin_amdgcn_s_memrealtime() - t0 > wtimeout) break;
+                __builtin_amdgcn_s_sleep(2);
+            }
+            if (!ok) atomicOr(&lc->err, (u32)ERR_PEER_TIMEOUT);
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
     const u64 nb = ctl->nb, n = ctl->n;
     u64* next = arena + (nb + n) * W;
     u64* next_par = apar + nb + n;

@@ -208,3 +208,23 @@ def test_direct_state_reused_across_checks(monkeypatch):
     finally:
         for c in comms:
             c.close()
+
+
+@pytest.mark.parametrize("head", ["0", "65536"])
+def test_direct_repeated_checks_same_ranks(head, monkeypatch):
+    # The bench's pattern: the same in-process ranks run several checks of 2pc N=7 back to back,
+    # with and without the replicated head.
+    monkeypatch.setenv("SR_HEAD_MAX", head)
+    n = 7
+    want = 6 ** n + 4 ** n + 2 ** n
+    comms = Communicator.local_group(2)
+    try:
+        for _ in range(4):
+            cs = [sr.TwoPhaseSys(n).checker().comm(c).capacity_hint(want).defer_paths().spawn_bfs() for c in comms]
+            for ch in cs:
+                ch.join()
+            assert [ch.unique_state_count() for ch in cs] == [want, want]
+            cs.clear()
+    finally:
+        for c in comms:
+            c.close()

@@ -90,11 +90,14 @@ def test_partitioned_restart_on_overflow():
     assert c.unique_state_count() == expect
 
 
-@pytest.mark.parametrize("direct", ["1", "0"])
-def test_rccl_single_rank(direct, monkeypatch):
+@pytest.mark.parametrize("direct,fused", [("1", "1"), ("1", "0"), ("0", "1")])
+def test_rccl_single_rank(direct, fused, monkeypatch):
     # the RCCL communicator's code path with one rank: the direct exchange (its flag protocol with
-    # this rank as the only source and owner), or RCCL's all-to-all (SR_DIRECT=0)
+    # this rank as the only source and owner; RCCL ranks have distinct devices, so the insert grid
+    # polls the flags itself unless SR_FUSED_WAIT=0 keeps the one-wave wait kernel), or RCCL's
+    # all-to-all (SR_DIRECT=0)
     monkeypatch.setenv("SR_DIRECT", direct)
+    monkeypatch.setenv("SR_FUSED_WAIT", fused)
     from stateright_amd.distributed import Communicator
     comm = Communicator(0, 1, Communicator.unique_id(), 0)
     c = sr.TwoPhaseSys(6).checker().comm(comm).spawn_bfs().join()
