@@ -222,9 +222,13 @@ void sr_gpu_bfs_free(sr_bfs* bfs);
  * which is single-process shared-memory: src/checker/bfs.rs:70-152) ----
  * One process per GPU. Rank 0 creates a unique id, every rank receives it out of band (e.g. a
  * torch.distributed broadcast) and calls sr_dist_init with its rank. The first small levels run
- * replicated on every rank with no collective; after them RCCL carries ONE all-to-all of
- * fixed-capacity buckets of successor records (8*W bytes each, every rank's row in the bucket
- * headers) per BFS level over xGMI, enqueued without a host wait inside the level.
+ * replicated on every rank with no collective. After them every level is exchanged DIRECTLY: each
+ * rank's expand kernel stores its successor records (8*W bytes each) into the owners' receive
+ * buffers through peer pointers (IPC handles across processes, shared once through the
+ * communicator) and raises a device flag per level in every owner; owners wait for the flags on
+ * the device. No collective and no host step runs inside a level. If a one-off
+ * collective probe finds the peer path unusable on any rank (or SR_DIRECT=0), RCCL instead carries
+ * ONE all-to-all of fixed-capacity buckets per level, every rank's row in the bucket headers.
  * Counts reported by every rank are global. Discovery paths are gathered on every rank at join
  * (sr_opts.defer_paths = 0, the default), so any rank may ask for them alone. */
 #define SR_DIST_ID_BYTES 128
@@ -235,7 +239,9 @@ sr_dist* sr_dist_init(int32_t rank, int32_t world, const uint8_t* id, int32_t de
 /* `world` communicators whose ranks are threads of THIS process (rank r on devices[r], or device 0
  * when devices is NULL): the same stream-ordered collectives as RCCL, carried by device copies
  * across the ranks' streams, with a host rendezvous per call that rejects ranks issuing different
- * collectives. Runs the partitioned engine's multi-rank code path on one GPU (tests). */
+ * collectives, and the direct exchange through raw device pointers. Runs the partitioned engine's
+ * multi-rank code path on one GPU (tests). Ranks that share a device each need a hardware queue of
+ * their own for the direct exchange's device-side waits (GPU_MAX_HW_QUEUES >= world + 2). */
 int32_t sr_dist_local_group(int32_t world, const int32_t* devices, sr_dist** comms_out);
 int32_t sr_dist_rank(const sr_dist* comm);
 int32_t sr_dist_world(const sr_dist* comm);
@@ -263,8 +269,8 @@ int32_t sr_selftest_tables(void);
  * returns the state itself, over every reachable state of 2pc N=1..7 (and its canonical form).
  * SR_OK or SR_ERR_ARG (sr_last_error says where). */
 int32_t sr_selftest_models(void);
-/* comm == NULL: `virtual_partitions` partitions in this process on opts->device (same protocol,
- * device-copy exchange). FAST order only. */
+/* comm == NULL: `virtual_partitions` partitions in this process on opts->device (same protocol;
+ * the partitions store into each other's receive buffers). FAST order only. */
 sr_bfs* sr_gpu_bfs_spawn_partitioned(sr_dist* comm, int32_t virtual_partitions, int32_t model_id,
                                      const int64_t* params, int32_t nparams, const sr_opts* opts);
 
