@@ -73,6 +73,10 @@ def parse():
     ap.add_argument("--config4-steps", type=int, default=3,
                     help="also time BASELINE configs[3] (2pc N=11, partitioned over the N GPUs; one GPU at N=1) "
                          "for this many checks after one warmup (0 = skip); reported as `config4`, not `value`")
+    ap.add_argument("--comm", default="rccl", choices=["rccl", "shm"],
+                    help="N>1 host-side transport: RCCL (one process per GPU), or a shared-memory segment "
+                         "(a rehearsal of the multi-process path with every rank on ONE GPU, where RCCL refuses "
+                         "two ranks on one device; its timings are not the node's)")
     ap.add_argument("--dry-run", action="store_true",
                     help="every rank prints its launch plan as JSON and exits before any GPU call")
     ap.add_argument("--mode", default="partitioned", choices=["partitioned", "replicas", "rccl1"],
@@ -317,9 +321,16 @@ def main():
     if world > 1 or args.mode == "rccl1":
         from stateright_amd.distributed import Communicator
         with stdout_to_stderr():
+            if args.comm == "shm":
+                # every rank names the same segment (the launcher's port and pid); ranks share a GPU
+                # when the node has fewer GPUs than ranks
+                name = f"/sr_bench_{os.environ.get('MASTER_PORT', '0')}_{os.getppid()}"
+                comm = Communicator.shm(rank, world, name, device=dev, slot_bytes=256 << 20,
+                                        devices_distinct=ndev >= world)
             # under a launcher (RANK set) every rank bootstraps from its environment, also at N=1
-            comm = (Communicator.from_env(device=dev) if "RANK" in os.environ
-                    else Communicator(0, 1, Communicator.unique_id(), dev))
+            else:
+                comm = (Communicator.from_env(device=dev) if "RANK" in os.environ
+                        else Communicator(0, 1, Communicator.unique_id(), dev))
 
     def step(profile=False, counters=False):
         b = make().checker().capacity_hint(expect_unique).device(dev)

@@ -243,11 +243,19 @@ sr_dist* sr_dist_init(int32_t rank, int32_t world, const uint8_t* id, int32_t de
  * multi-rank code path on one GPU (tests). Ranks that share a device each need a hardware queue of
  * their own for the direct exchange's device-side waits (GPU_MAX_HW_QUEUES >= world + 2). */
 int32_t sr_dist_local_group(int32_t world, const int32_t* devices, sr_dist** comms_out);
+/* `world` PROCESSES of one host whose host-side transport is the POSIX shared-memory segment `name`
+ * (created by the first rank to open it; rank 0 unlinks it when freed): synchronous staged
+ * collectives through per-rank slots of slot_bytes, a barrier in the segment, and the direct
+ * exchange through IPC handles. Lets the one-process-per-GPU code path run as separate processes on
+ * ONE GPU, where RCCL refuses two ranks on one device (tests, bench rehearsals).
+ * devices_distinct = 1 when every rank has its own GPU. */
+sr_dist* sr_dist_shm_init(int32_t rank, int32_t world, const char* name, int32_t device, int64_t slot_bytes,
+                          int32_t devices_distinct);
 int32_t sr_dist_rank(const sr_dist* comm);
 int32_t sr_dist_world(const sr_dist* comm);
 /* Ranks the transport reports (RCCL: ncclCommCount). */
 int32_t sr_dist_nranks(const sr_dist* comm);
-/* "rccl" or "local". */
+/* "rccl", "local" or "shm". */
 int32_t sr_dist_kind(const sr_dist* comm, char* buf, int32_t cap);
 /* Device synchronisation of this rank, then a collective barrier (bench timing brackets). */
 int32_t sr_dist_barrier(sr_dist* comm);

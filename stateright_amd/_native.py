@@ -112,6 +112,8 @@ SIGNATURES = [
     ("sr_dist_unique_id", ctypes.c_int32, [ctypes.c_char_p]),
     ("sr_dist_init", _P, [ctypes.c_int32, ctypes.c_int32, ctypes.c_char_p, ctypes.c_int32]),
     ("sr_dist_local_group", ctypes.c_int32, [ctypes.c_int32, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(_P)]),
+    ("sr_dist_shm_init", _P, [ctypes.c_int32, ctypes.c_int32, ctypes.c_char_p, ctypes.c_int32, ctypes.c_int64,
+                              ctypes.c_int32]),
     ("sr_dist_rank", ctypes.c_int32, [_P]),
     ("sr_dist_world", ctypes.c_int32, [_P]),
     ("sr_dist_nranks", ctypes.c_int32, [_P]),

@@ -29,7 +29,11 @@
 // Capacity planning is optimistic; an overflow on any partition is seen by every rank in the
 // rows and all of them restart the check together with larger buffers.
 #pragma once
+#include <fcntl.h>
 #include <rccl/rccl.h>
+#include <sched.h>
+#include <sys/mman.h>
+#include <unistd.h>
 
 #include <condition_variable>
 #include <memory>
@@ -490,6 +494,166 @@ struct LocalComm final : Comm {
         return reinterpret_cast<u64*>(b.ptr);
     }
     std::set<int> peer_enabled;
+};
+
+// Ranks that are PROCESSES of one host, with a POSIX shared-memory segment as the host-side
+// transport (sr_dist_shm_init): a barrier and one staging slot per rank. Its collectives are
+// synchronous host copies (they finish before they return, which the stream-ordered contract
+// allows), and buffers travel between the processes as IPC handles, as with RCCL. It exists so that
+// the one-process-per-GPU code path, direct exchange included, can run as separate processes on ONE
+// GPU, where RCCL refuses two ranks on the same device; `devices_distinct` is set when every rank
+// has its own GPU.
+struct ShmComm final : Comm {
+    struct Header {
+        std::atomic<u64> arrived;
+        std::atomic<u64> generation;
+        std::atomic<u32> failed;
+    };
+    static constexpr size_t HDR = 4096;
+    std::string name;
+    size_t slot_bytes = 0;
+    char* base = nullptr;
+    size_t bytes = 0;
+    bool devices_distinct = false;
+    IpcMaps ipc;
+    double timeout_s = std::getenv("SR_SHM_TIMEOUT_SEC") ? std::atof(std::getenv("SR_SHM_TIMEOUT_SEC")) : 300.0;
+
+    ShmComm(int r, int w, const std::string& nm, int dev, size_t slot, bool distinct) {
+        rank = r;
+        world = w;
+        device = dev;
+        name = nm;
+        slot_bytes = slot;
+        devices_distinct = distinct;
+        bytes = HDR + slot_bytes * (size_t)w;
+        const int fd = shm_open(name.c_str(), O_CREAT | O_RDWR, 0600);
+        if (fd < 0) throw Error(SR_ERR_ARG, "shm_open(" + name + ") failed");
+        if (ftruncate(fd, (off_t)bytes) != 0) {
+            ::close(fd);
+            throw Error(SR_ERR_ARG, "ftruncate of the shared segment failed");
+        }
+        void* m = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+        ::close(fd);
+        if (m == MAP_FAILED) throw Error(SR_ERR_ARG, "mmap of the shared segment failed");
+        base = static_cast<char*>(m);
+    }
+    ~ShmComm() override {
+        ipc.close();
+        if (base) munmap(base, bytes);
+        if (rank == 0) shm_unlink(name.c_str());
+    }
+    const char* kind() const override { return "shm"; }
+    int nranks() const override { return world; }
+    Header* hdr() { return reinterpret_cast<Header*>(base); }
+    char* slot(int q) { return base + HDR + slot_bytes * (size_t)q; }
+    void need(size_t b) {
+        if (b > slot_bytes) throw Error(SR_ERR_CAPACITY, "shm transport: " + std::to_string(b) + " bytes exceed its staging slot");
+    }
+    // every rank arrives (sense by generation); bounded
+    void sync() {
+        Header* h = hdr();
+        if (h->failed.load()) throw Error(SR_ERR_HIP, "shm transport: a rank failed");
+        const u64 g = h->generation.load();
+        if (h->arrived.fetch_add(1) + 1 == (u64)world) {
+            h->arrived.store(0);
+            h->generation.fetch_add(1);
+            return;
+        }
+        const auto t0 = Clock::now();
+        for (u64 spin = 0; h->generation.load() == g; ++spin) {
+            if ((spin & 1023) == 0 && secs(t0, Clock::now()) > timeout_s) {
+                h->failed.store(1);
+                throw Error(SR_ERR_HIP, "shm transport: ranks did not meet within SR_SHM_TIMEOUT_SEC");
+            }
+            if (spin > 4096) sched_yield();
+        }
+    }
+    void d2h(void* dst, const void* src, size_t b, hipStream_t s) {
+        if (b) SR_HIP(hipMemcpyAsync(dst, src, b, hipMemcpyDeviceToHost, s));
+    }
+    void h2d(void* dst, const void* src, size_t b, hipStream_t s) {
+        if (b) SR_HIP(hipMemcpyAsync(dst, src, b, hipMemcpyHostToDevice, s));
+    }
+    void all_to_all(const u64* send, u64* recv, u64 count, hipStream_t s) override {
+        need(count * 8 * (size_t)world);
+        d2h(slot(rank), send, count * 8 * world, s);
+        SR_HIP(hipStreamSynchronize(s));
+        sync();
+        for (int q = 0; q < world; ++q) h2d(recv + (u64)q * count, slot(q) + (size_t)rank * count * 8, count * 8, s);
+        SR_HIP(hipStreamSynchronize(s));
+        sync();
+    }
+    void all_gather(const u64* mine, u64* all, u64 count, hipStream_t s) override {
+        need(count * 8);
+        d2h(slot(rank), mine, count * 8, s);
+        SR_HIP(hipStreamSynchronize(s));
+        sync();
+        for (int q = 0; q < world; ++q) h2d(all + (u64)q * count, slot(q), count * 8, s);
+        SR_HIP(hipStreamSynchronize(s));
+        sync();
+    }
+    void exchange(const std::vector<const u64*>& send, const std::vector<u64>& scount, const std::vector<u64*>& recv,
+                  const std::vector<u64>& rcount, hipStream_t s) override {
+        // my slot: [T offsets][T counts][data]
+        size_t off = 16 * (size_t)world, total = off;
+        for (int q = 0; q < world; ++q) total += scount[q] * 8;
+        need(total);
+        u64* meta = reinterpret_cast<u64*>(slot(rank));
+        for (int q = 0; q < world; ++q) {
+            meta[q] = off;
+            meta[world + q] = scount[q];
+            d2h(slot(rank) + off, send[q], scount[q] * 8, s);
+            off += scount[q] * 8;
+        }
+        SR_HIP(hipStreamSynchronize(s));
+        sync();
+        for (int q = 0; q < world; ++q) {
+            const u64* m = reinterpret_cast<const u64*>(slot(q));
+            if (m[world + rank] != rcount[q])
+                throw Error(SR_ERR_HIP, "shm exchange: rank " + std::to_string(q) + " sends " + std::to_string(m[world + rank]) +
+                                            " words, rank " + std::to_string(rank) + " expects " + std::to_string(rcount[q]));
+            h2d(recv[q], slot(q) + m[rank], rcount[q] * 8, s);
+        }
+        SR_HIP(hipStreamSynchronize(s));
+        sync();
+    }
+    void broadcast(u64* buf, u64 count, int root, hipStream_t s) override {
+        need(count * 8);
+        if (rank == root) d2h(slot(root), buf, count * 8, s);
+        SR_HIP(hipStreamSynchronize(s));
+        sync();
+        if (rank != root) h2d(buf, slot(root), count * 8, s);
+        SR_HIP(hipStreamSynchronize(s));
+        sync();
+    }
+    void all_reduce(u64* buf, u64 count, RedOp op, hipStream_t s) override {
+        need(count * 8);
+        d2h(slot(rank), buf, count * 8, s);
+        SR_HIP(hipStreamSynchronize(s));
+        sync();
+        std::vector<u64> v(count);
+        std::memcpy(v.data(), slot(0), count * 8);
+        for (int q = 1; q < world; ++q) {
+            const u64* x = reinterpret_cast<const u64*>(slot(q));
+            for (u64 i = 0; i < count; ++i)
+                v[i] = op == RedOp::Min ? std::min(v[i], x[i]) : op == RedOp::Max ? std::max(v[i], x[i]) : v[i] + x[i];
+        }
+        sync();  // every rank has read every slot
+        h2d(buf, v.data(), count * 8, s);
+        SR_HIP(hipStreamSynchronize(s));
+    }
+    bool peer_capable() const override { return direct_env_on(); }
+    bool distinct_devices() const override { return devices_distinct; }
+    void share(const void* mine, size_t b, void* all, hipStream_t s) override {
+        need(b);
+        SR_HIP(hipStreamSynchronize(s));
+        std::memcpy(slot(rank), mine, b);
+        sync();
+        for (int q = 0; q < world; ++q) std::memcpy(static_cast<char*>(all) + (size_t)q * b, slot(q), b);
+        sync();
+    }
+    PeerBlob export_buf(void* p) const override { return IpcMaps::export_of(device, p); }
+    u64* map(int q, const PeerBlob& b) override { return ipc.open(device, q, b); }
 };
 
 // Per-device resources of the partitioned engine, pooled across checks like the single-GPU

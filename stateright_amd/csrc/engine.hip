@@ -600,6 +600,20 @@ int32_t sr_dist_local_group(int32_t world, const int32_t* devices, sr_dist** out
     }
 }
 
+sr_dist* sr_dist_shm_init(int32_t rank, int32_t world, const char* name, int32_t device, int64_t slot_bytes,
+                          int32_t devices_distinct) {
+    try {
+        if (world < 1 || rank < 0 || rank >= world || !name || slot_bytes < 4096) throw Error(SR_ERR_ARG, "bad shm communicator");
+        SR_HIP(hipSetDevice(device));
+        auto d = std::make_unique<sr_dist>();
+        d->c = std::make_unique<ShmComm>(rank, world, std::string(name), device, (size_t)slot_bytes, devices_distinct != 0);
+        return d.release();
+    } catch (const std::exception& x) {
+        set_error(x.what());
+        return nullptr;
+    }
+}
+
 int32_t sr_dist_rank(const sr_dist* d) { return d ? d->c->rank : SR_ERR_ARG; }
 int32_t sr_dist_world(const sr_dist* d) { return d ? d->c->world : SR_ERR_ARG; }
 int32_t sr_dist_nranks(const sr_dist* d) { return d ? d->c->nranks() : SR_ERR_ARG; }

@@ -10,7 +10,8 @@ The RCCL communicator is created natively (sr_dist_init). Its 128-byte unique id
 rank 0 to the others either through a file next to the launcher (`from_env`, one node) or through
 an initialised torch.distributed group (`from_torch`). `local_group(world)` builds `world` ranks
 that are threads of this process (the in-process transport of include/stateright_gpu.h), which
-runs the engine's multi-rank code on one GPU.
+runs the engine's multi-rank code on one GPU. `shm(rank, world, name)` makes the ranks separate
+processes of one host with a shared-memory host transport (tests and rehearsals on one GPU).
 """
 import ctypes
 import os
@@ -94,6 +95,19 @@ class Communicator:
         if lib.sr_dist_local_group(world, devs, handles) != 0:
             raise CheckerError("sr_dist_local_group")
         return [cls._wrap(handles[r], devs[r]) for r in range(world)]
+
+    @classmethod
+    def shm(cls, rank, world, name, device=0, slot_bytes=64 << 20, devices_distinct=False):
+        """One rank of `world` PROCESSES of this host whose host-side transport is the POSIX
+        shared-memory segment `name` (every rank passes the same name). Its collectives are staged
+        host copies; the partitioned levels use the direct exchange through IPC, as under RCCL. It
+        runs the one-process-per-GPU code path with all ranks on ONE GPU, where RCCL refuses two
+        ranks on one device."""
+        lib = N.load()
+        h = lib.sr_dist_shm_init(rank, world, name.encode(), device, slot_bytes, 1 if devices_distinct else 0)
+        if not h:
+            raise CheckerError("sr_dist_shm_init")
+        return cls._wrap(h, device)
 
     def kind(self):
         buf = ctypes.create_string_buffer(16)

@@ -1,0 +1,77 @@
+"""The one-process-per-GPU path (what `bench.py --gpus N` runs on a node) as separate PROCESSES on
+one MI355X: two ranks joined by the shared-memory communicator (RCCL refuses two ranks on one
+device), each a fresh interpreter started with subprocess (tests/shm_rank_worker.py). The
+partitioned levels use the direct exchange across processes (IPC handles of pool buffers, device
+flags), its set-up reused over consecutive checks and redone when buffers grow; SR_DIRECT=0 runs
+the collective exchange instead. Counts must equal the oracle's on every rank."""
+import json
+import os
+import subprocess
+import sys
+import uuid
+
+import pytest
+
+from oracle_lib import INCREMENT_LOCK, TWO_PHASE, OracleRun
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def run_ranks(checks, world=2, distinct=False, env=None, timeout=240):
+    name = f"/sr_test_{os.getpid()}_{uuid.uuid4().hex[:8]}"
+    e = dict(os.environ, **(env or {}))
+    procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "shm_rank_worker.py"), str(r), str(world), name,
+                               "1" if distinct else "0", *checks], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                              text=True, env=e) for r in range(world)]
+    outs = []
+    for p in procs:
+        try:
+            o, err = p.communicate(timeout=timeout)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+        assert p.returncode == 0, err[-2000:]
+        outs.append([json.loads(line) for line in o.splitlines() if line.startswith("{")])
+    return outs
+
+
+def expect(spec):
+    model, n = spec.split(":")
+    o = OracleRun(TWO_PHASE if model == "2pc" else INCREMENT_LOCK, [int(n)])
+    return o.unique_state_count, o.state_count, o.max_depth, o.discovery_names()
+
+
+@pytest.mark.parametrize("direct", ["1", "0"], ids=["direct", "collective"])
+def test_processes_match_oracle(direct):
+    # consecutive checks on the same ranks: the direct exchange's set-up is reused (2pc 5 twice),
+    # grows with a larger check (2pc 7, increment_lock 7) and is reused again
+    checks = ["2pc:5", "2pc:5", "2pc:7", "inclock:7", "2pc:5"]
+    outs = run_ranks(checks, env={"SR_DIRECT": direct, "SR_HEAD_MAX": "0"})
+    for rank_out in outs:
+        assert [r["check"] for r in rank_out] == checks
+        for r in rank_out:
+            assert (r["unique"], r["states"], r["depth"], r["discoveries"]) == expect(r["check"])
+            assert r["pipelined"] == (2 if direct == "1" else 1)
+
+
+def test_processes_bench_config_with_head():
+    # the bench's configuration (2pc N=9, replicated head, then partitioned levels), twice
+    n = 9
+    outs = run_ranks(["2pc:9", "2pc:9"])
+    for rank_out in outs:
+        for r in rank_out:
+            assert r["unique"] == 6 ** n + 4 ** n + 2 ** n and r["depth"] == 3 * n + 1
+            assert r["pipelined"] == 2 and r["restarts"] == 0
+
+
+def test_processes_fused_wait():
+    # ranks declared on distinct devices: the insert grid polls the flags itself (what one process
+    # per GPU runs). On ONE shared GPU this is safe only for tiny grids (a spinning insert grid must
+    # not hold the CUs the other process's expand grid needs): 2pc N=4, every level a few blocks.
+    outs = run_ranks(["2pc:4", "2pc:4"], distinct=True, env={"SR_HEAD_MAX": "0"})
+    for rank_out in outs:
+        for r in rank_out:
+            assert (r["unique"], r["states"], r["depth"], r["discoveries"]) == expect(r["check"])
+            assert r["pipelined"] == 2
