@@ -1142,7 +1142,8 @@ class DistEngine final : public EngineBase {
                 const u32 ppw_log2 = route_ppw_env_ >= 0 ? (u32)route_ppw_env_ : ppw_for(p.n_est);
                 const u32 grid = (u32)std::min<u64>(std::max<u64>(1, blocks_for(p.n_hi, 4u << ppw_log2)), route_grid_cap());
                 u64* row = comm_ ? rows_mine_.p : rows_all_.p + (u64)p.id * RW;
-                expand_route<M, 1><<<grid, 256, route_lds(), stream_>>>(
+                auto route = self_rec() ? expand_route<M, 1, true> : expand_route<M, 1, false>;
+                route<<<grid, 256, route_lds(), stream_>>>(
                     m_, p.arena.p, p.apar.p, nb, p.arena_cap, p.view(), p.id, T_, p.send.p, (u32)p.bucket_cap,
                     p.sendc.p, p.lc, p.ctl, undiscovered, row, ppw_log2, filt_log2_, p.bucket_cap * REC, 0u,
                     p.sent_mask ? p.sent.p : nullptr, p.sent_mask, rstage_recs(), nullptr, nullptr, 0u, self_rec());
@@ -1446,7 +1447,8 @@ class DistEngine final : public EngineBase {
             const u32 ppw_log2 = route_ppw_env_ >= 0 ? (u32)route_ppw_env_ : ppw_for(n_plan[p.id]);
             const u32 grid = (u32)std::min<u64>(std::max<u64>(1, blocks_for(n_plan[p.id], 4u << ppw_log2)), route_grid_cap());
             u64* row = comm_ ? rows_mine_.p : rows_all_.p + (u64)p.id * RW;
-            expand_route<M, 1><<<grid, 256, route_lds(), stream_>>>(
+            auto route = self_rec() ? expand_route<M, 1, true> : expand_route<M, 1, false>;
+            route<<<grid, 256, route_lds(), stream_>>>(
                 m_, p.arena.p, p.apar.p, 0, p.arena_cap, p.view(), p.id, T_, direct_ ? nullptr : p.send.p + DIST_HDR,
                 (u32)C, p.sendc.p, p.lc, p.ctl, undiscovered, row, ppw_log2, filt_log2_, S, 1u,
                 p.sent_mask ? p.sent.p : nullptr, p.sent_mask, rstage_recs(), direct_ ? ctx_->parts[p.res].ptab[par].p : nullptr,
@@ -1991,7 +1993,8 @@ class DistEngine final : public EngineBase {
         if (const char* e = std::getenv("SR_ROUTE_GRID_MAX"))
             if (std::atoi(e) > 0) return route_grid_max_ = (u32)std::atoi(e);
         int per_cu = 0, cus = 0;
-        SR_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)expand_route<M, 1>, 256, route_lds()));
+        const void* k = self_rec() ? (const void*)expand_route<M, 1, true> : (const void*)expand_route<M, 1, false>;
+        SR_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 256, route_lds()));
         SR_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, o_.device));
         route_grid_max_ = per_cu > 0 && cus > 0 ? (u32)(2 * per_cu * cus) : 8192u;
         return route_grid_max_;

@@ -134,7 +134,7 @@ __host__ __device__ __forceinline__ u32 route_local_stage(u32 nparts, int W, u32
 // bucket counters are the only same-address atomics, so they must be rare: per-successor or
 // per-wave reservations serialise at the L2 when every wave of the GPU targets T addresses.
 // A stage that overflows (a chunk larger than planned) falls back to per-wave reservations.
-template <class M, int PB>
+template <class M, int PB, bool SELF = false>
 __global__ void __launch_bounds__(256) expand_route(M m, u64* __restrict__ arena, u64* __restrict__ apar, u64 nb,
                                                     u64 arena_cap, TableView t, u32 my_part, u32 nparts,
                                                     u64* __restrict__ send, u32 bucket_cap, u32* send_counts,
@@ -145,7 +145,13 @@ __global__ void __launch_bounds__(256) expand_route(M m, u64* __restrict__ arena
     // self_rec: successors owned by this partition become records too (to its own slot), so this
     // kernel probes nothing and has no global round trip per round of successors: with many
     // partitions 1/T of the lanes probed and the whole wave waited for them. The insert kernel
-    // then probes every successor, with its batched probes.
+    // then probes every successor, with its batched probes. SELF = the same, fixed at compile time:
+    // the instantiation for self records has no probe, claim, local stage or sent-cache code at all
+    // (the kernel is instruction-bound there: profiles/r03_pmc_instruction_mix.txt).
+    if constexpr (SELF) {
+        self_rec = 1;
+        sent = nullptr;
+    }
     // Destinations. Exchanged buckets (ptab == nullptr): owner q's records go to this partition's
     // own send bucket q, send + q * bucket_stride. Direct exchange: straight into slot my_part of
     // owner q's receive buffer, ptab[q] + my_part * bucket_stride (both past the header; the row
@@ -282,7 +288,7 @@ __global__ void __launch_bounds__(256) expand_route(M m, u64* __restrict__ arena
                     }
                 }
                 own[j] = ok[j] ? owner_of(key[j], nparts) : my_part;
-                rem[j] = ok[j] && (self_rec || own[j] != my_part);
+                rem[j] = ok[j] && (SELF || self_rec || own[j] != my_part);
             }
             // One memory round trip per round: a local successor's visited-set probe and a remote
             // one's sent-cache lookup are issued together (the lookup used to be resolved before
@@ -293,10 +299,10 @@ __global__ void __launch_bounds__(256) expand_route(M m, u64* __restrict__ arena
             // eviction or a race only re-sends (the owner dedups).
 #pragma unroll
             for (int j = 0; j < PB; ++j)
-                cur[j] = !ok[j] ? 0 : !rem[j] ? probe_load<0>(&t.keys[pk[j].home]) : sent ? sent[key[j] & sent_mask] : 0;
+                cur[j] = SELF || !ok[j] ? 0 : !rem[j] ? probe_load<0>(&t.keys[pk[j].home]) : sent ? sent[key[j] & sent_mask] : 0;
 #pragma unroll
             for (int j = 0; j < PB; ++j) {
-                if (!(sent && rem[j])) continue;
+                if (SELF || !(sent && rem[j])) continue;
                 if (cur[j] == key[j]) {
                     ++succ;
                     ok[j] = rem[j] = false;
@@ -310,14 +316,14 @@ __global__ void __launch_bounds__(256) expand_route(M m, u64* __restrict__ arena
                 nw[j] = false;
                 if (!ok[j]) continue;
                 ++succ;
-                if (rem[j] || cur[j] == pk[j].tag) continue;
+                if (SELF || rem[j] || cur[j] == pk[j].tag) continue;
                 find_or_claim_from<0>(t, pk[j], cur[j], &nw[j], &lc->err);
             }
 #pragma unroll
             for (int j = 0; j < PB; ++j) {
                 const u64 pg = gid_base + wave0 + par[j];
                 // local new states -> the chunk's stage (one LDS atomic per wave)
-                const u64 mask = __ballot(nw[j]);
+                const u64 mask = SELF ? 0ull : __ballot(nw[j]);
                 if (mask) {
                     const u32 cnt = __popcll(mask);
                     const u32 below = __popcll(mask & lanes_below);
