@@ -675,7 +675,10 @@ __global__ void __launch_bounds__(256) expand_fast(M m, const u64* __restrict__ 
     // successor lane reads its (parent, action) with one LDS load; the binary search over the
     // parents' prefix sums (6 dependent LDS loads) and the k-th-set-bit select it replaces were
     // the largest per-successor costs.
-    constexpr u32 MAPCAP = 1024;
+#ifndef SR_MAPCAP
+#define SR_MAPCAP 1024
+#endif
+    constexpr u32 MAPCAP = SR_MAPCAP;
     static_assert(MW * 64 <= 1024, "action ids must fit 10 bits");
     __shared__ u16 smap[4][MAPCAP];
     __shared__ u32 stage_n, base, scratch[8];
