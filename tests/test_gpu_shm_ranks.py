@@ -75,3 +75,19 @@ def test_processes_fused_wait():
         for r in rank_out:
             assert (r["unique"], r["states"], r["depth"], r["discoveries"]) == expect(r["check"])
             assert r["pipelined"] == 2
+
+
+def test_bench_two_ranks_rehearsal():
+    # bench.py's multi-process flow (torch.distributed.run as a child, one rank per process, timing
+    # barrier, max over ranks, the replicas leg) with both ranks on this GPU over the shared-memory
+    # transport: one JSON line from rank 0, the partitioned check on the direct exchange.
+    root = os.path.dirname(HERE)
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--comm", "shm", "--steps", "2",
+                        "--warmup", "1", "--config4-steps", "0"], capture_output=True, text=True, timeout=300, cwd=root)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["world_size"] == 2 and d["config"]["comm"] == "shm"
+    assert "direct exchange" in d["config"]["parallelism"]
+    assert d["replicas"]["n_gpus"] == 2 and d["value"] > 0
