@@ -3,7 +3,9 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -25,6 +27,29 @@ struct Error : std::runtime_error {
             throw ::sr::Error(-2, std::string(#expr) + ": " + hipGetErrorString(e_) + " at " +   \
                                       __FILE__ + ":" + std::to_string(__LINE__));                 \
     } while (0)
+
+// The host waits until every launch enqueued on `s` has finished: a spin on hipStreamQuery for up
+// to ~0.5 ms, then a blocking wait. A blocking hipStreamSynchronize returned ~30 us after the last
+// kernel had ended (measured at the end of a 2pc N=9 check), and a check's host path has a few
+// such waits on short device work (votes, counters, the last level).
+// A query that answered "not ready" may leave hipErrorNotReady as the thread's last error: cleared
+// here (only that one) so that a later hipGetLastError after a launch does not report it.
+inline void clear_not_ready() {
+    if (hipPeekAtLastError() == hipErrorNotReady) (void)hipGetLastError();
+}
+inline hipError_t stream_sync(hipStream_t s) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (unsigned spin = 1;; ++spin) {
+        const hipError_t e = hipStreamQuery(s);
+        if (e != hipErrorNotReady) {
+            if (spin > 1) clear_not_ready();
+            return e;
+        }
+        if ((spin & 255) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(500))
+            return clear_not_ready(), hipStreamSynchronize(s);
+        __builtin_ia32_pause();
+    }
+}
 
 // Process-wide caching allocator: freed blocks go to a per-(device, size) free list. Sizes are
 // rounded up to 2 MiB (or a power of two below that) so that a run with a slightly different
@@ -60,12 +85,56 @@ class DevicePool {
         std::lock_guard<std::mutex> g(mu_);
         free_[{dev, round(bytes)}].push_back(p);
     }
+    // Blocks handed back while the work that zeroes them is still in flight: `ready` is recorded
+    // behind that work. A check returns its visited set this way as soon as its last level is
+    // done, and the clear then runs while the host finishes that check and sets up the next one.
+    void free_zeroed(int dev, void* p, size_t bytes, hipEvent_t ready) {
+        std::lock_guard<std::mutex> g(mu_);
+        zeroed_[{dev, round(bytes)}].push_back({p, ready});
+    }
+    // A zeroed block of this size if one is pooled, with `s` ordered after its clear on the device
+    // (the host does not wait), else nullptr. A block whose clear has finished is preferred.
+    void* alloc_zeroed(int dev, size_t bytes, hipStream_t s) {
+        Zeroed z{nullptr, nullptr};
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            auto& fl = zeroed_[{dev, round(bytes)}];
+            if (fl.empty()) return nullptr;
+            size_t pick = 0;
+            for (size_t i = 0; i < fl.size(); ++i)
+                if (hipEventQuery(fl[i].ready) == hipSuccess) {
+                    pick = i;
+                    break;
+                }
+            clear_not_ready();
+            z = fl[pick];
+            fl.erase(fl.begin() + (long)pick);
+        }
+        const hipError_t e = hipStreamWaitEvent(s, z.ready, 0);
+        if (e != hipSuccess) {
+            (void)hipEventSynchronize(z.ready);
+            (void)hipEventDestroy(z.ready);
+            free(dev, z.p, bytes);  // not known to be ordered for this stream: an ordinary block
+            return nullptr;
+        }
+        (void)hipEventDestroy(z.ready);  // the wait holds what it needs
+        return z.p;
+    }
     void release_all(int dev) {
         std::lock_guard<std::mutex> g(mu_);
         ++epoch_[dev];  // blocks may come back at the same addresses: peers' IPC mappings are stale
         for (auto& [k, v] : free_)
             if (k.first == dev) {
                 for (void* p : v) (void)hipFree(p);
+                v.clear();
+            }
+        for (auto& [k, v] : zeroed_)
+            if (k.first == dev) {
+                for (auto& z : v) {
+                    (void)hipEventSynchronize(z.ready);
+                    (void)hipEventDestroy(z.ready);
+                    (void)hipFree(z.p);
+                }
                 v.clear();
             }
     }
@@ -84,8 +153,13 @@ class DevicePool {
     }
 
   private:
+    struct Zeroed {
+        void* p;
+        hipEvent_t ready;
+    };
     std::mutex mu_;
     std::map<std::pair<int, size_t>, std::vector<void*>> free_;
+    std::map<std::pair<int, size_t>, std::vector<Zeroed>> zeroed_;
     std::map<int, uint64_t> epoch_;
 };
 
@@ -111,6 +185,35 @@ struct DBuf {
         n = count ? count : 1;
         p = static_cast<T*>(DevicePool::get().alloc(d, n * sizeof(T)));
     }
+    // All-zero bytes, ordered before the work enqueued on `s` afterwards: a pooled zeroed block,
+    // or a fresh one cleared on `s`.
+    void alloc_zero(int d, size_t count, hipStream_t s) {
+        reset();
+        dev = d;
+        n = count ? count : 1;
+        p = static_cast<T*>(DevicePool::get().alloc_zeroed(d, n * sizeof(T), s));
+        if (p) return;
+        p = static_cast<T*>(DevicePool::get().alloc(d, n * sizeof(T)));
+        SR_HIP(hipMemsetAsync(p, 0, n * sizeof(T), s));
+    }
+    // Hands the block back to be zeroed on `s` behind the work enqueued there so far (alloc_zero
+    // takes it without a clear at its start). Falls back to an ordinary free on any error.
+    void release_zero(hipStream_t s) noexcept {
+        if (!p) return;
+        hipEvent_t ready = nullptr;
+        if (hipEventCreateWithFlags(&ready, hipEventDisableTiming) == hipSuccess) {
+            if (hipMemsetAsync(p, 0, n * sizeof(T), s) == hipSuccess && hipEventRecord(ready, s) == hipSuccess) {
+                DevicePool::get().free_zeroed(dev, p, n * sizeof(T), ready);
+                p = nullptr;
+                n = 0;
+                return;
+            }
+            (void)hipEventDestroy(ready);
+        }
+        (void)hipStreamSynchronize(s);  // no writer of the block may still be in flight
+        (void)hipGetLastError();
+        reset();
+    }
     void swap(DBuf& o) {
         std::swap(p, o.p);
         std::swap(n, o.n);
@@ -130,11 +233,13 @@ struct DeviceContext {
     HostMirror* hc_dev = nullptr;  // the same memory, device pointer
     uint32_t seq = 0;
     std::vector<hipEvent_t> events;
+    hipEvent_t done = nullptr;  // marks a point of the stream the host waits for (no timing)
 
     void init(int d) {
         dev = d;
         SR_HIP(hipSetDevice(d));
         SR_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+        SR_HIP(hipEventCreateWithFlags(&done, hipEventDisableTiming));
         SR_HIP(hipMalloc(&lc, sizeof(Counters)));
         // two mirrors: launch `seq` publishes to slot seq & 1, so a launch may run while the host
         // still reads the previous one's snapshot

@@ -104,7 +104,7 @@ struct Comm {
         one.alloc(device, 1);
         SR_HIP(hipMemsetAsync(one.p, 0, 8, s));
         all_reduce(one.p, 1, RedOp::Sum, s);
-        SR_HIP(hipStreamSynchronize(s));
+        SR_HIP(stream_sync(s));
     }
 
     // ---- direct exchange (peer pointers) ----
@@ -160,7 +160,7 @@ inline bool Comm::probe_direct(hipStream_t s) {
         SR_HIP(hipMemcpyAsync(v.p, &vote, 8, hipMemcpyHostToDevice, s));
         all_reduce(v.p, 1, RedOp::Min, s);
         SR_HIP(hipMemcpyAsync(&vote, v.p, 8, hipMemcpyDeviceToHost, s));
-        SR_HIP(hipStreamSynchronize(s));
+        SR_HIP(stream_sync(s));
         return vote == 1;
     };
     direct_ok = 0;
@@ -173,7 +173,7 @@ inline bool Comm::probe_direct(hipStream_t s) {
     lcbuf.alloc(device, (sizeof(LevelCounters) + 7) / 8);
     SR_HIP(hipMemsetAsync(flags.p, 0, world * 4, s));
     SR_HIP(hipMemsetAsync(lcbuf.p, 0, sizeof(LevelCounters), s));
-    SR_HIP(hipStreamSynchronize(s));
+    SR_HIP(stream_sync(s));
     u64 ok = 1;
     PeerBlob b;
     try {
@@ -201,7 +201,7 @@ inline bool Comm::probe_direct(hipStream_t s) {
     SR_HIP(hipGetLastError());
     u32 err = 0;
     SR_HIP(hipMemcpyAsync(&err, &lc->err, 4, hipMemcpyDeviceToHost, s));
-    SR_HIP(hipStreamSynchronize(s));
+    SR_HIP(stream_sync(s));
     if (err) flags.p = nullptr;  // a late peer store may still land: never reuse the block
     direct_ok = agree(err == 0 ? 1 : 0) ? 1 : 0;
     return direct_ok == 1;
@@ -294,7 +294,7 @@ struct RcclComm final : Comm {
         SR_NCCL(ncclAllGather(d.p + (u64)rank * words, d.p, words, ncclUint64, nccl, s));
         std::vector<u64> h(words * world);
         SR_HIP(hipMemcpyAsync(h.data(), d.p, words * world * 8, hipMemcpyDeviceToHost, s));
-        SR_HIP(hipStreamSynchronize(s));
+        SR_HIP(stream_sync(s));
         for (int q = 0; q < world; ++q)
             std::memcpy(static_cast<char*>(all) + (size_t)q * bytes, h.data() + (u64)q * words, bytes);
     }
@@ -446,7 +446,7 @@ struct LocalComm final : Comm {
         copy(tmp.p, g->slots[root].send, count * 8, s);
         leave(s);
         copy(buf, tmp.p, count * 8, s);
-        SR_HIP(hipStreamSynchronize(s));  // tmp returns to the pool at scope exit
+        SR_HIP(stream_sync(s));  // tmp returns to the pool at scope exit
     }
     void all_reduce(u64* buf, u64 count, RedOp op, hipStream_t s) override {
         DBuf<u64> all;  // every rank's vector, reduced locally on the device
@@ -456,7 +456,7 @@ struct LocalComm final : Comm {
         leave(s);
         reduce_rows<<<blocks_for(count, 256), 256, 0, s>>>(all.p, (u32)world, count, (u32)op, buf);
         SR_HIP(hipGetLastError());
-        SR_HIP(hipStreamSynchronize(s));  // `all` returns to the pool at scope exit
+        SR_HIP(stream_sync(s));  // `all` returns to the pool at scope exit
     }
 
     // Direct exchange between threads of one process: raw device pointers (peer access enabled
@@ -468,7 +468,7 @@ struct LocalComm final : Comm {
         return (int)d.size() == world;
     }
     void share(const void* mine, size_t bytes, void* all, hipStream_t s) override {
-        SR_HIP(hipStreamSynchronize(s));
+        SR_HIP(stream_sync(s));
         auto& sl = g->slots[rank];
         sl.op = SHARE;
         sl.count = bytes;
@@ -577,19 +577,19 @@ struct ShmComm final : Comm {
     void all_to_all(const u64* send, u64* recv, u64 count, hipStream_t s) override {
         need(count * 8 * (size_t)world);
         d2h(slot(rank), send, count * 8 * world, s);
-        SR_HIP(hipStreamSynchronize(s));
+        SR_HIP(stream_sync(s));
         sync();
         for (int q = 0; q < world; ++q) h2d(recv + (u64)q * count, slot(q) + (size_t)rank * count * 8, count * 8, s);
-        SR_HIP(hipStreamSynchronize(s));
+        SR_HIP(stream_sync(s));
         sync();
     }
     void all_gather(const u64* mine, u64* all, u64 count, hipStream_t s) override {
         need(count * 8);
         d2h(slot(rank), mine, count * 8, s);
-        SR_HIP(hipStreamSynchronize(s));
+        SR_HIP(stream_sync(s));
         sync();
         for (int q = 0; q < world; ++q) h2d(all + (u64)q * count, slot(q), count * 8, s);
-        SR_HIP(hipStreamSynchronize(s));
+        SR_HIP(stream_sync(s));
         sync();
     }
     void exchange(const std::vector<const u64*>& send, const std::vector<u64>& scount, const std::vector<u64*>& recv,
@@ -605,7 +605,7 @@ struct ShmComm final : Comm {
             d2h(slot(rank) + off, send[q], scount[q] * 8, s);
             off += scount[q] * 8;
         }
-        SR_HIP(hipStreamSynchronize(s));
+        SR_HIP(stream_sync(s));
         sync();
         for (int q = 0; q < world; ++q) {
             const u64* m = reinterpret_cast<const u64*>(slot(q));
@@ -614,22 +614,22 @@ struct ShmComm final : Comm {
                                             " words, rank " + std::to_string(rank) + " expects " + std::to_string(rcount[q]));
             h2d(recv[q], slot(q) + m[rank], rcount[q] * 8, s);
         }
-        SR_HIP(hipStreamSynchronize(s));
+        SR_HIP(stream_sync(s));
         sync();
     }
     void broadcast(u64* buf, u64 count, int root, hipStream_t s) override {
         need(count * 8);
         if (rank == root) d2h(slot(root), buf, count * 8, s);
-        SR_HIP(hipStreamSynchronize(s));
+        SR_HIP(stream_sync(s));
         sync();
         if (rank != root) h2d(buf, slot(root), count * 8, s);
-        SR_HIP(hipStreamSynchronize(s));
+        SR_HIP(stream_sync(s));
         sync();
     }
     void all_reduce(u64* buf, u64 count, RedOp op, hipStream_t s) override {
         need(count * 8);
         d2h(slot(rank), buf, count * 8, s);
-        SR_HIP(hipStreamSynchronize(s));
+        SR_HIP(stream_sync(s));
         sync();
         std::vector<u64> v(count);
         std::memcpy(v.data(), slot(0), count * 8);
@@ -640,13 +640,13 @@ struct ShmComm final : Comm {
         }
         sync();  // every rank has read every slot
         h2d(buf, v.data(), count * 8, s);
-        SR_HIP(hipStreamSynchronize(s));
+        SR_HIP(stream_sync(s));
     }
     bool peer_capable() const override { return direct_env_on(); }
     bool distinct_devices() const override { return devices_distinct; }
     void share(const void* mine, size_t b, void* all, hipStream_t s) override {
         need(b);
-        SR_HIP(hipStreamSynchronize(s));
+        SR_HIP(stream_sync(s));
         std::memcpy(slot(rank), mine, b);
         sync();
         for (int q = 0; q < world; ++q) std::memcpy(static_cast<char*>(all) + (size_t)q * b, slot(q), b);
@@ -795,7 +795,7 @@ class DistEngine final : public EngineBase {
     }
     ~DistEngine() override {
         if (ctx_) {
-            (void)hipStreamSynchronize(stream_);
+            (void)stream_sync(stream_);
             for (size_t i = 0; i < parts_.size(); ++i) ctx_->parts[i].seq = parts_[i].seq;
             ContextPool<DistContext>::get().release(ctx_);
         }
@@ -843,7 +843,7 @@ class DistEngine final : public EngineBase {
                 return;
             } catch (const Error& e) {
                 if (e.code != SR_ERR_CAPACITY || attempt >= 3) throw;
-                SR_HIP(hipStreamSynchronize(stream_));
+                SR_HIP(stream_sync(stream_));
                 stats.restarts++;
                 restarts_++;
                 if (head_failed_) {  // the head's scratch buffers were too small: no head
@@ -885,14 +885,14 @@ class DistEngine final : public EngineBase {
             SR_HIP(hipMemcpyAsync(buf.p, &len, 8, hipMemcpyHostToDevice, stream_));
             comm_->broadcast(buf.p, 1, 0, stream_);
             SR_HIP(hipMemcpyAsync(&len, buf.p, 8, hipMemcpyDeviceToHost, stream_));
-            SR_HIP(hipStreamSynchronize(stream_));
+            SR_HIP(stream_sync(stream_));
             buf.alloc(o_.device, std::max<u64>(1, len));
             if (comm_->rank == 0 && len)
                 SR_HIP(hipMemcpyAsync(buf.p, paths_[p].data(), len * 8, hipMemcpyHostToDevice, stream_));
             comm_->broadcast(buf.p, std::max<u64>(1, len), 0, stream_);
             paths_[p].resize(len);
             if (len) SR_HIP(hipMemcpyAsync(paths_[p].data(), buf.p, len * 8, hipMemcpyDeviceToHost, stream_));
-            SR_HIP(hipStreamSynchronize(stream_));
+            SR_HIP(stream_sync(stream_));
         }
         paths_ready_ = true;
     }
@@ -979,7 +979,7 @@ class DistEngine final : public EngineBase {
         p.apar.swap(np);
         p.arena_cap = cap;
         arena_grows_++;
-        SR_HIP(hipStreamSynchronize(stream_));
+        SR_HIP(stream_sync(stream_));
     }
 
     hipEvent_t event(size_t i) {
@@ -1001,7 +1001,7 @@ class DistEngine final : public EngineBase {
         SR_HIP(hipMemsetAsync(p.keys.p, 0, p.cap * 8, stream_));
         rehash<<<blocks_for(old_cap, 256), 256, 0, stream_>>>(make_table_view(m_, ok.p, nullptr, old_cap), old_cap, p.view(), &p.lc->err);
         SR_HIP(hipGetLastError());
-        SR_HIP(hipStreamSynchronize(stream_));
+        SR_HIP(stream_sync(stream_));
         stats.rehashes++;
     }
 
@@ -1074,7 +1074,7 @@ class DistEngine final : public EngineBase {
             insert_roots_part<M><<<1, 64, 0, stream_>>>(m_, p.view(), dinit.p, (u32)k, p.id, T_, p.arena.p, p.apar.p, dn.p, p.lc);
             u32 n0 = 0;
             SR_HIP(hipMemcpyAsync(&n0, dn.p, 4, hipMemcpyDeviceToHost, stream_));
-            SR_HIP(hipStreamSynchronize(stream_));
+            SR_HIP(stream_sync(stream_));
             p.n = n0;
             if (n0) eval_roots<M><<<blocks_for(n0, 64), 64, 0, stream_>>>(m_, p.arena.p, n0, p.lc, (1u << M::NPROPS) - 1);
             p.seq++;
@@ -1088,12 +1088,12 @@ class DistEngine final : public EngineBase {
             c0.roots = p.last.claims;
             for (int pr = 0; pr < MAX_PROPS; ++pr) c0.disc_prev[pr] = pr < M::NPROPS ? p.last.disc[pr] : ~0u;
             SR_HIP(hipMemcpyAsync(p.ctl, &c0, sizeof(c0), hipMemcpyHostToDevice, stream_));
-            SR_HIP(hipStreamSynchronize(stream_));
+            SR_HIP(stream_sync(stream_));
             p.uniq = p.last.claims;
             p.n_hi = n0;
             p.n_est = n0;
         }
-        SR_HIP(hipStreamSynchronize(stream_));
+        SR_HIP(stream_sync(stream_));
         state_count = (u64)k;
         u64 unique_total = 0;
         if (use_head) run_head(rev, k, unique_total);
@@ -1400,7 +1400,7 @@ class DistEngine final : public EngineBase {
             SR_HIP(hipGetLastError());
             u32 h[2];
             SR_HIP(hipMemcpyAsync(h, cnt.p, 8, hipMemcpyDeviceToHost, stream_));
-            SR_HIP(hipStreamSynchronize(stream_));
+            SR_HIP(stream_sync(stream_));
             if (h[0] > p.arena_cap) throw Error(SR_ERR_CAPACITY, "replicated head: arena of a partition too small");
             p.n = h[0];
             p.uniq = h[1];
@@ -1411,7 +1411,7 @@ class DistEngine final : public EngineBase {
             for (int pr = 0; pr < MAX_PROPS; ++pr) c0.disc_prev[pr] = ~0u;  // evaluated in the head
             SR_HIP(hipMemcpyAsync(p.ctl, &c0, sizeof(c0), hipMemcpyHostToDevice, stream_));
         }
-        SR_HIP(hipStreamSynchronize(stream_));
+        SR_HIP(stream_sync(stream_));
         stats.head_levels = level;
     }
 
@@ -1433,7 +1433,7 @@ class DistEngine final : public EngineBase {
             bool sync = false;
             for (auto& p : parts_) {
                 if (p.send_words < S * T_ || p.recv_words < S * T_) {
-                    if (!sync) SR_HIP(hipStreamSynchronize(stream_));  // in-flight levels use the old buffers
+                    if (!sync) SR_HIP(stream_sync(stream_));  // in-flight levels use the old buffers
                     sync = true;
                     const u64 words = std::max<u64>(S * T_, p.send_words * 2);
                     p.send.alloc(o_.device, words);
@@ -1498,7 +1498,7 @@ class DistEngine final : public EngineBase {
         for (auto& p : parts_) grow |= R(p).drecv_words < S * T_;
         if (!grow) return;
         if (comm_) comm_->barrier(stream_);
-        else SR_HIP(hipStreamSynchronize(stream_));
+        else SR_HIP(stream_sync(stream_));
         for (auto& p : parts_) {
             const u64 words = std::max<u64>(S * T_, R(p).drecv_words * 2);
             for (int k = 0; k < 2; ++k) R(p).drecv[k].alloc(o_.device, words);
@@ -1517,7 +1517,7 @@ class DistEngine final : public EngineBase {
                 SR_HIP(hipMemcpyAsync(R(p).ptab[k].p, owners.data(), T_ * sizeof(u64*), hipMemcpyHostToDevice, stream_));
             }
         }
-        SR_HIP(hipStreamSynchronize(stream_));  // the host tables may go
+        SR_HIP(stream_sync(stream_));  // the host tables may go
         direct_grows_++;
     }
 
@@ -1543,7 +1543,7 @@ class DistEngine final : public EngineBase {
             SR_HIP(hipMemcpyAsync(dv.p, v, sizeof(v), hipMemcpyHostToDevice, stream_));
             comm_->all_reduce(dv.p, 5, RedOp::Min, stream_);
             SR_HIP(hipMemcpyAsync(v, dv.p, sizeof(v), hipMemcpyDeviceToHost, stream_));
-            SR_HIP(hipStreamSynchronize(stream_));
+            SR_HIP(stream_sync(stream_));
             reuse = v[0] == 1 && v[1] == ~v[2] && v[3] == ~v[4];  // everyone holds the same set-up
             gen = ~v[4] + 1;  // a new set-up's generation: past every rank's
         }
@@ -1569,7 +1569,7 @@ class DistEngine final : public EngineBase {
             for (u32 q = 0; q < T_; ++q) ft[q] = reinterpret_cast<u32*>(owners[q]) + comm_->rank;
             d.ftab.alloc(o_.device, T_);
             SR_HIP(hipMemcpyAsync(d.ftab.p, ft.data(), T_ * sizeof(u32*), hipMemcpyHostToDevice, stream_));
-            SR_HIP(hipStreamSynchronize(stream_));
+            SR_HIP(stream_sync(stream_));
         }
         d.valid = true;
     }
@@ -1706,7 +1706,7 @@ class DistEngine final : public EngineBase {
                 std::string fl;
                 if (d.flags.p) {  // what this rank's flag words hold against the last sequence enqueued
                     std::vector<u32> f(T_);
-                    SR_HIP(hipStreamSynchronize(stream_));
+                    SR_HIP(stream_sync(stream_));
                     SR_HIP(hipMemcpy(f.data(), d.flags.p, T_ * 4, hipMemcpyDeviceToHost));
                     for (u32 q = 0; q < T_; ++q) fl += (q ? "," : "") + std::to_string(f[q]);
                 }
@@ -1773,7 +1773,7 @@ class DistEngine final : public EngineBase {
             stats.levels++;
             if (enq == level + 1) plan_enqueue(1);
         }
-        SR_HIP(hipStreamSynchronize(stream_));  // the speculative level enqueued past the end
+        SR_HIP(stream_sync(stream_));  // the speculative level enqueued past the end
     }
 
     void exchange(const std::vector<u64>& all, size_t RW) {
@@ -1858,7 +1858,7 @@ class DistEngine final : public EngineBase {
                 }
                 comm_->broadcast(buf.p, TREC, (int)owner, stream_);
                 SR_HIP(hipMemcpyAsync(rec, buf.p, TREC * 8, hipMemcpyDeviceToHost, stream_));
-                SR_HIP(hipStreamSynchronize(stream_));
+                SR_HIP(stream_sync(stream_));
             }
             rev.insert(rev.end(), rec, rec + W);
             if (rec[W] == NONE) break;
@@ -1871,7 +1871,7 @@ class DistEngine final : public EngineBase {
                 SR_HIP(hipGetLastError());
                 unsigned long long h = ~0ull;
                 SR_HIP(hipMemcpyAsync(&h, best.p, 8, hipMemcpyDeviceToHost, stream_));
-                SR_HIP(hipStreamSynchronize(stream_));
+                SR_HIP(stream_sync(stream_));
                 if (h == ~0ull) throw Error(SR_ERR_NONDETERMINISM, "Unable to reconstruct a `Path` into the replicated head");
                 in_head = true;
                 --level;
@@ -1895,16 +1895,16 @@ class DistEngine final : public EngineBase {
                         DBuf<unsigned long long> g;
                         g.alloc(o_.device, 1);
                         SR_HIP(hipMemcpyAsync(&h, best.p, 8, hipMemcpyDeviceToHost, stream_));
-                        SR_HIP(hipStreamSynchronize(stream_));
+                        SR_HIP(stream_sync(stream_));
                         unsigned long long lg = h == ~0ull ? ~0ull : (((u64)p.id << GID_SHIFT) | (lo + h));
                         SR_HIP(hipMemcpyAsync(g.p, &lg, 8, hipMemcpyHostToDevice, stream_));
                         comm_->all_reduce(reinterpret_cast<u64*>(g.p), 1, RedOp::Min, stream_);
                         SR_HIP(hipMemcpyAsync(&h, g.p, 8, hipMemcpyDeviceToHost, stream_));
-                        SR_HIP(hipStreamSynchronize(stream_));
+                        SR_HIP(stream_sync(stream_));
                         found = std::min<u64>(found, h);
                     } else {
                         SR_HIP(hipMemcpyAsync(&h, best.p, 8, hipMemcpyDeviceToHost, stream_));
-                        SR_HIP(hipStreamSynchronize(stream_));
+                        SR_HIP(stream_sync(stream_));
                         if (h != ~0ull) found = std::min<u64>(found, ((u64)p.id << GID_SHIFT) | (lo + h));
                     }
                 }

@@ -316,6 +316,7 @@ class Engine final : public EngineBase {
         if (const char* e = std::getenv("SR_PIPELINE")) pipeline_ = std::atoi(e) != 0;
         if (const char* e = std::getenv("SR_QUERY_LOG2")) query_mask_ = (1ull << std::atoi(e)) - 1;
         if (const char* e = std::getenv("SR_GRID_MAX")) grid_max_ = (u32)std::max(0, std::atoi(e));  // <= 0: unset
+        if (const char* e = std::getenv("SR_TABLE_RECYCLE")) table_recycle_ = std::atoi(e) != 0;
     }
     ~Engine() override = default;
 
@@ -356,7 +357,7 @@ class Engine final : public EngineBase {
                 if (o_.verbose) std::fprintf(stderr, "[sr] %s; restarting with larger buffers\n", e.what());
                 pessimistic_ = true;
                 grow_factor_ *= 4;
-                (void)hipStreamSynchronize(stream_);
+                (void)stream_sync(stream_);
                 init_counters();
             }
         }
@@ -478,8 +479,7 @@ class Engine final : public EngineBase {
     void alloc_table(u64 cap) {
         cap_ = cap;
         lmax_ = max_load(cap);
-        keys_.alloc(o_.device, cap);
-        SR_HIP(hipMemsetAsync(keys_.p, 0, cap * sizeof(u64), stream_));
+        keys_.alloc_zero(o_.device, cap, stream_);
         if (fifo_) {
             meta_.alloc(o_.device, cap);
             SR_HIP(hipMemsetAsync(meta_.p, 0xff, cap * sizeof(u64), stream_));
@@ -504,7 +504,7 @@ class Engine final : public EngineBase {
             SR_HIP(hipGetLastError());
             u32 err = 0;
             SR_HIP(hipMemcpyAsync(&err, aux_.p, sizeof(u32), hipMemcpyDeviceToHost, stream_));
-            SR_HIP(hipStreamSynchronize(stream_));
+            SR_HIP(stream_sync(stream_));
             if (!err) break;
             if (f >= 64) throw Error(SR_ERR_CAPACITY, "rehash: probe limit exceeded at 64x the capacity");
         }
@@ -512,7 +512,7 @@ class Engine final : public EngineBase {
             remap_slots<<<blocks_for(cand_n, 256), 256, 0, stream_>>>(cand, cand_n, from, view());
             SR_HIP(hipGetLastError());
         }
-        SR_HIP(hipStreamSynchronize(stream_));
+        SR_HIP(stream_sync(stream_));
         stats.rehashes++;
     }
 
@@ -537,7 +537,7 @@ class Engine final : public EngineBase {
         SR_HIP(hipGetLastError());
         u32 d = 0;
         SR_HIP(hipMemcpyAsync(&d, aux_.p + 1, sizeof(u32), hipMemcpyDeviceToHost, stream_));
-        SR_HIP(hipStreamSynchronize(stream_));
+        SR_HIP(stream_sync(stream_));
         stats.max_displacement = d;
     }
 
@@ -563,7 +563,7 @@ class Engine final : public EngineBase {
         arena_cap_ = cap;
         // the old buffers go back to the pool when na/np/ne leave scope: wait until no enqueued work
         // reads them (a first allocation has none, and the start of a check does not wait here)
-        if (had) SR_HIP(hipStreamSynchronize(stream_));
+        if (had) SR_HIP(stream_sync(stream_));
     }
 
     void bind(Ctx* c) {
@@ -654,7 +654,7 @@ class Engine final : public EngineBase {
         std::copy(first.disc, first.disc + MAX_PROPS, dmin);
         for (int attempt = 0;; ++attempt) {
             if (attempt >= 8) throw Error(SR_ERR_CAPACITY, "visited set probe limit exceeded after 8 doublings");
-            SR_HIP(hipStreamSynchronize(stream_));
+            SR_HIP(stream_sync(stream_));
             if (o_.verbose)
                 std::fprintf(stderr, "[sr] level of %llu states overflowed the probe limit %u at %llu slots: doubling\n",
                              (unsigned long long)n, view().plimit, (unsigned long long)cap_);
@@ -749,18 +749,33 @@ class Engine final : public EngineBase {
         ensure_arena(std::max<u64>(1u << 16, (o_.capacity_hint + slack + 1024) * grow_factor_), 0);
         lstart_.assign({0, (u64)k});
         lvisited_.clear();
-        SR_HIP(hipMemcpyAsync(arena_.p, rev.data(), rev.size() * sizeof(u64), hipMemcpyHostToDevice, stream_));
-        SR_HIP(hipMemsetAsync(apar_.p, 0xff, (size_t)k * sizeof(u32), stream_));
-        init_counters();
-        if (emask_) fill_u32<<<blocks_for(k, 64), 64, 0, stream_>>>(aeb_.p, (u32)k, emask_);  // bfs.rs:52-60
-        u32 sq = next_seq();
-        if (k <= 256) {
-            roots_fused<M><<<1, 256, 0, stream_>>>(m_, view(), arena_.p, (u32)k, lc_d_, ((1u << M::NPROPS) - 1) & ~emask_,
-                                                  hcd(sq), sq);
+        const u32 und0 = ((1u << M::NPROPS) - 1) & ~emask_;
+        u32 sq = 0;
+        if ((u64)k * W <= ROOTS_INLINE_WORDS) {
+            // one launch: counters reset, level 0 into the arena (no parents; `eventually` bits
+            // pending, bfs.rs:52-60), roots inserted and evaluated, published
+            InlineStates init{};
+            std::copy(rev.begin(), rev.end(), init.w);
+            if (!slots_.p) slots_.alloc(o_.device, (SLOTS * sizeof(LevelCounters) + 7) / 8);
+            slot_k_ = 0;
+            slot_published_ = true;
+            sq = next_seq();
+            roots_start<M><<<1, 256, 0, stream_>>>(m_, view(), init, (u32)k, arena_.p, apar_.p, emask_ ? aeb_.p : nullptr,
+                                                   emask_, lc_d_, reinterpret_cast<LevelCounters*>(slots_.p), SLOTS,
+                                                   und0, hcd(sq), sq);
         } else {
-            insert_roots<M><<<blocks_for(k, 64), 64, 0, stream_>>>(m_, view(), arena_.p, (u32)k, lc_d_);
-            eval_roots<M><<<blocks_for(k, 64), 64, 0, stream_>>>(m_, arena_.p, (u32)k, lc_d_, ((1u << M::NPROPS) - 1) & ~emask_);
-            publish_kernel<<<1, 64, 0, stream_>>>(lc_d_, hcd(sq), sq, 1, nullptr);
+            SR_HIP(hipMemcpyAsync(arena_.p, rev.data(), rev.size() * sizeof(u64), hipMemcpyHostToDevice, stream_));
+            SR_HIP(hipMemsetAsync(apar_.p, 0xff, (size_t)k * sizeof(u32), stream_));
+            init_counters();
+            if (emask_) fill_u32<<<blocks_for(k, 64), 64, 0, stream_>>>(aeb_.p, (u32)k, emask_);  // bfs.rs:52-60
+            sq = next_seq();
+            if (k <= 256) {
+                roots_fused<M><<<1, 256, 0, stream_>>>(m_, view(), arena_.p, (u32)k, lc_d_, und0, hcd(sq), sq);
+            } else {
+                insert_roots<M><<<blocks_for(k, 64), 64, 0, stream_>>>(m_, view(), arena_.p, (u32)k, lc_d_);
+                eval_roots<M><<<blocks_for(k, 64), 64, 0, stream_>>>(m_, arena_.p, (u32)k, lc_d_, und0);
+                publish_kernel<<<1, 64, 0, stream_>>>(lc_d_, hcd(sq), sq, 1, nullptr);
+            }
         }
         SR_HIP(hipGetLastError());
         // FAST pipelined order: level 0 is enqueued before the host reads the roots' outcome (it is
@@ -801,7 +816,7 @@ class Engine final : public EngineBase {
                                                                     emask_, tsat.p, evd.p);
                 SR_HIP(hipGetLastError());
                 SR_HIP(hipMemcpyAsync(evf.data(), evd.p, M::NPROPS * sizeof(u32), hipMemcpyDeviceToHost, stream_));
-                SR_HIP(hipStreamSynchronize(stream_));
+                SR_HIP(stream_sync(stream_));
             }
             u64 limit = n, visited = n;
             bool stop = false;
@@ -863,7 +878,7 @@ class Engine final : public EngineBase {
                                                                        evd.p, peb.p, evd.p + M::NPROPS);
                 SR_HIP(hipGetLastError());
                 SR_HIP(hipMemcpyAsync(evl.data(), evd.p + M::NPROPS, M::NPROPS * sizeof(u32), hipMemcpyDeviceToHost, stream_));
-                SR_HIP(hipStreamSynchronize(stream_));
+                SR_HIP(stream_sync(stream_));
             }
             if (limit) {
                 produced = expand_level(level, n, limit, undiscovered & ~emask_, peb.p);
@@ -908,6 +923,7 @@ class Engine final : public EngineBase {
         stats.level_loop_sec = secs(t_loop, t_end);
         stats.total_sec = secs(t_start, t_end);
         stats.table_capacity = cap_;
+        release_table();  // (the pipelined loop released it already)
         return order_dependent && !fifo_;
     }
 
@@ -940,7 +956,7 @@ class Engine final : public EngineBase {
         if (newly && undiscovered == 0) {
             lvisited_.push_back(max_rank + 1);
             reference_done = true;
-            SR_HIP(hipStreamSynchronize(stream_));  // the level-0 launch is not counted
+            drain();  // the level-0 launch is not counted
             return true;
         }
         // One level's outcome (counters c); false when the check is over.
@@ -1012,8 +1028,38 @@ class Engine final : public EngineBase {
             if (!account(lc_, spec_ok ? " (next enqueued)" : "")) break;
             sq = spec_ok ? sq_next : launch_sync(n, undiscovered);
         }
-        (void)hipStreamSynchronize(stream_);
+        // A speculative level past the end may still be in flight: the host waits for it, but the
+        // visited set's clear for the next check is enqueued behind it first (release_table), so
+        // that the clear runs while this check returns and the next one is set up.
+        SR_HIP(hipEventRecord(ctx_->done, stream_));
+        release_table();
+        drain(ctx_->done);
         return order_dependent;
+    }
+
+    // Until the stream has passed event `ev` (or every launch enqueued on it, ev = nullptr): a
+    // spin on the query. (A blocking hipStreamSynchronize returned ~30 us after a check's last
+    // kernel had ended.)
+    void drain(hipEvent_t ev = nullptr) {
+        if (!ev) {
+            SR_HIP(stream_sync(stream_));
+            return;
+        }
+        for (;;) {
+            const hipError_t e = hipEventQuery(ev);
+            if (e == hipSuccess) return clear_not_ready();
+            if (e != hipErrorNotReady) SR_HIP(e);
+            _mm_pause();
+        }
+    }
+
+    // Nothing reads the visited set after the search (paths, replay and the Explorer use the arena
+    // and the model): it goes back to the pool, zeroed on this stream behind the work enqueued so
+    // far (a full table write: ~34 us for 2pc N=9's 256 MiB), and the next check takes it without
+    // a clear at its start. Kept for the displacement scan of a counting run (sr_opts.counters),
+    // and in FIFO order. SR_TABLE_RECYCLE=0: an ordinary free, each check clears its own table.
+    void release_table() {
+        if (table_recycle_ && !fifo_ && !o_.counters) keys_.release_zero(stream_);
     }
 
     // Launch of the level whose frontier (n states) ends the arena, after the previous one is done:
@@ -1084,7 +1130,7 @@ class Engine final : public EngineBase {
         SR_HIP(hipGetLastError());
         std::vector<u32> h(n);
         SR_HIP(hipMemcpyAsync(h.data(), counts.p, n * sizeof(u32), hipMemcpyDeviceToHost, stream_));
-        SR_HIP(hipStreamSynchronize(stream_));
+        SR_HIP(stream_sync(stream_));
         u64 sc = state_count;
         u64 r = 0;
         for (u64 k = popped_before / 1500 + 1;; ++k) {
@@ -1240,7 +1286,8 @@ class Engine final : public EngineBase {
     int probe_batch_ = 1;
     int probe_load_ = 0;
     int ppw_env_ = -1;
-    u32 grid_max_ = 0;       // cap on expand_fast's grid, 0 = two device residencies (SR_GRID_MAX)
+    bool table_recycle_ = true;  // the visited set is returned zeroed (~Engine)
+    u32 grid_max_ = 0;      // cap on expand_fast's grid, 0 = two device residencies (SR_GRID_MAX)
     u64 query_mask_ = 4095;  // spins between hipStreamQuery calls in wait_publish (SR_QUERY_LOG2)
     bool pipeline_ = true;  // FAST-order level pipelining (SR_PIPELINE=0 disables, for A/B runs)
     DBuf<u64> slots_;                 // SLOTS per-level counter slots (the pipelined loop)

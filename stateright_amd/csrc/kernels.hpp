@@ -1218,7 +1218,7 @@ __global__ void __launch_bounds__(256) roots_fused(M m, TableView t, const u64* 
 
 // Device counters and the pipelined loop's counter slots to their level-start values (no host
 // buffer, so no host wait at the start of a check).
-__global__ void init_level_counters(LevelCounters* lc, LevelCounters* slots, u32 nslots) {
+__device__ __forceinline__ void init_counter_words(LevelCounters* lc, LevelCounters* slots, u32 nslots) {
     constexpr u32 WORDS = sizeof(LevelCounters) / 4;
     constexpr u32 D0 = offsetof(LevelCounters, disc) / 4;
     for (u32 i = threadIdx.x; i < WORDS * (1 + nslots); i += blockDim.x) {
@@ -1226,6 +1226,48 @@ __global__ void init_level_counters(LevelCounters* lc, LevelCounters* slots, u32
         u32* w = i < WORDS ? reinterpret_cast<u32*>(lc) + i : reinterpret_cast<u32*>(slots) + (i - WORDS);
         *w = o >= D0 && o < D0 + MAX_PROPS ? ~0u : 0u;
     }
+}
+__global__ void init_level_counters(LevelCounters* lc, LevelCounters* slots, u32 nslots) {
+    init_counter_words(lc, slots, nslots);
+}
+
+// The whole start of a check in ONE launch when the init states fit the kernel arguments (every
+// model here has a handful): the counters and counter slots reset (init_level_counters), level 0
+// written to the arena with no parents (and, for `eventually` models, every property pending),
+// then roots_fused. Replaces a host-to-device copy, two fills and two launches per check.
+constexpr u32 ROOTS_INLINE_WORDS = 32;
+struct InlineStates {
+    u64 w[ROOTS_INLINE_WORDS];
+};
+template <class M>
+__global__ void __launch_bounds__(256) roots_start(M m, TableView t, InlineStates init, u32 n, u64* arena, u32* apar,
+                                                   u32* aeb, u32 emask, LevelCounters* lc, LevelCounters* slots,
+                                                   u32 nslots, u32 undiscovered, HostCounters* h, u32 seq) {
+    constexpr int W = M::W;
+    init_counter_words(lc, slots, nslots);
+    for (u32 i = threadIdx.x; i < n * W; i += blockDim.x) arena[i] = init.w[i];
+    for (u32 i = threadIdx.x; i < n; i += blockDim.x) {
+        apar[i] = ~0u;
+        if (aeb) aeb[i] = emask;
+    }
+    __syncthreads();  // the counters are reset before any thread claims or counts into them
+    const u32 r = threadIdx.x;
+    if (r < n) {
+        u64 s[W];
+#pragma unroll
+        for (int i = 0; i < W; ++i) s[i] = init.w[r * W + i];
+        bool is_new;
+        const u64 slot = find_or_claim(t, probe_key(m, t, s), &is_new, &lc->err);
+        if (is_new) {
+            if (t.meta) t.meta[slot] = 0;  // level 0
+            atomicAdd(&lc->claims, 1u);
+        }
+        for (u32 und = undiscovered; und; und &= und - 1) {
+            const int p = __builtin_ctz(und);
+            if (m.discovers(p, s)) atomicMin(&lc->disc[p], r);
+        }
+    }
+    publish<M::NPROPS>(lc, h, seq, true, nullptr);
 }
 
 // Rehash into a larger table (keys and meta move together); an entry that does not fit the new
