@@ -57,6 +57,15 @@ UNIFORM_CAS_RATE = 26.7e9
 BIG_LEVEL_MS = 0.1  # levels whose expand launch takes >= 100 us count as "big"
 
 
+
+def _proc_start(pid):
+    """Start time of process `pid` in clock ticks since boot (/proc/<pid>/stat field 22), or 0."""
+    try:
+        with open(f"/proc/{pid}/stat") as f:
+            return int(f.read().rsplit(")", 1)[1].split()[19])
+    except (OSError, IndexError, ValueError):
+        return 0
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -70,6 +79,8 @@ def parse():
     ap.add_argument("--order", default="fast", choices=["fast", "fifo"])
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU restatement (rank 0, N=1)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="host threads for the CPU baseline (0 = usable CPUs)")
+    ap.add_argument("--no-hint-steps", type=int, default=10,
+                    help="checks timed WITHOUT capacity_hint (reported as `no_hint`; 0 = skip)")
     ap.add_argument("--config4-steps", type=int, default=3,
                     help="also time BASELINE configs[3] (2pc N=11, partitioned over the N GPUs; one GPU at N=1) "
                          "for this many checks after one warmup (0 = skip); reported as `config4`, not `value`")
@@ -322,9 +333,9 @@ def main():
         from stateright_amd.distributed import Communicator
         with stdout_to_stderr():
             if args.comm == "shm":
-                # every rank names the same segment (the launcher's port and pid); ranks share a GPU
-                # when the node has fewer GPUs than ranks
-                name = f"/sr_bench_{os.environ.get('MASTER_PORT', '0')}_{os.getppid()}"
+                # every rank names the same segment (the launcher's port, pid and start time: unique
+                # per launch); ranks share a GPU when the node has fewer GPUs than ranks
+                name = f"/sr_bench_{os.environ.get('MASTER_PORT', '0')}_{os.getppid()}_{_proc_start(os.getppid())}"
                 comm = Communicator.shm(rank, world, name, device=dev, slot_bytes=256 << 20,
                                         devices_distinct=ndev >= world)
             # under a launcher (RANK set) every rank bootstraps from its environment, also at N=1
@@ -332,8 +343,10 @@ def main():
                 comm = (Communicator.from_env(device=dev) if "RANK" in os.environ
                         else Communicator(0, 1, Communicator.unique_id(), dev))
 
-    def step(profile=False, counters=False):
-        b = make().checker().capacity_hint(expect_unique).device(dev)
+    def step(profile=False, counters=False, hint=True):
+        b = make().checker().device(dev)
+        if hint:  # the headline is pre-sized; `no_hint` times the path users get (no such option
+            b = b.capacity_hint(expect_unique)  # in the reference, src/checker.rs:35-51)
         if counters:
             b = b.counters()
         # the reference's join reconstructs no paths (discoveries() does, bfs.rs:289-298): the
@@ -411,6 +424,28 @@ def main():
     if world > 1:
         elapsed = comm.allreduce([elapsed], "max")[0]
     unique_total = float(unique) if partitioned or world == 1 else float(unique) * world
+
+    # The path users get: the same checks without capacity_hint (the visited set and the arena grow
+    # during the check, as the reference's DashMap does). Not `value`: reported beside it.
+    no_hint = None
+    if args.no_hint_steps > 0:
+        step(hint=False)  # warmup
+        barrier()
+        t2 = time.perf_counter()
+        c = None
+        for _ in range(args.no_hint_steps):
+            c = None
+            c = step(hint=False)
+        stn = c.stats()
+        c = None
+        barrier()
+        el_nh = time.perf_counter() - t2
+        if world > 1:
+            el_nh = comm.allreduce([el_nh], "max")[0]
+        nh_total = expect_unique * args.no_hint_steps * (1 if partitioned or world == 1 else world)
+        no_hint = {"steps": args.no_hint_steps, "ms_per_step": el_nh / args.no_hint_steps * 1e3,
+                   "value": nh_total / el_nh, "unit": "unique states/s",
+                   "rehashes": stn["rehashes"], "table_capacity": stn["table_capacity"], "restarts": stn["restarts"]}
 
     config4 = None
     if args.config4_steps > 0 and args.model == "2pc":
@@ -532,6 +567,9 @@ def main():
                                       "restarts", "pipelined", "records_routed", "head_levels")},
         "runtime": {"hip": versions["hip"], "rccl": versions["rccl"], "libs": N.loaded_runtime_paths()},
     }
+    if no_hint is not None:
+        no_hint["vs_value"] = no_hint["value"] / res["value"]
+        res["no_hint"] = no_hint
     if config4 is not None:
         res["config4"] = config4
     if replicas is not None:

@@ -108,7 +108,7 @@ typedef struct sr_opts {
 } sr_opts;
 
 /* Timing/throughput counters of a finished run (sr_gpu_bfs_stats / sr_gpu_bfs_stats_sized).
- * Layout of SR_PLUGIN_ABI 3 (the ABI-2 fields bucketed_levels and multi_levels are retired). */
+ * Layout of SR_PLUGIN_ABI 4 (ABI 3 plus exchange_fallbacks and owner_key). */
 typedef struct sr_stats {
     double level_loop_sec;       /* first expand launch .. last level synchronised              */
     double total_sec;            /* spawn .. done, excluding one-time device allocation          */
@@ -136,6 +136,11 @@ typedef struct sr_stats {
                                     2^dbits - 2; fingerprint mode: 65536)                          */
     uint32_t table_doublings;    /* quotient mode: in-check doublings after a level overflowed the
                                     probe limit (the level is finished on the larger table)       */
+    uint32_t exchange_fallbacks; /* partitioned search: checks redone on the collective exchange after
+                                    the direct exchange failed its per-slot sequence tag / checksum
+                                    or a peer's flag timed out (the result is then still exact)    */
+    uint32_t owner_key;          /* partitioned search: 1 = states are owned by the model's owner key
+                                    (a projection most actions keep), 0 = by fingerprint          */
 } sr_stats;
 
 typedef struct sr_bfs sr_bfs;
@@ -288,7 +293,7 @@ sr_bfs* sr_gpu_bfs_spawn_partitioned(sr_dist* comm, int32_t virtual_partitions, 
  * include/stateright_gpu_model.hpp; the macro SR_GPU_PLUGIN(name, Model, make) there exports
  * `const sr_plugin* sr_plugin_<name>(void)`. The engine library then runs it like a registered
  * model. The plugin must be built from the same headers (abi). */
-#define SR_PLUGIN_ABI 3
+#define SR_PLUGIN_ABI 4
 typedef struct sr_plugin {
     uint32_t abi;         /* SR_PLUGIN_ABI of the headers the plugin was built with */
     uint32_t opts_size;   /* sizeof(sr_opts) in that build */

@@ -63,6 +63,8 @@ class sr_stats(ctypes.Structure):
         ("max_displacement", ctypes.c_uint64),
         ("displacement_limit", ctypes.c_uint32),
         ("table_doublings", ctypes.c_uint32),
+        ("exchange_fallbacks", ctypes.c_uint32),
+        ("owner_key", ctypes.c_uint32),
     ]
 
     def as_dict(self):

@@ -11,6 +11,7 @@
 #include <mutex>
 #include <stdexcept>
 #include <string>
+#include <tuple>
 #include <vector>
 
 namespace sr {
@@ -51,6 +52,41 @@ inline hipError_t stream_sync(hipStream_t s) {
     }
 }
 
+// Streams this library created per device (the pooled contexts' streams, never destroyed), and the
+// hardware queues the HIP runtime gives this process per device (GPU_MAX_HW_QUEUES, read by the
+// runtime at its initialisation; HIP's default is 4). The runtime gives each stream a queue of its
+// own while there are enough, and makes later streams SHARE queues: a kernel that spins on the
+// device (the direct exchange's wait) can then sit in front of the kernel it waits for.
+struct StreamCensus {
+    static StreamCensus& get() {
+        static StreamCensus c;
+        return c;
+    }
+    void created(int dev) {
+        std::lock_guard<std::mutex> g(mu_);
+        ++n_[dev];
+    }
+    void destroyed(int dev) {
+        std::lock_guard<std::mutex> g(mu_);
+        --n_[dev];
+    }
+    int on(int dev) {
+        std::lock_guard<std::mutex> g(mu_);
+        return n_[dev];
+    }
+    static int hw_queues() {
+        const char* e = std::getenv("GPU_MAX_HW_QUEUES");
+        return e && std::atoi(e) > 0 ? std::atoi(e) : 4;
+    }
+    std::mutex mu_;
+    std::map<int, int> n_;
+};
+inline hipError_t create_stream(hipStream_t* s, int dev) {
+    const hipError_t e = hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+    if (e == hipSuccess) StreamCensus::get().created(dev);
+    return e;
+}
+
 // Process-wide caching allocator: freed blocks go to a per-(device, size) free list. Sizes are
 // rounded up to 2 MiB (or a power of two below that) so that a run with a slightly different
 // frontier reuses the same blocks.
@@ -60,30 +96,39 @@ class DevicePool {
         static DevicePool p;
         return p;
     }
-    void* alloc(int dev, size_t bytes) {
+    // kind 0: ordinary (coarse-grained) device memory; kind 1: fine-grained device memory
+    // (hipDeviceMallocFinegrained), which a system-scope acquire makes coherent with stores that
+    // ANOTHER device issued over xGMI while a kernel runs (the direct exchange's flags and receive
+    // buffers: its owner's L2 must not serve a line it cached before a peer's store).
+    void* alloc(int dev, size_t bytes, int kind = 0) {
         bytes = round(bytes);
         {
             std::lock_guard<std::mutex> g(mu_);
-            auto& fl = free_[{dev, bytes}];
+            auto& fl = free_[{dev, bytes, kind}];
             if (!fl.empty()) {
                 void* p = fl.back();
                 fl.pop_back();
                 return p;
             }
+            if (kind == 0)
+                if (void* p = take_zeroed_locked(dev, bytes)) return p;
         }
         void* p = nullptr;
-        hipError_t e = hipMalloc(&p, bytes);
+        auto raw = [&]() {
+            return kind == 1 ? hipExtMallocWithFlags(&p, bytes, hipDeviceMallocFinegrained) : hipMalloc(&p, bytes);
+        };
+        hipError_t e = raw();
         if (e != hipSuccess) {
             release_all(dev);  // retry once with the cache emptied
             (void)hipGetLastError();
-            SR_HIP(hipMalloc(&p, bytes));
+            SR_HIP(raw());
         }
         return p;
     }
-    void free(int dev, void* p, size_t bytes) {
+    void free(int dev, void* p, size_t bytes, int kind = 0) {
         if (!p) return;
         std::lock_guard<std::mutex> g(mu_);
-        free_[{dev, round(bytes)}].push_back(p);
+        free_[{dev, round(bytes), kind}].push_back(p);
     }
     // Blocks handed back while the work that zeroes them is still in flight: `ready` is recorded
     // behind that work. A check returns its visited set this way as soon as its last level is
@@ -124,7 +169,7 @@ class DevicePool {
         std::lock_guard<std::mutex> g(mu_);
         ++epoch_[dev];  // blocks may come back at the same addresses: peers' IPC mappings are stale
         for (auto& [k, v] : free_)
-            if (k.first == dev) {
+            if (std::get<0>(k) == dev) {
                 for (void* p : v) (void)hipFree(p);
                 v.clear();
             }
@@ -157,8 +202,28 @@ class DevicePool {
         void* p;
         hipEvent_t ready;
     };
+    // An ordinary allocation may take a pooled zeroed block of its size class whose clear has
+    // finished (the clear is then simply wasted): a table size that no later check asks for again
+    // would otherwise hold its memory until an out-of-memory retry flushes the whole pool. A block
+    // whose clear is still in flight is left for the check it was released for (alloc() has no
+    // stream to order after it).
+    void* take_zeroed_locked(int dev, size_t bytes) {
+        auto it = zeroed_.find({dev, bytes});
+        if (it == zeroed_.end()) return nullptr;
+        auto& fl = it->second;
+        for (size_t i = 0; i < fl.size(); ++i) {
+            if (hipEventQuery(fl[i].ready) != hipSuccess) continue;
+            Zeroed z = fl[i];
+            fl.erase(fl.begin() + (long)i);
+            (void)hipEventDestroy(z.ready);
+            clear_not_ready();
+            return z.p;
+        }
+        clear_not_ready();
+        return nullptr;
+    }
     std::mutex mu_;
-    std::map<std::pair<int, size_t>, std::vector<void*>> free_;
+    std::map<std::tuple<int, size_t, int>, std::vector<void*>> free_;
     std::map<std::pair<int, size_t>, std::vector<Zeroed>> zeroed_;
     std::map<int, uint64_t> epoch_;
 };
@@ -169,21 +234,24 @@ struct DBuf {
     T* p = nullptr;
     size_t n = 0;
     int dev = 0;
+    int kind = 0;  // DevicePool memory kind (1: fine-grained)
     DBuf() = default;
     DBuf(const DBuf&) = delete;
     DBuf& operator=(const DBuf&) = delete;
     DBuf(DBuf&& o) noexcept { swap(o); }
     ~DBuf() { reset(); }
     void reset() {
-        if (p) DevicePool::get().free(dev, p, n * sizeof(T));
+        if (p) DevicePool::get().free(dev, p, n * sizeof(T), kind);
         p = nullptr;
         n = 0;
+        kind = 0;
     }
-    void alloc(int d, size_t count) {
+    void alloc(int d, size_t count, int k = 0) {
         reset();
         dev = d;
         n = count ? count : 1;
-        p = static_cast<T*>(DevicePool::get().alloc(d, n * sizeof(T)));
+        kind = k;
+        p = static_cast<T*>(DevicePool::get().alloc(d, n * sizeof(T), k));
     }
     // All-zero bytes, ordered before the work enqueued on `s` afterwards: a pooled zeroed block,
     // or a fresh one cleared on `s`.
@@ -218,6 +286,7 @@ struct DBuf {
         std::swap(p, o.p);
         std::swap(n, o.n);
         std::swap(dev, o.dev);
+        std::swap(kind, o.kind);
     }
 };
 
@@ -238,7 +307,7 @@ struct DeviceContext {
     void init(int d) {
         dev = d;
         SR_HIP(hipSetDevice(d));
-        SR_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+        SR_HIP(create_stream(&stream, d));
         SR_HIP(hipEventCreateWithFlags(&done, hipEventDisableTiming));
         SR_HIP(hipMalloc(&lc, sizeof(Counters)));
         // two mirrors: launch `seq` publishes to slot seq & 1, so a launch may run while the host

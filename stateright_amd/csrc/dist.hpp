@@ -33,6 +33,7 @@
 #include <rccl/rccl.h>
 #include <sched.h>
 #include <sys/mman.h>
+#include <sys/stat.h>
 #include <unistd.h>
 
 #include <condition_variable>
@@ -72,6 +73,10 @@ __global__ void reduce_rows(const u64* in, u32 rows, u64 n, u32 op, u64* out) {
 //   broadcast    count words of root's buf to every rank's buf
 //   all_reduce   element-wise min / max / sum of count u64 words
 enum class RedOp { Min, Max, Sum };
+
+// Internal error code (never returned through the C ABI): the direct exchange failed its check on
+// this rank (ERR_EXCHANGE or ERR_PEER_TIMEOUT); DistEngine::run turns it into a fallback.
+constexpr int ERR_CODE_EXCHANGE = -101;
 
 // A device buffer as another rank can name it (direct exchange): its address in the exporting
 // process, the hipMalloc allocation around it, and an IPC handle of that allocation.
@@ -150,6 +155,80 @@ inline u64 peer_timeout_ticks() {
     return ms * 100000ull;
 }
 
+// Flag words of the direct exchange cleared with system-scope stores and a system-scope release: no
+// dirty line of them stays in this device's L2 to be written back over a peer's later flag store.
+__global__ void flags_clear(u32* f, u32 n) {
+    for (u32 i = threadIdx.x; i < n; i += blockDim.x) __hip_atomic_store(&f[i], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+}
+
+// The probe's data pattern: word i of the slot that rank `src` stores into rank `dst`'s buffer.
+__device__ __host__ __forceinline__ u64 probe_word(u32 src, u32 dst, u64 i, u32 seq) {
+    return fmix64(((u64)(src + 1) << 48) ^ ((u64)(dst + 1) << 40) ^ ((u64)seq << 32) ^ i) | 1;
+}
+// Every word of `buf` set to `v` and read back (the owner's L2 then holds the lines, as it holds
+// those of a receive buffer it read two levels earlier); `sink` keeps the reads.
+// The stores are written back (system-scope release) before the reads: a dirty line of the owner
+// could otherwise be evicted over a peer's later store.
+__global__ void probe_warm(u64* buf, u64 n, u64 v, u64* sink) {
+    u64 acc = 0;
+    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) buf[i] = v;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    __syncthreads();
+    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) acc += buf[i];
+    if (acc == 0x5bd1e995ull) sink[0] = acc;
+}
+// One workgroup of rank `me` stores its pattern into slot `me` of every rank's buffer (btab[q]),
+// then releases at system scope and raises its flag in every rank's flags (expand_route's order).
+__global__ void probe_store(u64* const* btab, u32* const* ftab, u32 world, u64 K, u32 me, u32 seq) {
+    for (u32 q = 0; q < world; ++q)
+        for (u64 i = threadIdx.x; i < K; i += blockDim.x) btab[q][i] = probe_word(me, q, i, seq);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    __syncthreads();
+    for (u32 q = threadIdx.x; q < world; q += blockDim.x)
+        __hip_atomic_store(ftab[q], seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// The owner waits for every flag inside the kernel that reads (insert_recv_lag's fused wait: poll,
+// system-scope acquire, then plain loads), bounded, and counts the words that differ.
+__global__ void probe_verify(const u64* buf, const u32* flags, u32 world, u64 K, u32 me, u32 seq, u64 timeout,
+                             unsigned long long* bad, LevelCounters* lc) {
+    __shared__ u32 ok;
+    if (threadIdx.x == 0) {
+        ok = 1;
+        const u64 t0 = __builtin_amdgcn_s_memrealtime();
+        for (u32 q = 0; q < world; ++q)
+            while ((int)(__hip_atomic_load(&flags[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - seq) < 0) {
+                if (__builtin_amdgcn_s_memrealtime() - t0 > timeout) {
+                    ok = 0;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+        if (!ok) atomicOr(&lc->err, (u32)ERR_PEER_TIMEOUT);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    }
+    __syncthreads();
+    if (!ok) return;
+    u64 nbad = 0;
+    for (u32 q = 0; q < world; ++q)
+        for (u64 i = threadIdx.x; i < K; i += blockDim.x) nbad += buf[(u64)q * K + i] != probe_word(q, me, i, seq);
+    if (nbad) atomicAdd(bad, (unsigned long long)nbad);
+}
+
+// Checked once per communicator (collective, on first use), in the exchange's steady state: every
+// rank fills and READS its own receive area first (its lines are then cached, as a receive buffer
+// read two levels earlier is), then every rank stores a pattern into its slot of every rank's area
+// and raises its flag there, and every owner waits for the flags inside the reading kernel and
+// checks every word. Same memory kind as the exchange (dx_kind), 1 s bound. Every rank reaches every
+// collective whatever failed on it, and all take the same decision.
+inline int dx_probe_kind() {
+    const char* e = std::getenv("SR_DX_FINE");
+    return e && std::atoi(e) == 0 ? 0 : 1;
+}
 inline bool Comm::probe_direct(hipStream_t s) {
     if (direct_ok >= 0) return direct_ok == 1;
     // Every rank reaches every collective below, whatever failed on it: a local failure becomes
@@ -165,45 +244,69 @@ inline bool Comm::probe_direct(hipStream_t s) {
     };
     direct_ok = 0;
     if (!agree(peer_capable() ? 1 : 0)) return false;
+    constexpr u64 K = 8192;  // words per slot (64 KiB)
+    constexpr u32 SEQ = 7;
+    const int kind = dx_probe_kind();
     DBuf<u32> flags;
-    flags.alloc(device, world);
+    flags.alloc(device, world, kind);
+    DBuf<u64> area;
+    area.alloc(device, (u64)world * K, kind);
     DBuf<u32*> ftab;
     ftab.alloc(device, world);
-    DBuf<u64> lcbuf;  // a LevelCounters for the wait's error bit
-    lcbuf.alloc(device, (sizeof(LevelCounters) + 7) / 8);
-    SR_HIP(hipMemsetAsync(flags.p, 0, world * 4, s));
-    SR_HIP(hipMemsetAsync(lcbuf.p, 0, sizeof(LevelCounters), s));
+    DBuf<u64*> btab;
+    btab.alloc(device, world);
+    DBuf<u64> lcbuf;  // a LevelCounters for the wait's error bit, then the mismatch count
+    lcbuf.alloc(device, (sizeof(LevelCounters) + 7) / 8 + 2);
+    auto* lc = reinterpret_cast<LevelCounters*>(lcbuf.p);
+    auto* bad = reinterpret_cast<unsigned long long*>(lcbuf.p + (sizeof(LevelCounters) + 7) / 8);
+    flags_clear<<<1, 64, 0, s>>>(flags.p, (u32)world);
+    SR_HIP(hipMemsetAsync(lcbuf.p, 0, lcbuf.n * 8, s));
+    probe_warm<<<64, 256, 0, s>>>(area.p, (u64)world * K, 0xa5a5a5a5a5a5a5a5ull, reinterpret_cast<u64*>(bad + 1));
+    SR_HIP(hipGetLastError());
     SR_HIP(stream_sync(s));
     u64 ok = 1;
-    PeerBlob b;
+    PeerBlob b[2];
     try {
-        b = export_buf(flags.p);
+        b[0] = export_buf(flags.p);
+        b[1] = export_buf(area.p);
     } catch (const Error&) {
         ok = 0;
-        b = PeerBlob{};
+        b[0] = b[1] = PeerBlob{};
     }
-    std::vector<PeerBlob> all(world);
-    share(&b, sizeof(b), all.data(), s);  // collective: every rank's flags are zero from here on
+    std::vector<PeerBlob> all(2 * (size_t)world);
+    share(b, sizeof(b), all.data(), s);  // collective: every rank's area is warm and its flags zero from here on
     std::vector<u32*> ft(world);
+    std::vector<u64*> bt(world);
     for (int q = 0; q < world && ok; ++q) {
-        if (!all[q].ptr) ok = 0;  // that rank could not export
+        if (!all[2 * q].ptr || !all[2 * q + 1].ptr) ok = 0;  // that rank could not export
         try {
-            if (ok) ft[q] = (q == rank ? flags.p : reinterpret_cast<u32*>(map(q, all[q]))) + rank;
+            if (ok) {
+                ft[q] = (q == rank ? flags.p : reinterpret_cast<u32*>(map(q, all[2 * q]))) + rank;
+                bt[q] = (q == rank ? area.p : map(q, all[2 * q + 1])) + (u64)rank * K;
+            }
         } catch (const Error&) {
             ok = 0;
         }
     }
     if (!agree(ok)) return false;
     SR_HIP(hipMemcpyAsync(ftab.p, ft.data(), world * sizeof(u32*), hipMemcpyHostToDevice, s));
-    peer_signal<<<1, 64, 0, s>>>(ftab.p, (u32)world, 7u);
-    auto* lc = reinterpret_cast<LevelCounters*>(lcbuf.p);
-    peer_wait<<<1, 64, 0, s>>>(flags.p, (u32)world, 7u, lc, 100000000ull);  // 1 s
+    SR_HIP(hipMemcpyAsync(btab.p, bt.data(), world * sizeof(u64*), hipMemcpyHostToDevice, s));
+    probe_store<<<1, 256, 0, s>>>(btab.p, ftab.p, (u32)world, K, (u32)rank, SEQ);
+    probe_verify<<<1, 256, 0, s>>>(area.p, flags.p, (u32)world, K, (u32)rank, SEQ, 100000000ull, bad, lc);  // 1 s
     SR_HIP(hipGetLastError());
     u32 err = 0;
+    unsigned long long nbad = 0;
     SR_HIP(hipMemcpyAsync(&err, &lc->err, 4, hipMemcpyDeviceToHost, s));
+    SR_HIP(hipMemcpyAsync(&nbad, bad, 8, hipMemcpyDeviceToHost, s));
     SR_HIP(stream_sync(s));
-    if (err) flags.p = nullptr;  // a late peer store may still land: never reuse the block
-    direct_ok = agree(err == 0 ? 1 : 0) ? 1 : 0;
+    if (err || nbad) {
+        // a late peer store may still land: never reuse these blocks
+        flags.p = nullptr;
+        area.p = nullptr;
+        std::fprintf(stderr, "[sr] direct exchange probe failed on rank %d (%s, %llu wrong words): collective exchange\n",
+                     rank, err ? "a flag did not arrive" : "stale or lost data", nbad);
+    }
+    direct_ok = agree(err == 0 && nbad == 0 ? 1 : 0) ? 1 : 0;
     return direct_ok == 1;
 }
 
@@ -462,7 +565,17 @@ struct LocalComm final : Comm {
     // Direct exchange between threads of one process: raw device pointers (peer access enabled
     // when the ranks sit on different devices). share() first finishes this rank's stream, so a
     // rank that shares a buffer it just cleared has cleared it before any peer can write to it.
-    bool peer_capable() const override { return direct_env_on(); }
+    // Ranks that share a device wait for each other's flags on that device: each rank's stream
+    // needs a hardware queue of its own, or a rank's wait may be queued in front of the expand it
+    // waits for. Unless every stream this library created on the device (plus the runtime's own)
+    // has one, the ranks take the collective exchange.
+    bool peer_capable() const override {
+        if (!direct_env_on()) return false;
+        int same = 0;
+        for (int d : g->devices) same += d == device;
+        if (same <= 1) return true;
+        return StreamCensus::get().on(device) + 1 <= StreamCensus::hw_queues();
+    }
     bool distinct_devices() const override {
         std::set<int> d(g->devices.begin(), g->devices.end());
         return (int)d.size() == world;
@@ -508,7 +621,9 @@ struct ShmComm final : Comm {
         std::atomic<u64> arrived;
         std::atomic<u64> generation;
         std::atomic<u32> failed;
+        std::atomic<u32> ready;  // READY once rank 0 has initialised this segment
     };
+    static constexpr u32 READY = 0x53524844u;
     static constexpr size_t HDR = 4096;
     std::string name;
     size_t slot_bytes = 0;
@@ -526,16 +641,49 @@ struct ShmComm final : Comm {
         slot_bytes = slot;
         devices_distinct = distinct;
         bytes = HDR + slot_bytes * (size_t)w;
-        const int fd = shm_open(name.c_str(), O_CREAT | O_RDWR, 0600);
-        if (fd < 0) throw Error(SR_ERR_ARG, "shm_open(" + name + ") failed");
-        if (ftruncate(fd, (off_t)bytes) != 0) {
-            ::close(fd);
-            throw Error(SR_ERR_ARG, "ftruncate of the shared segment failed");
+        // Rank 0 removes a segment a crashed run may have left under this name and creates a fresh
+        // one exclusively, with a zeroed header, marked READY last; the other ranks open it (no
+        // create) once it exists at full size, and wait for READY. A stale segment's barrier state
+        // therefore never reaches a new run through rank 0; callers still name segments per run.
+        int fd = -1;
+        const auto t0 = Clock::now();
+        if (rank == 0) {
+            (void)shm_unlink(name.c_str());
+            fd = shm_open(name.c_str(), O_CREAT | O_EXCL | O_RDWR, 0600);
+            if (fd < 0) throw Error(SR_ERR_ARG, "shm_open(" + name + ", O_EXCL) failed");
+            if (ftruncate(fd, (off_t)bytes) != 0) {
+                ::close(fd);
+                throw Error(SR_ERR_ARG, "ftruncate of the shared segment failed");
+            }
+        } else {
+            for (;;) {
+                fd = shm_open(name.c_str(), O_RDWR, 0600);
+                if (fd >= 0) {
+                    struct stat st;
+                    if (fstat(fd, &st) == 0 && (size_t)st.st_size >= bytes) break;
+                    ::close(fd);
+                    fd = -1;
+                }
+                if (secs(t0, Clock::now()) > timeout_s) throw Error(SR_ERR_ARG, "shm transport: rank 0 never created " + name);
+                usleep(1000);
+            }
         }
         void* m = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
         ::close(fd);
         if (m == MAP_FAILED) throw Error(SR_ERR_ARG, "mmap of the shared segment failed");
         base = static_cast<char*>(m);
+        Header* h = hdr();
+        if (rank == 0) {
+            h->arrived.store(0);
+            h->generation.store(0);
+            h->failed.store(0);
+            h->ready.store(READY, std::memory_order_release);
+        } else {
+            while (h->ready.load(std::memory_order_acquire) != READY) {
+                if (secs(t0, Clock::now()) > timeout_s) throw Error(SR_ERR_ARG, "shm transport: " + name + " never became ready");
+                usleep(100);
+            }
+        }
     }
     ~ShmComm() override {
         ipc.close();
@@ -675,6 +823,7 @@ struct DistContext {
         DBuf<u64> drecv[2];
         u64 drecv_words = 0;
         DBuf<u64*> ptab[2];
+        DBuf<u64> dsum;  // [NSHARD][MAX_PARTS] record-word sums per owner (exchange check)
     };
     // Direct exchange state kept across the checks of one communicator (or one set of virtual
     // partitions): the flag words of this rank, the table of its word in every owner's flags, and
@@ -703,7 +852,7 @@ struct DistContext {
     void init(int d) {
         dev = d;
         SR_HIP(hipSetDevice(d));
-        SR_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+        SR_HIP(create_stream(&stream, d));
         SR_HIP(hipHostMalloc(&hrows, (ROW_WORDS + 8) * 8, hipHostMallocCoherent | hipHostMallocMapped));
         SR_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&hrows_dev), hrows, 0));
         std::memset(hrows, 0, (ROW_WORDS + 8) * 8);
@@ -837,32 +986,91 @@ class DistEngine final : public EngineBase {
             }
         }
         for (int attempt = 0;; ++attempt) {
+            // With the direct exchange every rank votes on the outcome of the check (one small
+            // collective over the communicator's own transport): an exchange that delivered a
+            // stale or partial slot is seen by its owner only (ERR_EXCHANGE, ERR_PEER_TIMEOUT), and
+            // its rows may not reach the others. Same decision on every rank: `vote` depends only
+            // on collectively agreed state.
+            const bool vote = comm_ && lag_ && direct_env_on() && comm_->direct_ok != 0;
+            int code = 0;  // 0 ok, 1 capacity restart, 2 exchange failure, 3 other error
+            std::string what;
+            int ecode = 0;
             try {
                 run_once();
+            } catch (const Error& e) {
+                code = e.code == SR_ERR_CAPACITY ? 1 : e.code == ERR_CODE_EXCHANGE ? 2 : 3;
+                what = e.what();
+                ecode = e.code;
+                if (!vote) {
+                    if (code == 2 && !comm_ && attempt < 3) {  // virtual partitions: no collective to agree on
+                        exchange_fallback(what);
+                        continue;
+                    }
+                    if (code == 2) throw Error(SR_ERR_HIP, what);
+                    if (code != 1 || attempt >= 3) throw;
+                }
+            }
+            if (vote) {
+                SR_HIP(stream_sync(stream_));  // in-flight levels end (a wait for a stopped peer times out)
+                u64 v[2] = {(u64)code, ~(u64)code};  // max and min of the ranks' outcomes
+                DBuf<u64> dv;
+                dv.alloc(o_.device, 2);
+                SR_HIP(hipMemcpyAsync(dv.p, v, sizeof(v), hipMemcpyHostToDevice, stream_));
+                comm_->all_reduce(dv.p, 2, RedOp::Max, stream_);
+                SR_HIP(hipMemcpyAsync(v, dv.p, sizeof(v), hipMemcpyDeviceToHost, stream_));
+                SR_HIP(stream_sync(stream_));
+                const int hi = (int)v[0], lo = (int)~v[1];
+                if (hi == 3) {
+                    if (code == 3) throw Error(ecode, what);
+                    throw Error(SR_ERR_HIP, "partitioned search: another rank failed");
+                }
+                if (hi == 2 || hi != lo) {  // a corrupt exchange somewhere, or ranks that disagree
+                    if (attempt >= 3) throw Error(SR_ERR_HIP, "partitioned search: the exchange failed repeatedly: " + what);
+                    exchange_fallback(code == 2 ? what : std::string("another rank's exchange failed"));
+                    continue;
+                }
+                if (hi == 0) {
+                    gather_paths();
+                    return;
+                }
+                if (attempt >= 3) throw Error(ecode, what);
+            } else if (code == 0) {
                 gather_paths();
                 return;
-            } catch (const Error& e) {
-                if (e.code != SR_ERR_CAPACITY || attempt >= 3) throw;
-                SR_HIP(stream_sync(stream_));
-                stats.restarts++;
-                restarts_++;
-                if (head_failed_) {  // the head's scratch buffers were too small: no head
-                    head_ok_ = false;
-                    head_failed_ = false;
-                    continue;
-                }
-                if (lag_) {
-                    // the pipelined plan under-estimated a level: rerun with one host
-                    // synchronisation per level (exact bucket sizes)
-                    if (o_.verbose) std::fprintf(stderr, "[sr] %s; restarting in synchronous mode\n", e.what());
-                    lag_ = false;
-                    continue;
-                }
-                if (o_.verbose) std::fprintf(stderr, "[sr] %s; restarting with larger buffers\n", e.what());
-                pessimistic_ = true;
-                grow_factor_ *= 4;
             }
+            // capacity: every rank saw it at the same level (the rows are the same everywhere)
+            SR_HIP(stream_sync(stream_));
+            stats.restarts++;
+            restarts_++;
+            if (head_failed_) {  // the head's scratch buffers were too small: no head
+                head_ok_ = false;
+                head_failed_ = false;
+                continue;
+            }
+            if (lag_) {
+                // the pipelined plan under-estimated a level: rerun with one host
+                // synchronisation per level (exact bucket sizes)
+                if (o_.verbose) std::fprintf(stderr, "[sr] %s; restarting in synchronous mode\n", what.c_str());
+                lag_ = false;
+                continue;
+            }
+            if (o_.verbose) std::fprintf(stderr, "[sr] %s; restarting with larger buffers\n", what.c_str());
+            pessimistic_ = true;
+            grow_factor_ *= 4;
         }
+    }
+
+    // The direct exchange failed its check (a slot's sequence tag or checksum, or a source that
+    // never raised its flag): the check is redone on the collective exchange, which this
+    // communicator (or these virtual partitions) keeps from now on.
+    void exchange_fallback(const std::string& why) {
+        SR_HIP(stream_sync(stream_));
+        if (comm_) comm_->direct_ok = 0;
+        direct_off_ = true;
+        ctx_->dx.valid = false;  // never reused: a late peer store may still land in it
+        exchange_fallbacks_++;
+        std::fprintf(stderr, "[sr] direct exchange failed (%s); redoing the check with the collective exchange\n",
+                     why.c_str());
     }
 
     // Every discovery path, gathered on every rank at the end of the run (one collective walk per
@@ -1023,6 +1231,8 @@ class DistEngine final : public EngineBase {
         stats.words_per_state = W;
         stats.order_used = SR_ORDER_FAST;
         stats.restarts = restarts_;
+        stats.exchange_fallbacks = exchange_fallbacks_;
+        stats.owner_key = okey_ ? 1u : 0u;
         stats.pipelined = lag_ ? 1u : 0u;
         const u64 hint = o_.capacity_hint ? o_.capacity_hint : (u64)1 << 22;
         gl_lstart_.assign(T_, {});
@@ -1146,7 +1356,7 @@ class DistEngine final : public EngineBase {
                 route<<<grid, 256, route_lds(), stream_>>>(
                     m_, p.arena.p, p.apar.p, nb, p.arena_cap, p.view(), p.id, T_, p.send.p, (u32)p.bucket_cap,
                     p.sendc.p, p.lc, p.ctl, undiscovered, row, ppw_log2, filt_log2_, p.bucket_cap * REC, 0u,
-                    p.sent_mask ? p.sent.p : nullptr, p.sent_mask, rstage_recs(), nullptr, nullptr, 0u, self_rec());
+                    p.sent_mask ? p.sent.p : nullptr, p.sent_mask, rstage_recs(), nullptr, nullptr, 0u, rflags(), nullptr);
                 SR_HIP(hipGetLastError());
                 if (o_.profile) SR_HIP(hipEventRecord(event(2 * stats.expand_launches + 1), stream_));
                 stats.expand_launches++;
@@ -1452,7 +1662,7 @@ class DistEngine final : public EngineBase {
                 m_, p.arena.p, p.apar.p, 0, p.arena_cap, p.view(), p.id, T_, direct_ ? nullptr : p.send.p + DIST_HDR,
                 (u32)C, p.sendc.p, p.lc, p.ctl, undiscovered, row, ppw_log2, filt_log2_, S, 1u,
                 p.sent_mask ? p.sent.p : nullptr, p.sent_mask, rstage_recs(), direct_ ? ctx_->parts[p.res].ptab[par].p : nullptr,
-                dflags_ ? ctx_->dx.ftab.p : nullptr, fseq, self_rec());
+                dflags_ ? ctx_->dx.ftab.p : nullptr, fseq, rflags(), dcheck() ? ctx_->parts[p.res].dsum.p : nullptr);
             SR_HIP(hipGetLastError());
             if (o_.profile) SR_HIP(hipEventRecord(event(2 * stats.expand_launches + 1), stream_));
             stats.expand_launches++;
@@ -1460,8 +1670,14 @@ class DistEngine final : public EngineBase {
         if (direct_) {
             // the records are in the owners' buffers already; ranks on their own streams wait for
             // every source's flag (virtual partitions share this stream: the routes ran before)
-            if (dflags_ && !fused_wait_) {
+            const bool corrupt = corrupt_level_ == (i64)level && (!comm_ || comm_->rank == 0);
+            if (dflags_ && (!fused_wait_ || corrupt)) {
                 peer_wait<<<1, 64, 0, stream_>>>(ctx_->dx.flags.p, T_, fseq, parts_[0].lc, peer_timeout_);
+                SR_HIP(hipGetLastError());
+            }
+            if (corrupt) {
+                corrupt_level_ = -1;
+                dx_corrupt<<<1, 64, 0, stream_>>>(ctx_->parts[parts_[0].res].drecv[par].p, S, (u32)C, parts_[0].id, T_);
                 SR_HIP(hipGetLastError());
             }
         } else if (comm_) {
@@ -1481,10 +1697,16 @@ class DistEngine final : public EngineBase {
             kern<<<ig, 256, 0, stream_>>>(m_, direct_ ? r.drecv[par].p : p.recv.p, S, (u32)C, p.id, T_, p.view(),
                                           p.arena.p, p.apar.p, p.arena_cap, p.lc, undiscovered, p.ctl,
                                           r.pub_dev[p.seq & 1], p.seq, dflags_ && fused_wait_ ? ctx_->dx.flags.p : nullptr,
-                                          fseq, peer_timeout_);
+                                          fseq, peer_timeout_, dcheck() ? 1u : 0u);
             SR_HIP(hipGetLastError());
         }
-        (void)level;
+    }
+    bool dcheck() const { return direct_ && xcheck_; }
+    // memory of the direct exchange's flags and receive buffers (SR_DX_FINE=0: ordinary device
+    // memory, measurements only)
+    static int dx_kind() {
+        const char* e = std::getenv("SR_DX_FINE");
+        return e && std::atoi(e) == 0 ? 0 : 1;
     }
 
     // Direct exchange: receive buffers of T slots of S words for both level parities, and every
@@ -1501,7 +1723,7 @@ class DistEngine final : public EngineBase {
         else SR_HIP(stream_sync(stream_));
         for (auto& p : parts_) {
             const u64 words = std::max<u64>(S * T_, R(p).drecv_words * 2);
-            for (int k = 0; k < 2; ++k) R(p).drecv[k].alloc(o_.device, words);
+            for (int k = 0; k < 2; ++k) R(p).drecv[k].alloc(o_.device, words, dx_kind());
             R(p).drecv_words = words;
         }
         for (int k = 0; k < 2; ++k) {
@@ -1561,8 +1783,9 @@ class DistEngine final : public EngineBase {
         d.T = T_;
         d.fseq = 0;
         if (comm_) {
-            d.flags.alloc(o_.device, T_);
-            SR_HIP(hipMemsetAsync(d.flags.p, 0, T_ * 4, stream_));
+            d.flags.alloc(o_.device, T_, dx_kind());
+            flags_clear<<<1, 64, 0, stream_>>>(d.flags.p, T_);
+            SR_HIP(hipGetLastError());
             std::vector<u64*> owners;
             comm_->peer_addresses(d.flags.p, owners, stream_);
             std::vector<u32*> ft(T_);
@@ -1599,11 +1822,17 @@ class DistEngine final : public EngineBase {
         const size_t RW = T_ + 6 + M::NPROPS;
         for (auto& p : parts_) ctx_->ensure_pub(p.res, RW * T_);
         // the exchange of this check's levels (every rank decides the same: probe_direct is collective)
-        direct_ = direct_env_on() && (comm_ ? comm_->probe_direct(stream_) : T_ > 1);
+        direct_ = direct_env_on() && !direct_off_ && (comm_ ? comm_->probe_direct(stream_) : T_ > 1);
         dflags_ = direct_ && comm_ != nullptr;
         fused_wait_ = dflags_ && comm_->distinct_devices() && fused_env_on();
         stats.pipelined = direct_ ? 2u : 1u;
         if (direct_) direct_setup();
+        if (dcheck())
+            for (auto& p : parts_) {
+                auto& ds = ctx_->parts[p.res].dsum;
+                if (!ds.p) ds.alloc(o_.device, (size_t)NSHARD * MAX_PARTS);
+                SR_HIP(hipMemsetAsync(ds.p, 0, (size_t)NSHARD * MAX_PARTS * 8, stream_));
+            }
         const u64 cmin = lag_cmin_;
         glob_prev_ = 0;
         // What the plan knows (the same on every rank): exact frontier sizes up to the last rows
@@ -1700,6 +1929,11 @@ class DistEngine final : public EngineBase {
             // one level later, the receiver's) error bit is in these rows on every rank.
             if (glob_err & ERR_TABLE_FULL) throw Error(SR_ERR_CAPACITY, "visited set probe limit exceeded");
             if (glob_err & ERR_FRONTIER_OVERFLOW) throw Error(SR_ERR_CAPACITY, "frontier or send bucket overflow");
+            u32 own_err = 0;  // this rank's inserts of `level` (their exchange check)
+            for (size_t i = 0; i < parts_.size(); ++i) own_err |= ctx_->parts[parts_[i].res].pub[(seq0[i] + (level - lvl0_)) & 1]->err;
+            if ((glob_err | own_err) & ERR_EXCHANGE)
+                throw Error(ERR_CODE_EXCHANGE, "direct exchange: a receive slot failed its sequence tag or checksum (level " +
+                                                   std::to_string(level) + ")");
             if (glob_err & ERR_PEER_TIMEOUT) {
                 auto& d = ctx_->dx;
                 d.valid = false;
@@ -1710,7 +1944,7 @@ class DistEngine final : public EngineBase {
                     SR_HIP(hipMemcpy(f.data(), d.flags.p, T_ * 4, hipMemcpyDeviceToHost));
                     for (u32 q = 0; q < T_; ++q) fl += (q ? "," : "") + std::to_string(f[q]);
                 }
-                throw Error(SR_ERR_HIP, "direct exchange: a source's records did not arrive within SR_PEER_TIMEOUT_MS "
+                throw Error(ERR_CODE_EXCHANGE, "direct exchange: a source's records did not arrive within SR_PEER_TIMEOUT_MS "
                                         "(level " + std::to_string(level) + ", rank " + std::to_string(comm_ ? comm_->rank : 0) +
                                         ", last sequence " + std::to_string(d.fseq) + ", flags [" + fl + "], check started at " +
                                         std::to_string(d.fseq_start) + (d.reused ? " reusing" : " after set-up") + ")");
@@ -1754,6 +1988,9 @@ class DistEngine final : public EngineBase {
             if (glob_n) {
                 en_ratio_ = std::max(1.0, (double)glob_enabled / (double)glob_n);
                 rec_ratio_ = (double)recs / (double)glob_n;
+                u64 lnew = 0;
+                for (u32 q = 0; q < T_; ++q) lnew += all[q * RW + T_ + 2];
+                lnew_ratio_ = (double)lnew / (double)glob_n;
                 pair_ratio = (double)maxpair / (double)glob_n;
                 if (glob_prev_) growth = (double)glob_n / (double)glob_prev_;
                 have_rows = true;
@@ -1938,6 +2175,13 @@ class DistEngine final : public EngineBase {
     u64 lag_big_ = std::getenv("SR_LAG_BIG") ? std::strtoull(std::getenv("SR_LAG_BIG"), nullptr, 10) : 262144;
                                // global frontier from which a level is planned after the previous one's rows
     u32 restarts_ = 0;
+    u32 exchange_fallbacks_ = 0;
+    bool direct_off_ = false;  // the direct exchange failed once: the collective exchange from then on
+    // test hook (SR_DX_CORRUPT_LEVEL): corrupt one received slot of this level (enqueue index, first
+    // partition of rank 0 only, once per engine) after its sources checksummed it
+    i64 corrupt_level_ = std::getenv("SR_DX_CORRUPT_LEVEL") ? std::atoll(std::getenv("SR_DX_CORRUPT_LEVEL")) : -1;
+    // the exchange check (SR_DX_CHECK=0 turns it off: measurements only)
+    bool xcheck_ = !(std::getenv("SR_DX_CHECK") && std::atoi(std::getenv("SR_DX_CHECK")) == 0);
     u32 send_cache_max_parts_ = std::getenv("SR_SEND_CACHE") ? (u32)std::atoi(std::getenv("SR_SEND_CACHE")) : 4;
     u64 glob_prev_ = 0;        // pipelined mode: global frontier of the last level read
     // replicated head (SR_HEAD_MAX: largest head frontier; 0 disables)
@@ -1973,18 +2217,29 @@ class DistEngine final : public EngineBase {
         // clamp would force 4 parents per wave, one partly filled round each)
         if (const u32 rs = rstage_recs())
             while (l > 2 && 4.0 * (double)(1u << l) * rec_ratio_ * 1.3 > (double)rs) --l;
+        // ... and, with an owner key, its local new states the local stage
+        if (okey_)
+            while (l > 2 && 4.0 * (double)(1u << l) * lnew_ratio_ * 1.3 > (double)route_local_stage(T_, W, rflags())) --l;
         return l;
     }
-    double rec_ratio_ = 4.0;  // remote records per parent, last level
+    double rec_ratio_ = 4.0;   // remote records per parent, last level
+    double lnew_ratio_ = 2.0;  // new states claimed in place per parent, last level
     // Records staged per chunk in LDS (none with one partition), and expand_route's dynamic LDS.
     u32 rstage_recs() const { return T_ > 1 ? rstage_words() / REC : 0u; }
     // expand_route turns local successors into records to itself from this many partitions on
     // (SR_SELF_RECORDS_MIN; 0 = never): its rounds then wait on no visited-set probe
-    u32 self_rec() const { return self_rec_min_ && T_ >= self_rec_min_ ? 1u : 0u; }
+    // (not with an owner key: most successors are then local, and probing them in place is cheaper)
+    u32 self_rec() const { return !okey_ && self_rec_min_ && T_ >= self_rec_min_ ? 1u : 0u; }
+    u32 rflags() const {
+        const u32 ls = lstage_words_ ? lstage_words_ / W : 0u;  // SR_LSTAGE_WORDS: the local stage's size
+        return self_rec() | (okey_ ? (u32)RF_LOCAL : 0u) | ls << RF_LSTAGE_SHIFT;
+    }
+    u32 lstage_words_ = std::getenv("SR_LSTAGE_WORDS") ? (u32)std::atoi(std::getenv("SR_LSTAGE_WORDS")) : 0u;
+    const bool okey_ = uses_owner_key(m_);  // states owned by the model's owner key (kernels_dist.hpp part_of)
     u32 self_rec_min_ = std::getenv("SR_SELF_RECORDS_MIN") ? (u32)std::atoi(std::getenv("SR_SELF_RECORDS_MIN")) : 5u;
     size_t route_lds() const {
         return (filt_log2_ ? (8u << filt_log2_) : 0u) + (size_t)rstage_recs() * (REC * 8 + 2 + 1) +
-               (size_t)route_local_stage(T_, W, self_rec()) * (W * 8 + 4);
+               (size_t)route_local_stage(T_, W, rflags()) * (W * 8 + 4);
     }
     // expand_route's grid: two device residencies at its LDS footprint (expand_fast's rule); the
     // kernel strides over further parents. SR_ROUTE_GRID_MAX > 0 overrides it.
@@ -2023,7 +2278,8 @@ class DistEngine final : public EngineBase {
     // chunk of 4 x 32 parents then fits: 2pc N=11 at T = 8 routes in 41 instead of 69 ms per check)
     // (0 = that default; SR_RSTAGE_WORDS overrides)
     u32 rstage_words_ = std::getenv("SR_RSTAGE_WORDS") ? (u32)std::atoi(std::getenv("SR_RSTAGE_WORDS")) : 0u;
-    u32 rstage_words() const { return rstage_words_ ? rstage_words_ : self_rec() ? 2048u : 1024u; }
+    // (with an owner key most successors are local: a small record stage leaves LDS for residency)
+    u32 rstage_words() const { return rstage_words_ ? rstage_words_ : self_rec() ? 2048u : okey_ ? 256u : 1024u; }
     int route_ppw_env_ = std::getenv("SR_ROUTE_PPW_LOG2") ? std::atoi(std::getenv("SR_ROUTE_PPW_LOG2")) : -1;
     bool trace_ = std::getenv("SR_DIST_TRACE") != nullptr;
     Clock::time_point t_trace_ = Clock::now();

@@ -15,6 +15,14 @@ static void set_error(const std::string& e) { g_last_error = e; }
 
 namespace sr {
 
+// 2pc's owner key for the partitioned search (TwoPhase::okey_rms): the tuples of this many RMs.
+// More RMs balance the partitions better, fewer keep more successors local (DESIGN.md §6 measures
+// the trade-off). SR_OWNER_RMS overrides it; 0 owns states by fingerprint.
+static int two_phase_owner_rms(int n) {
+    if (const char* e = std::getenv("SR_OWNER_RMS")) return std::max(0, std::min(n, std::atoi(e)));
+    return std::min(6, (n + 1) / 2);
+}
+
 // The registry below instantiates `E<Model>` for every model; the single-GPU engine and the
 // partitioned engine share it.
 template <template <class> class E, class... Args>
@@ -33,8 +41,9 @@ static std::unique_ptr<EngineBase> make_model_engine(int model, const i64* p, in
         case SR_MODEL_2PC:
             need(1);
             if (p[0] < 1 || p[0] > 14) throw Error(SR_ERR_UNSUPPORTED, "2pc: rm_count must be in 1..=14 (4n+4 <= 63 bits)");
-            if (o.symmetry) return std::make_unique<E<Canon<TwoPhase>>>(Canon<TwoPhase>(TwoPhase{(int)p[0]}), o, args...);
-            return std::make_unique<E<TwoPhase>>(TwoPhase{(int)p[0]}, o, args...);
+            if (o.symmetry)
+                return std::make_unique<E<Canon<TwoPhase>>>(Canon<TwoPhase>(TwoPhase{(int)p[0], two_phase_owner_rms((int)p[0])}), o, args...);
+            return std::make_unique<E<TwoPhase>>(TwoPhase{(int)p[0], two_phase_owner_rms((int)p[0])}, o, args...);
         case SR_MODEL_INCREMENT:
             need(1);
             if (p[0] < 1 || p[0] > 15) throw Error(SR_ERR_UNSUPPORTED, "increment: threads must be in 1..=15");
@@ -245,7 +254,7 @@ struct sr_dist {
     hipStream_t get_stream() {
         if (!stream) {
             SR_HIP(hipSetDevice(c->device));
-            SR_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+            SR_HIP(create_stream(&stream, c->device));
         }
         return stream;
     }
@@ -669,7 +678,7 @@ int32_t sr_dist_allreduce_f64(sr_dist* d, double* values, int32_t n, int32_t op)
 
 void sr_dist_free(sr_dist* d) {
     if (!d) return;
-    if (d->stream) (void)hipStreamDestroy(d->stream);
+    if (d->stream && hipStreamDestroy(d->stream) == hipSuccess) StreamCensus::get().destroyed(d->c->device);
     delete d;
 }
 

@@ -45,7 +45,9 @@ constexpr int MAX_PARTS = 64;  // visited-set partitions (one per GPU, or virtua
 #define SR_WIDE_STAGE_WORDS 2048
 #endif
 
-enum ErrBits { ERR_TABLE_FULL = 1, ERR_FRONTIER_OVERFLOW = 2, ERR_PEER_TIMEOUT = 4 };
+// ERR_EXCHANGE: the direct exchange delivered a receive slot whose sequence tag or checksum does
+// not match what its source stored (kernels_dist.hpp): the check is redone on the collective exchange.
+enum ErrBits { ERR_TABLE_FULL = 1, ERR_FRONTIER_OVERFLOW = 2, ERR_PEER_TIMEOUT = 4, ERR_EXCHANGE = 8 };
 
 // Two slot encodings ("Visited set"):
 //  * fingerprint mode (qbits == 0): a slot holds the 64-bit fingerprint. Exact for one-word states
@@ -572,6 +574,18 @@ __device__ __forceinline__ u32 block_sum(u32 v, u32* scratch) {
     __syncthreads();
     u32 t = 0;
     for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += scratch[w];
+    __syncthreads();
+    return t;
+}
+
+// 64-bit sum of v over the workgroup, returned to every thread (one LDS round; sc: a u64 per wave).
+__device__ __forceinline__ u64 block_sum64(u64 v, u64* sc) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+    if ((threadIdx.x & 63) == 0) sc[threadIdx.x >> 6] = v;
+    __syncthreads();
+    u64 t = 0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += sc[w];
     __syncthreads();
     return t;
 }

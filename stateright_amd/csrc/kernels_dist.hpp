@@ -23,6 +23,24 @@ constexpr u64 PAR_SEARCH = ~0ull - 1;  // parent not recorded: search the previo
 
 // Owner partition of a fingerprint: the high 32 bits scaled to [0, T) (any T, uniform).
 __device__ __host__ __forceinline__ u32 owner_of(u64 fp, u32 nparts) { return (u32)(((fp >> 32) * (u64)nparts) >> 32); }
+// Owner partition of state s (fingerprint fp): by the model's owner key when it has one
+// (models.hpp has_owner_key; mixed, then scaled like a fingerprint), else by the fingerprint.
+template <class M>
+__device__ __host__ __forceinline__ u32 part_of(const M& m, const u64* s, u64 fp, u32 nparts) {
+    if constexpr (has_owner_key<M>::value) {
+        u64 key;
+        if (m.owner_key(s, &key)) return owner_of(fmix64(key * 0x9E3779B97F4A7C15ull + 0x632BE59BD9B4E019ull), nparts);
+    }
+    return owner_of(fp, nparts);
+}
+template <class M>
+inline bool uses_owner_key(const M& m) {
+    if constexpr (has_owner_key<M>::value) {
+        u64 s[M::W] = {}, key;
+        return m.owner_key(s, &key);
+    }
+    return false;
+}
 
 // Device-side control block of one partition: the size of the frontier being expanded and the
 // discovery ranks among it. The last workgroup of insert_recv writes it for the next level, so the
@@ -40,6 +58,13 @@ struct DistCtl {
 // the all-to-all also delivers every partition's row to every rank (no separate all-gather, no
 // host wait inside a level). Bucket q of a sender = [HDR words: row][C records].
 constexpr u32 DIST_HDR = 128;
+// Direct exchange: the last two header words of a slot are the level's flag sequence number and a
+// checksum: the wrapping sum of every record word the source stored into that slot plus every row
+// word of the header. The owner's insert recomputes both (ERR_EXCHANGE on a mismatch), so a slot
+// read with a stale cached line, a late or a lost store cannot turn into a silently wrong count:
+// the sequence tag shares a line with the checksum, and the checksum covers every other line.
+constexpr u32 HDR_SEQ = DIST_HDR - 2, HDR_SUM = DIST_HDR - 1;
+static_assert(MAX_PARTS + 6 + MAX_PROPS <= (int)HDR_SEQ, "the row fits the header before its tag");
 
 // Row published by the last workgroup of expand_route (u64 words; RW = T + 6 + NPROPS):
 //   [0, T)  records routed to each partition      T     frontier size n
@@ -64,14 +89,16 @@ __device__ __forceinline__ bool last_workgroup(LevelCounters* lc) {
 // Pipelined mode: the last workgroup of a launch, told to every thread of that workgroup.
 // `sysrel`: the workgroup's stores went (also) to another device's memory (direct exchange), so
 // they are released at system scope before the ticket, and the last workgroup acquires them.
-__device__ __forceinline__ bool last_block(LevelCounters* lc, bool sysrel = false) {
+// `sysacq`: the last workgroup acquires at system scope whatever its own stores were (it then
+// raises flags that publish every workgroup's remote stores).
+__device__ __forceinline__ bool last_block(LevelCounters* lc, bool sysrel = false, bool sysacq = false) {
     __shared__ u32 is_last;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
         if (sysrel) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
         is_last = take_ticket(lc);
-        if (sysrel && is_last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        if ((sysrel || sysacq) && is_last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     }
     __syncthreads();
     return is_last != 0;
@@ -116,9 +143,15 @@ __global__ void peer_signal(u32* const* ftab, u32 nparts, u32 seq) {
 // new states (a growth level of 2pc makes ~3 per parent, 768 per 256-parent chunk), so the stage
 // shrinks with T and leaves its LDS to the record stage: LDS per block sets residency, and the
 // probes of this kernel are latency-bound.
-// With self records (below) nothing is inserted locally: no stage.
-__host__ __device__ __forceinline__ u32 route_local_stage(u32 nparts, int W, u32 self_rec) {
-    return self_rec ? 0u : (nparts <= 1 ? 1024u : nparts == 2 ? 512u : 256u) / (u32)W;
+// With self records (below) nothing is inserted locally: no stage. With an owner key most new
+// states are local: the stage of one partition.
+// rflags: RF_SELF (self records), RF_LOCAL (owner key: most successors stay local), and from bit 8
+// on the local stage's size in states when the host sets one (RF_LSTAGE_SHIFT; 0 = this default).
+enum RouteFlags : u32 { RF_SELF = 1, RF_LOCAL = 2, RF_LSTAGE_SHIFT = 8 };
+__host__ __device__ __forceinline__ u32 route_local_stage(u32 nparts, int W, u32 rflags) {
+    if (rflags & RF_SELF) return 0u;
+    if (rflags >> RF_LSTAGE_SHIFT) return rflags >> RF_LSTAGE_SHIFT;
+    return (nparts <= 1 || (rflags & RF_LOCAL) ? 1024u : nparts == 2 ? 512u : 256u) / (u32)W;
 }
 
 // Expands the frontier of this partition (its size n is read from ctl). Same structure as
@@ -134,20 +167,28 @@ __host__ __device__ __forceinline__ u32 route_local_stage(u32 nparts, int W, u32
 // bucket counters are the only same-address atomics, so they must be rare: per-successor or
 // per-wave reservations serialise at the L2 when every wave of the GPU targets T addresses.
 // A stage that overflows (a chunk larger than planned) falls back to per-wave reservations.
+// Six waves per SIMD (<= 80 VGPRs) for narrow states: the kernel waits on memory, and at its
+// natural 83 VGPRs it ran five (2pc N=11 at T = 8 with an owner key, where it probes most
+// successors in place). Wide states (paxos) are bound by their LDS stages instead.
 template <class M, int PB, bool SELF = false>
-__global__ void __launch_bounds__(256) expand_route(M m, u64* __restrict__ arena, u64* __restrict__ apar, u64 nb,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W <= 2 ? 6 : 1))) expand_route(M m, u64* __restrict__ arena, u64* __restrict__ apar, u64 nb,
                                                     u64 arena_cap, TableView t, u32 my_part, u32 nparts,
                                                     u64* __restrict__ send, u32 bucket_cap, u32* send_counts,
                                                     LevelCounters* lc, DistCtl* ctl, u32 undiscovered, u64* row,
                                                     u32 ppw_log2, u32 filt_log2, u64 bucket_stride, u32 lag,
                                                     u64* __restrict__ sent, u64 sent_mask, u32 rs,
-                                                    u64* const* ptab, u32* const* ftab, u32 fseq, u32 self_rec) {
+                                                    u64* const* ptab, u32* const* ftab, u32 fseq, u32 rflags,
+                                                    u64* dsum) {
+    // dsum (direct exchange): [NSHARD][MAX_PARTS] per-owner sums of the record words this launch
+    // stores, accumulated per chunk flush into shard blockIdx % NSHARD (non-returning atomics, spread
+    // like the statistics); the last workgroup folds them into each owner's slot checksum (HDR_SUM).
     // self_rec: successors owned by this partition become records too (to its own slot), so this
     // kernel probes nothing and has no global round trip per round of successors: with many
     // partitions 1/T of the lanes probed and the whole wave waited for them. The insert kernel
     // then probes every successor, with its batched probes. SELF = the same, fixed at compile time:
     // the instantiation for self records has no probe, claim, local stage or sent-cache code at all
     // (the kernel is instruction-bound there: profiles/r03_pmc_instruction_mix.txt).
+    u32 self_rec = rflags & RF_SELF;
     if constexpr (SELF) {
         self_rec = 1;
         sent = nullptr;
@@ -165,7 +206,7 @@ __global__ void __launch_bounds__(256) expand_route(M m, u64* __restrict__ arena
     // rs (records staged per chunk, all owners) is chosen on the host: 0 with one partition, so the
     // one-partition launch keeps expand_fast's occupancy; ls = route_local_stage(nparts).
     extern __shared__ u64 dyn[];
-    const u32 RSTAGE = rs, STAGE = route_local_stage(nparts, W, self_rec);
+    const u32 RSTAGE = rs, STAGE = route_local_stage(nparts, W, SELF ? (u32)RF_SELF : rflags);
     u64* filt = dyn;
     u64* rstage = dyn + (filt_log2 ? (1u << filt_log2) : 0u);
     u64* stage = rstage + (u64)rs * REC;
@@ -173,6 +214,7 @@ __global__ void __launch_bounds__(256) expand_route(M m, u64* __restrict__ arena
     u16* rrank = reinterpret_cast<u16*>(stage_par + STAGE);
     u8* rown = reinterpret_cast<u8*>(rrank + rs);
     __shared__ u32 ocnt[MAX_PARTS], obase[MAX_PARTS];
+    __shared__ u64 ocsum[MAX_PARTS];  // the chunk's record-word sum per owner (dsum)
     __shared__ u64 pst[4][64 * W];
     // the wave's successor list, (parent, action) per successor (see expand_fast), in windows
     constexpr u32 MAPCAP = 512;
@@ -192,8 +234,9 @@ __global__ void __launch_bounds__(256) expand_route(M m, u64* __restrict__ arena
     const u32 fmask = filt_log2 ? (1u << filt_log2) - 1 : 0;
     __shared__ u32 sent_any;  // this workgroup stored records (direct exchange: release them)
     if (threadIdx.x == 0) stage_n = rstage_n = sent_any = 0;
-    for (u32 q = threadIdx.x; q < nparts; q += blockDim.x) ocnt[q] = 0;
+    for (u32 q = threadIdx.x; q < nparts; q += blockDim.x) ocnt[q] = 0, ocsum[q] = 0;
     for (u32 i = threadIdx.x; i < (fmask ? fmask + 1 : 0u); i += blockDim.x) filt[i] = 0;
+    u64* const my_dsum = dsum ? dsum + (u64)(blockIdx.x % NSHARD) * MAX_PARTS : nullptr;
 
     u32 succ = 0, enabled = 0;
     const u64 chunk = (u64)(blockDim.x >> 6) * ppw;
@@ -287,7 +330,7 @@ __global__ void __launch_bounds__(256) expand_route(M m, u64* __restrict__ arena
                         ok[j] = false;
                     }
                 }
-                own[j] = ok[j] ? owner_of(key[j], nparts) : my_part;
+                own[j] = ok[j] ? part_of(m, ns[j], key[j], nparts) : my_part;
                 rem[j] = ok[j] && (SELF || self_rec || own[j] != my_part);
             }
             // One memory round trip per round: a local successor's visited-set probe and a remote
@@ -385,8 +428,10 @@ __global__ void __launch_bounds__(256) expand_route(M m, u64* __restrict__ arena
                         const u32 pos = gb + __popcll(qm & lanes_below);
                         if (pos < bucket_cap) {
                             u64* rec = sdst[q] + (u64)pos * REC;
+                            u64 v = 0;
 #pragma unroll
-                            for (int x = 0; x < W; ++x) rec[x] = ns[j][x];
+                            for (int x = 0; x < W; ++x) rec[x] = ns[j][x], v += ns[j][x];
+                            if (my_dsum) atomicAdd(reinterpret_cast<unsigned long long*>(&my_dsum[q]), (unsigned long long)v);
                         } else {
                             atomicOr(&lc->err, (u32)ERR_FRONTIER_OVERFLOW);
                         }
@@ -403,7 +448,15 @@ __global__ void __launch_bounds__(256) expand_route(M m, u64* __restrict__ arena
         const u32 nl = min(stage_n, (u32)STAGE);
         const u32 nr = min(rstage_n, RSTAGE);
         if (nr && threadIdx.x == 0) sent_any = 1;
-        for (u32 i = threadIdx.x; i < nr; i += blockDim.x) rrank[i] = (u16)atomicAdd(&ocnt[rown[i]], 1u);
+        for (u32 i = threadIdx.x; i < nr; i += blockDim.x) {
+            rrank[i] = (u16)atomicAdd(&ocnt[rown[i]], 1u);
+            if (my_dsum) {
+                u64 v = 0;
+#pragma unroll
+                for (int x = 0; x < REC; ++x) v += rstage[i * REC + x];
+                atomicAdd(reinterpret_cast<unsigned long long*>(&ocsum[rown[i]]), (unsigned long long)v);
+            }
+        }
         if (threadIdx.x == 0 && nl) base = atomicAdd(&lc->claims, nl);
         __syncthreads();
         if (threadIdx.x == 0) stage_n = rstage_n = 0;
@@ -411,6 +464,10 @@ __global__ void __launch_bounds__(256) expand_route(M m, u64* __restrict__ arena
             const u32 c = ocnt[q];
             obase[q] = c ? atomicAdd(&send_counts[q], c) : 0;
             ocnt[q] = 0;
+            if (my_dsum && c) {
+                atomicAdd(reinterpret_cast<unsigned long long*>(&my_dsum[q]), (unsigned long long)ocsum[q]);
+                ocsum[q] = 0;
+            }
         }
         for (u32 i = threadIdx.x; i < nl; i += blockDim.x) {
             const u32 pos = base + i;
@@ -437,16 +494,28 @@ __global__ void __launch_bounds__(256) expand_route(M m, u64* __restrict__ arena
     u32 total_succ = block_sum(succ, scratch);
     u32 total_enabled = block_sum(enabled, scratch);
     if (threadIdx.x == 0) add_stats(lc, total_succ, total_enabled);
-    if (!last_block(lc, ftab != nullptr && sent_any)) return;
+    if (!last_block(lc, ftab != nullptr && sent_any, ftab != nullptr)) return;
     // The row, one word per thread (every source word is a round trip to the coherence point: one
     // thread loading them in turn was the floor of a small level), staged in LDS for the headers.
     __shared__ u64 srow[MAX_PARTS + 6 + MAX_PROPS];
     __shared__ u64 sstat[4];  // the statistics summed over their shards
+    __shared__ u64 hsum[MAX_PARTS];  // dsum: each owner's record-word sum over the shards
     if (threadIdx.x < 64) {
         const u64 v = gather_stats(lc, threadIdx.x);
         if ((threadIdx.x & 15) == 0) sstat[threadIdx.x >> 4] = v;
     }
+    for (u32 q = threadIdx.x; q < nparts; q += blockDim.x) hsum[q] = 0;
     __syncthreads();
+    if (dsum && lag) {  // the shards' loads are issued together with the row's below (one round trip)
+        for (u32 i = threadIdx.x; i < NSHARD * nparts; i += blockDim.x) {
+            u64* a = dsum + (u64)(i / nparts) * MAX_PARTS + (i % nparts);
+            const u64 v = __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (v) {
+                atomicAdd(reinterpret_cast<unsigned long long*>(&hsum[i % nparts]), (unsigned long long)v);
+                *a = 0;  // for the next level (a later launch)
+            }
+        }
+    }
     const u32 rw = nparts + 6 + M::NPROPS;
     for (u32 w = threadIdx.x; w < rw; w += blockDim.x) {
         const u32 f = w - nparts;  // row fields after the per-destination counts
@@ -467,6 +536,14 @@ __global__ void __launch_bounds__(256) expand_route(M m, u64* __restrict__ arena
         for (u32 i = threadIdx.x; i < nparts * rw; i += blockDim.x) {
             const u32 q = i / rw, w = i - q * rw;
             (sdst[q] - DIST_HDR)[w] = srow[w];
+        }
+    if (dsum && lag)  // each slot's sequence tag and checksum (records + row words)
+        for (u32 q = threadIdx.x; q < nparts; q += blockDim.x) {
+            u64 rs = 0;
+            for (u32 w = 0; w < rw; ++w) rs += srow[w];
+            u64* hdr = sdst[q] - DIST_HDR;
+            hdr[HDR_SEQ] = fseq;
+            hdr[HDR_SUM] = hsum[q] + rs;
         }
     if (threadIdx.x < 64) reset_stats_tickets(lc, threadIdx.x, true);
     if (!ftab) return;
@@ -489,7 +566,7 @@ __global__ void __launch_bounds__(256) expand_route(M m, u64* __restrict__ arena
 template <int IPB, class M, class RecAt>
 __device__ __forceinline__ void insert_records(const M& m, RecAt rec_at, u32 total, const TableView& t, u64* next,
                                                u64* next_par, u32 next_cap, LevelCounters* lc, u32 undiscovered,
-                                               u64* stage, u32 STAGE, u32& stage_n, u32& base) {
+                                               u64* stage, u32 STAGE, u32& stage_n, u32& base, u64& rsum) {
     constexpr int W = M::W;
     const int lane = threadIdx.x & 63;
     auto flush = [&](u32 nl) {
@@ -529,7 +606,7 @@ __device__ __forceinline__ void insert_records(const M& m, RecAt rec_at, u32 tot
             if (ok[j]) {
                 const u64* rec = rec_at((u32)g);
 #pragma unroll
-                for (int x = 0; x < W; ++x) ns[j][x] = rec[x];
+                for (int x = 0; x < W; ++x) ns[j][x] = rec[x], rsum += rec[x];
                 pk[j] = probe_key(m, t, ns[j]);
             }
         }
@@ -591,8 +668,9 @@ __global__ void __launch_bounds__(256) insert_recv(M m, const u64* __restrict__ 
     __shared__ u64 stage[STAGE * W];
     __shared__ u32 stage_n, base;
     if (threadIdx.x == 0) stage_n = 0;
+    u64 rsum = 0;  // (unchecked: RCCL's exchange)
     insert_records<1>(m, [&](u32 g) { return recv + (u64)g * REC; }, nrec, t, next, next_par, next_cap, lc, undiscovered,
-                   stage, STAGE, stage_n, base);
+                   stage, STAGE, stage_n, base, rsum);
     if (!last_workgroup<M::NPROPS>(lc)) return;
     const u32 claims = __hip_atomic_load(&lc->claims, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     ctl->n = min(claims, next_cap);
@@ -626,7 +704,10 @@ __global__ void __launch_bounds__(256) insert_recv_lag(M m, const u64* __restric
                                                        u32 nparts, TableView t, u64* __restrict__ arena,
                                                        u64* __restrict__ apar, u64 arena_cap, LevelCounters* lc,
                                                        u32 undiscovered, DistCtl* ctl, LagPub* pub, u32 seq,
-                                                       const u32* wflags, u32 wseq, u64 wtimeout) {
+                                                       const u32* wflags, u32 wseq, u64 wtimeout, u32 xcheck) {
+    // xcheck (direct exchange): verify every source's slot against its sequence tag and checksum
+    // (HDR_SEQ / HDR_SUM); the record words this launch read are summed per workgroup into the
+    // statistics shards' xsum word, and the last workgroup compares. ERR_EXCHANGE on a mismatch.
     constexpr int W = M::W, REC = W;
     constexpr u32 STAGE = 1024 / W;
     __shared__ u64 stage[STAGE * W];
@@ -685,23 +766,63 @@ __global__ void __launch_bounds__(256) insert_recv_lag(M m, const u64* __restric
             if (q + step < nparts && qoff[q + step] <= g) q += step;
         return recv + (u64)q * S + DIST_HDR + (u64)(g - qoff[q]) * REC;
     };
-    insert_records<IPB>(m, rec_at, total, t, next, next_par, next_cap, lc, undiscovered, stage, STAGE, stage_n, base);
+    u64 rsum = 0;
+    insert_records<IPB>(m, rec_at, total, t, next, next_par, next_cap, lc, undiscovered, stage, STAGE, stage_n, base, rsum);
+    __shared__ u64 sc64[4];
+    if (xcheck) {
+        const u64 bs = block_sum64(rsum, sc64);
+        if (threadIdx.x == 0 && bs) atomicAdd(reinterpret_cast<unsigned long long*>(&lc->stat[blockIdx.x % NSHARD].pad[0]),
+                                              (unsigned long long)bs);
+    }
     if (!last_block(lc)) return;
     // every row (the bucket headers) to the host, then the close
     const u32 rw = nparts + 6 + M::NPROPS;
+    u64 rows_sum = 0;
     for (u32 w = threadIdx.x; w < nparts * rw; w += blockDim.x) {
         const u32 q = w / rw;
-        pub->rows[w] = recv[(u64)q * S + (w - q * rw)];
+        const u64 v = recv[(u64)q * S + (w - q * rw)];
+        pub->rows[w] = v;
+        rows_sum += v;
+    }
+    __shared__ u32 xbad;
+    if (xcheck) {
+        // got = every record word read + every row word; want = the sources' checksums; each tag =
+        // this level's sequence number. A source that overflowed its slot (count > C) is a capacity
+        // error of its own row, not a corrupt exchange.
+        __shared__ u64 xacc[2];
+        __shared__ u32 xseq_bad, xover;
+        if (threadIdx.x == 0) xacc[0] = xacc[1] = 0, xseq_bad = xover = 0;
+        const u64 rs = block_sum64(rows_sum, sc64);  // (its barriers order the resets above)
+        for (u32 i = threadIdx.x; i < NSHARD + 2 * nparts; i += blockDim.x) {
+            if (i < NSHARD) {
+                u64* a = &lc->stat[i].pad[0];
+                const u64 v = __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (v) atomicAdd(reinterpret_cast<unsigned long long*>(&xacc[0]), (unsigned long long)v), *a = 0;
+            } else if (i < NSHARD + nparts) {
+                const u32 q = i - NSHARD;
+                if (recv[(u64)q * S + HDR_SEQ] != (u64)wseq) xseq_bad = 1;
+                if (recv[(u64)q * S + me] > (u64)C) xover = 1;
+            } else {
+                const u32 q = i - NSHARD - nparts;
+                atomicAdd(reinterpret_cast<unsigned long long*>(&xacc[1]), (unsigned long long)recv[(u64)q * S + HDR_SUM]);
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) xbad = !xover && (xseq_bad || xacc[0] + rs != xacc[1]);
+    } else if (threadIdx.x == 0) {
+        xbad = 0;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x >= 64) return;
+    if (threadIdx.x == 0 && xbad) atomicOr(&lc->err, (u32)ERR_EXCHANGE);  // persists into the next rows
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     // the close, one counter per lane of wave 0: lane 0 claims, 1 err, 2 + p disc[p]
     const u32 lane = threadIdx.x;
     const bool live = lane < 2u + (u32)M::NPROPS;
     const u32* src = lane == 0 ? &lc->claims : lane == 1 ? &lc->err : &lc->disc[live ? lane - 2 : 0];
     const u32 v = live ? __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-    const u32 claims = __shfl(v, 0, 64), err = __shfl(v, 1, 64);
+    const u32 claims = __shfl(v, 0, 64), err = __shfl(v, 1, 64) | (xbad ? (u32)ERR_EXCHANGE : 0u);
     if (lane >= 2 && live) {
         ctl->disc_prev[lane - 2] = v;
         lc->disc[lane - 2] = ~0u;
@@ -728,6 +849,21 @@ __global__ void rows_publish(const u64* rows, u64* host_rows, u32 words, u32* ho
     if (threadIdx.x == 0) __hip_atomic_store(host_seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// Test hook of the exchange check (SR_DX_CORRUPT_LEVEL): flips one bit of the first record some
+// source stored into this owner's receive slots, or of a header row word when no source sent any,
+// AFTER the sources computed their checksums. The owner's insert must report ERR_EXCHANGE.
+__global__ void dx_corrupt(u64* recv, u64 S, u32 C, u32 me, u32 nparts) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    for (u32 q = 0; q < nparts; ++q) {
+        const u64 c = recv[(u64)q * S + me];
+        if (c && c <= C) {
+            recv[(u64)q * S + DIST_HDR] ^= 1;
+            return;
+        }
+    }
+    recv[nparts + 4] ^= 1;  // source 0's row: enabled slots (statistics only)
+}
+
 // Init states owned by this partition (insert + level-0 properties), in visit order.
 template <class M>
 __global__ void insert_roots_part(M m, TableView t, const u64* states, u32 n, u32 my_part, u32 nparts, u64* out, u64* out_par,
@@ -738,7 +874,7 @@ __global__ void insert_roots_part(M m, TableView t, const u64* states, u32 n, u3
         u64 s[M::W];
         load_state<M::W>(states, r, s);
         u64 key = fingerprint<M::W>(s);
-        if (owner_of(key, nparts) != my_part) continue;
+        if (part_of(m, s, key, nparts) != my_part) continue;
         bool is_new;
         find_or_claim(t, probe_key(m, t, s), &is_new, &lc->err);
         if (is_new) lc->claims += 1;
@@ -763,7 +899,7 @@ __global__ void take_owned(M m, const u64* __restrict__ hstates, u32 total, u32 
     if (i < total) {
         load_state<M::W>(hstates, i, s);
         const u64 fp = fingerprint<M::W>(s);
-        mine = owner_of(fp, nparts) == my_part;
+        mine = part_of(m, s, fp, nparts) == my_part;
         if (mine) find_or_claim(t, probe_key(m, t, s), &nw, &lc->err);
     }
     const u64 cm = __ballot(nw);

@@ -73,6 +73,18 @@ template <class M>
 struct has_self_loops<M, std::void_t<decltype(std::declval<const M&>().self_loops((const u64*)nullptr, (const u64*)nullptr,
                                                                                   (u64*)nullptr))>> : std::true_type {};
 
+// Models with an OWNER KEY (`owner_key(s, &key)`: a projection of the state that most actions
+// leave unchanged; returns false when this instance has none). The partitioned search then owns a
+// state by its key instead of its fingerprint, so most successors stay in their parent's
+// partition and are inserted there instead of crossing to another GPU. Any
+// deterministic function of the state keeps the search exact (every state has exactly one
+// owner); the projection only sets the share of successors that cross and the load balance.
+template <class M, class = void>
+struct has_owner_key : std::false_type {};
+template <class M>
+struct has_owner_key<M, std::void_t<decltype(std::declval<const M&>().owner_key((const u64*)nullptr, (u64*)nullptr))>>
+    : std::true_type {};
+
 // Init states (`Model::init_states`, src/lib.rs:163). A model writes its init states into a host
 // buffer of W words each; the engine sizes that buffer from the model's optional `init_count()`,
 // or for MAX_INIT_STATES states when the model has none (the documented bound of the GpuModel
@@ -221,6 +233,17 @@ struct BinaryClock {
 struct TwoPhase {
     static constexpr int W = 1, MW = 2, NPROPS = 3;
     int n;
+    // Owner key of the partitioned search: the per-RM tuples (rm_state, tm_prepared,
+    // Prepared{rm} in msgs) of the first okey_rms resource managers (0: no key, own by
+    // fingerprint). Only the five actions of those RMs change it; TmCommit/TmAbort and the other
+    // RMs' actions keep a successor in its parent's partition.
+    int okey_rms = 0;
+    SR_HD bool owner_key(const u64* sp, u64* key) const {
+        const int k = okey_rms;
+        const u64 s = sp[0], m = (1ull << k) - 1;
+        *key = (s & ((1ull << (2 * k)) - 1)) | ((s >> (2 * n + 2)) & m) << (2 * k) | ((s >> (3 * n + 2)) & m) << (3 * k);
+        return k > 0;
+    }
     int max_actions() const { return 2 + 5 * n; }
     // Per rm at most three of its five slots (a Working rm after TmAbort: Prepare, ChooseToAbort,
     // RcvAbort); TmCommit/TmAbort only while the TM is Init (then at most two per rm).

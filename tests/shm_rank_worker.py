@@ -24,7 +24,8 @@ def main():
             st = c.stats()
             print(json.dumps({"rank": rank, "check": spec, "unique": c.unique_state_count(), "states": c.state_count(),
                               "depth": c.max_depth(), "discoveries": sorted(c.discoveries()),
-                              "pipelined": st["pipelined"], "restarts": st["restarts"]}), flush=True)
+                              "pipelined": st["pipelined"], "restarts": st["restarts"],
+                              "exchange_fallbacks": st["exchange_fallbacks"]}), flush=True)
             c = None
     finally:
         comm.close()

@@ -7,6 +7,11 @@ fail (RCCL would hang). Counts must equal the oracle's, every rank reports the s
 and discovery paths are available from ANY single rank after join (gathered at join), replaying on
 the CPU oracle model. Plus the BASELINE configuration 4 at its full size: 2pc N=11 partitioned 8
 ways (virtual partitions) against the closed forms of BASELINE.md §3."""
+import json
+import os
+import subprocess
+import sys
+
 import pytest
 
 from oracle_lib import INCREMENT_LOCK, LINEAR_EQUATION, TWO_PHASE, OracleRun, replay
@@ -228,3 +233,82 @@ def test_direct_repeated_checks_same_ranks(head, monkeypatch):
     finally:
         for c in comms:
             c.close()
+
+
+@pytest.mark.parametrize("level", [1, 3])
+def test_corrupt_slot_falls_back_to_collective(level, monkeypatch):
+    # The exchange check: a record (or a header row word, at a level where no source
+    # sent records to rank 0) flipped after its source checksummed the slot makes the owner's insert
+    # report ERR_EXCHANGE; the ranks vote, and the check is redone on the collective exchange with
+    # exact counts. The communicator then keeps the collective exchange.
+    monkeypatch.setenv("SR_HEAD_MAX", "0")
+    monkeypatch.setenv("SR_DX_CORRUPT_LEVEL", str(level))
+    o = oracle(TWO_PHASE, [6])
+    comms = Communicator.local_group(2)
+    try:
+        for k in range(2):
+            cs = [sr.TwoPhaseSys(6).checker().comm(c).spawn_bfs() for c in comms]
+            for ch in cs:
+                ch.join()
+            for ch in cs:
+                assert (ch.unique_state_count(), ch.state_count(), ch.max_depth()) == \
+                    (o.unique_state_count, o.state_count, o.max_depth)
+                st = ch.stats()
+                assert st["exchange_fallbacks"] == (1 if k == 0 else 0), st
+                assert st["pipelined"] == 1, st
+            cs.clear()
+    finally:
+        for c in comms:
+            c.close()
+
+
+def test_corrupt_slot_virtual_partitions(monkeypatch):
+    # the same check between virtual partitions of one process (no vote: the engine itself redoes
+    # the check on the device-copy exchange)
+    monkeypatch.setenv("SR_HEAD_MAX", "0")
+    monkeypatch.setenv("SR_DX_CORRUPT_LEVEL", "4")
+    o = oracle(TWO_PHASE, [7])
+    c = sr.TwoPhaseSys(7).checker().partitions(4).spawn_bfs().join()
+    assert (c.unique_state_count(), c.state_count(), c.max_depth()) == (o.unique_state_count, o.state_count, o.max_depth)
+    st = c.stats()
+    assert st["exchange_fallbacks"] == 1 and st["pipelined"] == 1, st
+
+
+def test_exchange_check_passes_without_corruption(monkeypatch):
+    # the checksum of every slot agrees on a full 2pc N=9 partitioned search (no fallback)
+    monkeypatch.delenv("SR_DX_CORRUPT_LEVEL", raising=False)
+    n = 9
+    c = sr.TwoPhaseSys(n).checker().partitions(3).spawn_bfs().join()
+    assert c.unique_state_count() == 6 ** n + 4 ** n + 2 ** n
+    st = c.stats()
+    assert st["exchange_fallbacks"] == 0 and st["pipelined"] == 2, st
+
+
+_QUEUE_SCRIPT = """
+import json, sys
+sys.path.insert(0, {root!r})
+import stateright_amd as sr
+from stateright_amd.distributed import Communicator
+comms = Communicator.local_group(8)
+cs = [sr.TwoPhaseSys(7).checker().comm(c).spawn_bfs() for c in comms]
+for ch in cs:
+    ch.join()
+print(json.dumps([[ch.unique_state_count(), ch.state_count(), ch.max_depth(), ch.stats()["pipelined"]] for ch in cs]))
+"""
+
+
+def test_world8_one_device_default_queues():
+    # Eight in-process ranks on ONE device with HIP's default of 4 hardware queues, set before the
+    # runtime starts (a fresh interpreter): the library itself must avoid the direct exchange's
+    # device-side waits (a wait queued in front of the expand it waits for), so the check completes
+    # on the collective exchange with exact counts and no timeout.
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, GPU_MAX_HW_QUEUES="4", SR_HEAD_MAX="0", SR_PEER_TIMEOUT_MS="5000")
+    r = subprocess.run([sys.executable, "-c", _QUEUE_SCRIPT.format(root=root)], capture_output=True, text=True,
+                       timeout=240, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rows = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("[")][-1])
+    o = oracle(TWO_PHASE, [7])
+    for unique, states, depth, pipelined in rows:
+        assert (unique, states, depth) == (o.unique_state_count, o.state_count, o.max_depth)
+        assert pipelined == 1

@@ -32,7 +32,7 @@ CASES = [
     (LINEAR_EQUATION, [1, 1, 0]),
     (BINARY_CLOCK, []),
 ] + [(TWO_PHASE, [n]) for n in range(1, 8)] + [
-    (INCREMENT, [n]) for n in (1, 2, 3, 4, 6, 8, 9, 10, 12)
+    (INCREMENT, [n]) for n in (1, 2, 3, 4, 6, 8, 9, 10, 11, 12)
 ] + [(INCREMENT_LOCK, [n]) for n in (1, 2, 3, 5, 7, 8, 9)] + [(PAXOS, [1]), (PAXOS, [2])]
 
 

@@ -56,6 +56,20 @@ def test_processes_match_oracle(direct):
             assert r["pipelined"] == (2 if direct == "1" else 1)
 
 
+def test_processes_corrupt_slot_falls_back():
+    # A received record flipped AFTER its source checksummed it (rank 0's owner slots, level 2): the
+    # owner's insert reports it, every rank votes, and the check is redone on the collective
+    # exchange with the oracle's counts. The communicator keeps the collective exchange afterwards.
+    checks = ["2pc:6", "2pc:5"]
+    outs = run_ranks(checks, env={"SR_HEAD_MAX": "0", "SR_DX_CORRUPT_LEVEL": "2"})
+    for rank_out in outs:
+        first, second = rank_out
+        for r in rank_out:
+            assert (r["unique"], r["states"], r["depth"], r["discoveries"]) == expect(r["check"])
+        assert first["exchange_fallbacks"] == 1 and first["pipelined"] == 1
+        assert second["exchange_fallbacks"] == 0 and second["pipelined"] == 1
+
+
 def test_processes_bench_config_with_head():
     # the bench's configuration (2pc N=9, replicated head, then partitioned levels), twice
     n = 9
