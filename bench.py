@@ -316,7 +316,7 @@ def main():
     n = args.rm_count
     if args.model == "paxos":
         make = lambda: Paxos(args.clients)  # noqa: E731
-        expect_unique = {1: 265, 2: 16_668, 3: 1_194_428}[args.clients]
+        expect_unique = {1: 265, 2: 16_668, 3: 1_194_428, 4: 2_372_188, 5: 4_711_569, 6: 9_357_525}[args.clients]
         label = f"paxos C={args.clients}"
     elif args.model == "increment_lock":
         t = args.threads

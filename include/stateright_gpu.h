@@ -56,7 +56,7 @@ enum sr_model_id {
     SR_MODEL_INCREMENT = 4,       /* (threads<=15)  examples/increment.rs:109-197       */
     SR_MODEL_INCREMENT_LOCK = 5,  /* (threads<=12)  examples/increment_lock.rs:3-107    */
     SR_MODEL_DGRAPH = 6,          /* (expectation, len, v.., len, v..) src/test_util.rs:47-116 */
-    SR_MODEL_PAXOS = 7,           /* (client_count<=3) examples/paxos.rs:93-263 + src/actor/model.rs */
+    SR_MODEL_PAXOS = 7,           /* (client_count<=6) examples/paxos.rs:93-263 + src/actor/model.rs */
     /* ActorModel fixtures (src/actor/model.rs:176-327 over stateright_amd/csrc/actor.hpp): */
     SR_MODEL_PINGPONG = 9,        /* (max_nat<=7, lossy, duplicating, maintains_history)
                                      src/actor/actor_test_util.rs:4-96                     */

@@ -1267,8 +1267,8 @@ class DistEngine final : public EngineBase {
             p.last = HostCounters{};
             p.lstart.assign(1, 0);
             ensure_arena(p, (per_part + per_part / 8 + 4096) * grow_factor_, 0);
-            p.sendc.alloc(o_.device, T_);
-            SR_HIP(hipMemsetAsync(p.sendc.p, 0, T_ * 4, stream_));
+            p.sendc.alloc(o_.device, (size_t)T_ * SENDC_STRIDE);
+            SR_HIP(hipMemsetAsync(p.sendc.p, 0, (size_t)T_ * SENDC_STRIDE * 4, stream_));
             // sent cache: with few partitions a sender generates each remote state several times
             // per level (in-degree / T), and every copy would cross the link
             p.sent_mask = 0;
@@ -1356,7 +1356,7 @@ class DistEngine final : public EngineBase {
                 route<<<grid, 256, route_lds(), stream_>>>(
                     m_, p.arena.p, p.apar.p, nb, p.arena_cap, p.view(), p.id, T_, p.send.p, (u32)p.bucket_cap,
                     p.sendc.p, p.lc, p.ctl, undiscovered, row, ppw_log2, filt_log2_, p.bucket_cap * REC, 0u,
-                    p.sent_mask ? p.sent.p : nullptr, p.sent_mask, rstage_recs(), nullptr, nullptr, 0u, rflags(), nullptr);
+                    p.sent_mask ? p.sent.p : nullptr, p.sent_mask, rstage_recs(), nullptr, nullptr, 0u, rflags(), nullptr, 0u);
                 SR_HIP(hipGetLastError());
                 if (o_.profile) SR_HIP(hipEventRecord(event(2 * stats.expand_launches + 1), stream_));
                 stats.expand_launches++;
@@ -1662,7 +1662,8 @@ class DistEngine final : public EngineBase {
                 m_, p.arena.p, p.apar.p, 0, p.arena_cap, p.view(), p.id, T_, direct_ ? nullptr : p.send.p + DIST_HDR,
                 (u32)C, p.sendc.p, p.lc, p.ctl, undiscovered, row, ppw_log2, filt_log2_, S, 1u,
                 p.sent_mask ? p.sent.p : nullptr, p.sent_mask, rstage_recs(), direct_ ? ctx_->parts[p.res].ptab[par].p : nullptr,
-                dflags_ ? ctx_->dx.ftab.p : nullptr, fseq, rflags(), dcheck() ? ctx_->parts[p.res].dsum.p : nullptr);
+                dflags_ ? ctx_->dx.ftab.p : nullptr, fseq, rflags(), dcheck() ? ctx_->parts[p.res].dsum.p : nullptr,
+                flush_at(ppw_log2));
             SR_HIP(hipGetLastError());
             if (o_.profile) SR_HIP(hipEventRecord(event(2 * stats.expand_launches + 1), stream_));
             stats.expand_launches++;
@@ -2222,6 +2223,14 @@ class DistEngine final : public EngineBase {
             while (l > 2 && 4.0 * (double)(1u << l) * lnew_ratio_ * 1.3 > (double)route_local_stage(T_, W, rflags())) --l;
         return l;
     }
+    // expand_route's flush thresholds for parents per wave 2^l: a stage is flushed once its fill
+    // exceeds its size minus a chunk's bound (the bound ppw_for sized the chunk by)
+    u32 flush_at(u32 l) const {
+        const double chunk = 4.0 * (double)(1u << l) * 1.3;
+        const double rs = (double)rstage_recs(), ls = (double)route_local_stage(T_, W, rflags());
+        const u32 fr = (u32)std::max(0.0, rs - chunk * rec_ratio_), fl = (u32)std::max(0.0, ls - chunk * lnew_ratio_);
+        return std::min<u32>(fl, 0xffffu) << 16 | std::min<u32>(fr, 0xffffu);
+    }
     double rec_ratio_ = 4.0;   // remote records per parent, last level
     double lnew_ratio_ = 2.0;  // new states claimed in place per parent, last level
     // Records staged per chunk in LDS (none with one partition), and expand_route's dynamic LDS.
@@ -2278,8 +2287,7 @@ class DistEngine final : public EngineBase {
     // chunk of 4 x 32 parents then fits: 2pc N=11 at T = 8 routes in 41 instead of 69 ms per check)
     // (0 = that default; SR_RSTAGE_WORDS overrides)
     u32 rstage_words_ = std::getenv("SR_RSTAGE_WORDS") ? (u32)std::atoi(std::getenv("SR_RSTAGE_WORDS")) : 0u;
-    // (with an owner key most successors are local: a small record stage leaves LDS for residency)
-    u32 rstage_words() const { return rstage_words_ ? rstage_words_ : self_rec() ? 2048u : okey_ ? 256u : 1024u; }
+    u32 rstage_words() const { return rstage_words_ ? rstage_words_ : self_rec() ? 2048u : 1024u; }
     int route_ppw_env_ = std::getenv("SR_ROUTE_PPW_LOG2") ? std::atoi(std::getenv("SR_ROUTE_PPW_LOG2")) : -1;
     bool trace_ = std::getenv("SR_DIST_TRACE") != nullptr;
     Clock::time_point t_trace_ = Clock::now();

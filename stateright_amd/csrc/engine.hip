@@ -56,8 +56,9 @@ static std::unique_ptr<EngineBase> make_model_engine(int model, const i64* p, in
             return std::make_unique<E<IncrementLock<2>>>(IncrementLock<2>{(int)p[0]}, o, args...);
         case SR_MODEL_PAXOS:
             need(1);
-            if (p[0] < 1 || p[0] > 3) throw Error(SR_ERR_UNSUPPORTED, "paxos: client_count must be in 1..=3");
-            return std::make_unique<E<Paxos>>(Paxos::make((int)p[0], o.device), o, args...);
+            if (p[0] < 1 || p[0] > px::MAX_CLIENTS) throw Error(SR_ERR_UNSUPPORTED, "paxos: client_count must be in 1..=6");
+            if (p[0] <= Paxos::max_clients()) return std::make_unique<E<Paxos>>(Paxos::make((int)p[0]), o, args...);
+            return std::make_unique<E<PaxosWide>>(PaxosWide::make((int)p[0]), o, args...);
         case SR_MODEL_DGRAPH:
             return std::make_unique<E<DGraph>>(DGraph::make(p, np, o.device), o, args...);
         case SR_MODEL_PINGPONG: {

@@ -19,6 +19,10 @@
 namespace sr {
 
 constexpr int GID_SHIFT = 40;
+// expand_route's per-owner record counters, one 128-byte line each (u32 stride): every workgroup
+// reserves its span of each owner's slot with a returning atomic, and atomics to one line
+// serialise at ~11 ns apiece whatever the addresses inside it (kernels.hpp LevelCounters).
+constexpr u32 SENDC_STRIDE = 32;
 constexpr u64 PAR_SEARCH = ~0ull - 1;  // parent not recorded: search the previous level
 
 // Owner partition of a fingerprint: the high 32 bits scaled to [0, T) (any T, uniform).
@@ -178,7 +182,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W <
                                                     u32 ppw_log2, u32 filt_log2, u64 bucket_stride, u32 lag,
                                                     u64* __restrict__ sent, u64 sent_mask, u32 rs,
                                                     u64* const* ptab, u32* const* ftab, u32 fseq, u32 rflags,
-                                                    u64* dsum) {
+                                                    u64* dsum, u32 flush_at) {
     // dsum (direct exchange): [NSHARD][MAX_PARTS] per-owner sums of the record words this launch
     // stores, accumulated per chunk flush into shard blockIdx % NSHARD (non-returning atomics, spread
     // like the statistics); the last workgroup folds them into each owner's slot checksum (HDR_SUM).
@@ -237,6 +241,61 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W <
     for (u32 q = threadIdx.x; q < nparts; q += blockDim.x) ocnt[q] = 0, ocsum[q] = 0;
     for (u32 i = threadIdx.x; i < (fmask ? fmask + 1 : 0u); i += blockDim.x) filt[i] = 0;
     u64* const my_dsum = dsum ? dsum + (u64)(blockIdx.x % NSHARD) * MAX_PARTS : nullptr;
+
+    // Block flush of the stages (every thread; fl / fr uniform): local new states get ONE claims
+    // reservation, records are counting-sorted by owner and get one reservation per owner.
+    auto flush = [&](bool fl, bool fr) {
+        const u32 nl = fl ? min(stage_n, (u32)STAGE) : 0u;
+        const u32 nr = fr ? min(rstage_n, RSTAGE) : 0u;
+        if (nr && threadIdx.x == 0) sent_any = 1;
+        for (u32 i = threadIdx.x; i < nr; i += blockDim.x) {
+            rrank[i] = (u16)atomicAdd(&ocnt[rown[i]], 1u);
+            if (my_dsum) {
+                u64 v = 0;
+#pragma unroll
+                for (int x = 0; x < REC; ++x) v += rstage[i * REC + x];
+                atomicAdd(reinterpret_cast<unsigned long long*>(&ocsum[rown[i]]), (unsigned long long)v);
+            }
+        }
+        if (threadIdx.x == 0 && nl) base = atomicAdd(&lc->claims, nl);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            if (fl) stage_n = 0;
+            if (fr) rstage_n = 0;
+        }
+        if (nr)
+            for (u32 q = threadIdx.x; q < nparts; q += blockDim.x) {
+                const u32 c = ocnt[q];
+                obase[q] = c ? atomicAdd(&send_counts[q * SENDC_STRIDE], c) : 0;
+                ocnt[q] = 0;
+                if (my_dsum && c) {
+                    atomicAdd(reinterpret_cast<unsigned long long*>(&my_dsum[q]), (unsigned long long)ocsum[q]);
+                    ocsum[q] = 0;
+                }
+            }
+        for (u32 i = threadIdx.x; i < nl; i += blockDim.x) {
+            const u32 pos = base + i;
+            u64 ns[W];
+#pragma unroll
+            for (int x = 0; x < W; ++x) ns[x] = stage[i * W + x];
+            if (pos < next_cap) {
+                store_state<W>(next, pos, ns);
+                next_par[pos] = gid_base + stage_par[i];
+            } else {
+                atomicOr(&lc->err, (u32)ERR_FRONTIER_OVERFLOW);
+            }
+            eval_props(m, ns, pos, undiscovered, lc);
+        }
+        __syncthreads();
+        for (u32 i = threadIdx.x; i < nr * REC; i += blockDim.x) {
+            const u32 rr = i / REC, x = i - rr * REC;
+            const u32 q = rown[rr];
+            const u32 pos = obase[q] + rrank[rr];
+            if (pos < bucket_cap) sdst[q][(u64)pos * REC + x] = rstage[rr * REC + x];
+            else if (x == 0) atomicOr(&lc->err, (u32)ERR_FRONTIER_OVERFLOW);
+        }
+        __syncthreads();  // the stages are read before any later append
+    };
 
     u32 succ = 0, enabled = 0;
     const u64 chunk = (u64)(blockDim.x >> 6) * ppw;
@@ -422,7 +481,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W <
                     const u64 qm = __ballot(mine);
                     om &= ~qm;
                     u32 gb = 0;
-                    if (lane == leader) gb = atomicAdd(&send_counts[q], (u32)__popcll(qm));
+                    if (lane == leader) gb = atomicAdd(&send_counts[q * SENDC_STRIDE], (u32)__popcll(qm));
                     gb = __shfl(gb, leader, 64);
                     if (mine) {
                         const u32 pos = gb + __popcll(qm & lanes_below);
@@ -443,54 +502,17 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W <
         wave_lds_sync();  // the window's map is read before the next window overwrites it
         }
 
-        // ---- block flush of the chunk's stages ----
+        // ---- the stages persist across the block's chunks: a stage is flushed (by the whole
+        // block) once it could not hold another chunk's output, flush_at = (local fill << 16 |
+        // record fill) thresholds from the host's per-chunk bound (ppw_for sizes a chunk to fit a
+        // whole stage). With few records per chunk (an owner key) a flush, its claims reservation
+        // and its reservation per owner are shared by several chunks ----
         __syncthreads();
-        const u32 nl = min(stage_n, (u32)STAGE);
-        const u32 nr = min(rstage_n, RSTAGE);
-        if (nr && threadIdx.x == 0) sent_any = 1;
-        for (u32 i = threadIdx.x; i < nr; i += blockDim.x) {
-            rrank[i] = (u16)atomicAdd(&ocnt[rown[i]], 1u);
-            if (my_dsum) {
-                u64 v = 0;
-#pragma unroll
-                for (int x = 0; x < REC; ++x) v += rstage[i * REC + x];
-                atomicAdd(reinterpret_cast<unsigned long long*>(&ocsum[rown[i]]), (unsigned long long)v);
-            }
-        }
-        if (threadIdx.x == 0 && nl) base = atomicAdd(&lc->claims, nl);
-        __syncthreads();
-        if (threadIdx.x == 0) stage_n = rstage_n = 0;
-        for (u32 q = threadIdx.x; q < nparts; q += blockDim.x) {
-            const u32 c = ocnt[q];
-            obase[q] = c ? atomicAdd(&send_counts[q], c) : 0;
-            ocnt[q] = 0;
-            if (my_dsum && c) {
-                atomicAdd(reinterpret_cast<unsigned long long*>(&my_dsum[q]), (unsigned long long)ocsum[q]);
-                ocsum[q] = 0;
-            }
-        }
-        for (u32 i = threadIdx.x; i < nl; i += blockDim.x) {
-            const u32 pos = base + i;
-            u64 ns[W];
-#pragma unroll
-            for (int x = 0; x < W; ++x) ns[x] = stage[i * W + x];
-            if (pos < next_cap) {
-                store_state<W>(next, pos, ns);
-                next_par[pos] = gid_base + stage_par[i];
-            } else {
-                atomicOr(&lc->err, (u32)ERR_FRONTIER_OVERFLOW);
-            }
-            eval_props(m, ns, pos, undiscovered, lc);
-        }
-        __syncthreads();
-        for (u32 i = threadIdx.x; i < nr * REC; i += blockDim.x) {
-            const u32 rr = i / REC, x = i - rr * REC;
-            const u32 q = rown[rr];
-            const u32 pos = obase[q] + rrank[rr];
-            if (pos < bucket_cap) sdst[q][(u64)pos * REC + x] = rstage[rr * REC + x];
-            else if (x == 0) atomicOr(&lc->err, (u32)ERR_FRONTIER_OVERFLOW);
-        }
+        const bool fl = stage_n > (flush_at >> 16), fr = rstage_n > (flush_at & 0xffffu);
+        if (fl || fr) flush(fl, fr);
     }
+    __syncthreads();
+    flush(true, true);
     u32 total_succ = block_sum(succ, scratch);
     u32 total_enabled = block_sum(enabled, scratch);
     if (threadIdx.x == 0) add_stats(lc, total_succ, total_enabled);
@@ -519,7 +541,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W <
     const u32 rw = nparts + 6 + M::NPROPS;
     for (u32 w = threadIdx.x; w < rw; w += blockDim.x) {
         const u32 f = w - nparts;  // row fields after the per-destination counts
-        const u32* src = w < nparts ? send_counts + w
+        const u32* src = w < nparts ? send_counts + w * SENDC_STRIDE
                          : f == 2   ? &lc->claims
                          : f == 3   ? &lc->err
                          : f == 5   ? &ctl->roots
@@ -531,7 +553,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W <
         row[w] = v;
     }
     __syncthreads();
-    for (u32 q = threadIdx.x; q < nparts; q += blockDim.x) send_counts[q] = 0;  // for the next level
+    for (u32 q = threadIdx.x; q < nparts; q += blockDim.x) send_counts[q * SENDC_STRIDE] = 0;  // for the next level
     if (lag)  // the row travels in the header of every bucket (and so reaches every rank)
         for (u32 i = threadIdx.x; i < nparts * rw; i += blockDim.x) {
             const u32 q = i / rw, w = i - q * rw;

@@ -4,26 +4,31 @@
 // (src/actor/register.rs:119-217) + PaxosActor (examples/paxos.rs:93-221) + a
 // LinearizabilityTester<Id, Register<char>> history (src/semantics/linearizability.rs:57-241).
 // Its per-state heap objects (Arc'd actor states, a HashSet network, BTreeMap histories) become
-// W = 11 words:
+// W = 11 words, for any client count C <= 6 (the reference's bench.sh runs `paxos check 6`):
 //
-//   word 0   server 0 (42 bits) | 3 client phases (2 bits each) | history index (16 bits)
-//   word 1   server 1           word 2   server 2
-//   words 3+ the network: 16 envelope codes (u32, ascending, unused = 0xffffffff)
+//   word 0   server 0 (47 bits) | history index (16 bits, from bit 48)
+//   word 1   server 1 (47 bits) | C client phases (2 bits each, from bit 48)
+//   word 2   server 2
+//   words 3+ the network: 16 envelope codes (u32, ascending, unused = 0xffffffff); at most 13,
+//            14 and 16 envelopes are ever in flight at C = 3, 4 and 6
 //
 // A server is PaxosState (examples/paxos.rs:78-91) in bit fields:
-//   [0,4) ballot (round << 2 | id)   [4,7) proposal (requester id 3..5, 0 = None)
-//   [7,31) prepares[j] (present << 7 | acc)   [31,34) accepts mask   [34,41) accepted acc
-//   [41] is_decided
-// with acc = Option<(Ballot, Proposal)> as some << 6 | ballot << 2 | (requester - 3). Every
+//   [0,4) ballot (round << 2 | id)   [4,8) proposal (requester id 3..8, 0 = None)
+//   [8,35) prepares[j] (present << 8 | acc)   [35,38) accepts mask   [38,46) accepted acc
+//   [46] is_decided
+// with acc = Option<(Ballot, Proposal)> as some << 7 | ballot << 3 | (requester - 3). Every
 // field is ORDER-PRESERVING, so comparing codes compares the reference's values. Ballot rounds
-// fit 2 bits: a round is raised only when a server takes a Put (examples/paxos.rs:128-140), each
-// server takes at most one (its proposal is never reset) and there are C <= 3 Puts.
+// fit 2 bits: a round is raised only when a server takes a Put (examples/paxos.rs:128-140), and
+// each of the 3 servers takes at most one (its proposal is never reset).
 //
-// An envelope code is src | dst | kind | ballot | last_accepted | proposal | request | value
-// (MSB first, 30 bits) — the lexicographic order of the reference's Envelope fields — so the
-// sorted code list is the network SET (src/actor/model.rs:69, non-duplicating) and action slot k
-// (deliver the k-th envelope) enumerates `actions()` in the same order as the CPU oracle's
-// ordered set.
+// An envelope code is src | dst | kind | ballot | payload (MSB first, 24 bits) — the
+// lexicographic order of the reference's Envelope fields: the payload is the one message field
+// that varies for a given (src, dst, kind, ballot): last_accepted (Prepared), the proposal's
+// requester (Accept, Decided: its request id and value are the requester's) or the value
+// (GetOk); a request id is always the client's own (Put/PutOk: its id, Get/GetOk: twice its id,
+// src/actor/register.rs:130-200), and a Put's value is the client's letter. So the sorted code
+// list is the network SET (src/actor/model.rs:69, non-duplicating) and action slot k (deliver the
+// k-th envelope) enumerates `actions()` in the same order as the CPU oracle's ordered set.
 //
 // Histories change only on client deliveries (record_returns / record_invocations,
 // src/actor/register.rs:37-87); the reachable ones are interned on the host by a closure over
@@ -46,40 +51,50 @@ namespace sr {
 namespace px {
 
 enum Kind : u32 { PREPARE, PREPARED, ACCEPT, ACCEPTED, DECIDED, PUT, GET, PUTOK, GETOK };
-constexpr int SLOTS = 16;          // network capacity (the reachable maximum is 13 at C = 3)
+constexpr int SLOTS = 16;          // network capacity (the reachable maximum is 16 at C = 6)
+constexpr int MAX_CLIENTS = 6;
 constexpr u32 EMPTY = 0xffffffffu;
-constexpr int SBITS = 42;          // bits per server
-constexpr int NEV_PER_CLIENT = 5;  // PutOk, GetOk('\0'), GetOk('A'..'C')
+constexpr int SBITS = 47;          // bits per server
+constexpr u64 SMASK = (1ull << SBITS) - 1;
+constexpr int HIST_SHIFT = 48;     // word 0: history index
+constexpr int PHASE_SHIFT = 48;    // word 1: client phases
+// History events per client: PutOk, GetOk('\0'), GetOk('A' + v - 1) for v = 1..MAX_CLIENTS.
+constexpr int NEV_PER_CLIENT = 2 + MAX_CLIENTS;
 
-SR_HD u32 env(u32 src, u32 dst, u32 kind, u32 bal, u32 acc, u32 pcl, u32 req, u32 val) {
-    return src << 27 | dst << 24 | kind << 20 | bal << 16 | acc << 9 | pcl << 6 | req << 2 | val;
+// payload: acc (Prepared), requester id (Accept, Decided), value (GetOk), else 0
+SR_HD u32 env(u32 src, u32 dst, u32 kind, u32 bal, u32 payload) {
+    return src << 20 | dst << 16 | kind << 12 | bal << 8 | payload;
 }
-SR_HD u32 e_src(u32 e) { return e >> 27 & 7; }
-SR_HD u32 e_dst(u32 e) { return e >> 24 & 7; }
-SR_HD u32 e_kind(u32 e) { return e >> 20 & 15; }
-SR_HD u32 e_bal(u32 e) { return e >> 16 & 15; }
-SR_HD u32 e_acc(u32 e) { return e >> 9 & 127; }
-SR_HD u32 e_pcl(u32 e) { return e >> 6 & 7; }
-SR_HD u32 e_req(u32 e) { return e >> 2 & 15; }
-SR_HD u32 e_val(u32 e) { return e & 3; }
+SR_HD u32 e_src(u32 e) { return e >> 20 & 15; }
+SR_HD u32 e_dst(u32 e) { return e >> 16 & 15; }
+SR_HD u32 e_kind(u32 e) { return e >> 12 & 15; }
+SR_HD u32 e_bal(u32 e) { return e >> 8 & 15; }
+SR_HD u32 e_acc(u32 e) { return e & 255; }
+SR_HD u32 e_pcl(u32 e) { return e & 15; }
+SR_HD u32 e_val(u32 e) { return e & 7; }
+// request ids are the client's: Put/PutOk carry its id, Get/GetOk twice its id
+SR_HD u32 e_req(u32 e) {
+    const u32 k = e_kind(e), client = k == PUT || k == GET ? e_src(e) : e_dst(e);  // Put, Get: from the client
+    return k == GET || k == GETOK ? 2 * client : client;
+}
 
 struct Srv {
     u32 bal, prop, prep[3], accepts, accepted, decided;
     SR_HD static Srv load(u64 w) {
         Srv s;
         s.bal = (u32)(w & 15);
-        s.prop = (u32)(w >> 4 & 7);
+        s.prop = (u32)(w >> 4 & 15);
 #pragma unroll
-        for (int j = 0; j < 3; ++j) s.prep[j] = (u32)(w >> (7 + 8 * j) & 255);
-        s.accepts = (u32)(w >> 31 & 7);
-        s.accepted = (u32)(w >> 34 & 127);
-        s.decided = (u32)(w >> 41 & 1);
+        for (int j = 0; j < 3; ++j) s.prep[j] = (u32)(w >> (8 + 9 * j) & 511);
+        s.accepts = (u32)(w >> 35 & 7);
+        s.accepted = (u32)(w >> 38 & 255);
+        s.decided = (u32)(w >> 46 & 1);
         return s;
     }
     SR_HD u64 store() const {
-        u64 w = bal | (u64)prop << 4 | (u64)accepts << 31 | (u64)accepted << 34 | (u64)decided << 41;
+        u64 w = bal | (u64)prop << 4 | (u64)accepts << 35 | (u64)accepted << 38 | (u64)decided << 46;
 #pragma unroll
-        for (int j = 0; j < 3; ++j) w |= (u64)prep[j] << (7 + 8 * j);
+        for (int j = 0; j < 3; ++j) w |= (u64)prep[j] << (8 + 9 * j);
         return w;
     }
 };
@@ -90,7 +105,7 @@ SR_HD bool server_on_msg(u32 id, Srv& s, u32 e, u32* out, int& n) {
     const u32 src = e_src(e), kind = e_kind(e), bal = e_bal(e);
     const u32 p0 = id == 0 ? 1 : 0, p1 = id == 2 ? 1 : 2;  // peers, ascending
     if (s.decided) {
-        if (kind == GET) out[n++] = env(id, src, GETOK, 0, 0, 0, e_req(e), (s.accepted & 3) + 1);
+        if (kind == GET) out[n++] = env(id, src, GETOK, 0, (s.accepted & 7) + 1);
         return false;
     }
     switch (kind) {
@@ -100,53 +115,53 @@ SR_HD bool server_on_msg(u32 id, Srv& s, u32 e, u32* out, int& n) {
             s.accepts = 0;
             s.bal = ((s.bal >> 2) + 1) << 2 | id;
 #pragma unroll
-            for (int j = 0; j < 3; ++j) s.prep[j] = (u32)j == id ? (128u | s.accepted) : 0u;
-            out[n++] = env(id, p0, PREPARE, s.bal, 0, 0, 0, 0);
-            out[n++] = env(id, p1, PREPARE, s.bal, 0, 0, 0, 0);
+            for (int j = 0; j < 3; ++j) s.prep[j] = (u32)j == id ? (256u | s.accepted) : 0u;
+            out[n++] = env(id, p0, PREPARE, s.bal, 0);
+            out[n++] = env(id, p1, PREPARE, s.bal, 0);
             return true;
         case PREPARE:
             if (!(s.bal < bal)) return false;
             s.bal = bal;
-            out[n++] = env(id, src, PREPARED, bal, s.accepted, 0, 0, 0);
+            out[n++] = env(id, src, PREPARED, bal, s.accepted);
             return true;
         case PREPARED: {
             if (bal != s.bal) return false;
             u32 cnt = 0, best = 0;
 #pragma unroll
             for (int j = 0; j < 3; ++j) {
-                if ((u32)j == src) s.prep[j] = 128u | e_acc(e);
-                cnt += s.prep[j] >> 7;
-                if ((s.prep[j] >> 7) && (s.prep[j] & 127) > best) best = s.prep[j] & 127;
+                if ((u32)j == src) s.prep[j] = 256u | e_acc(e);
+                cnt += s.prep[j] >> 8;
+                if ((s.prep[j] >> 8) && (s.prep[j] & 255) > best) best = s.prep[j] & 255;
             }
             if (cnt == 2) {  // majority(3) (src/actor.rs:437-439)
-                const u32 p = best ? (best & 3) + 3 : s.prop;
+                const u32 p = best ? (best & 7) + 3 : s.prop;
                 s.prop = p;
-                s.accepted = 64u | bal << 2 | (p - 3);
+                s.accepted = 128u | bal << 3 | (p - 3);
                 s.accepts |= 1u << id;
-                out[n++] = env(id, p0, ACCEPT, bal, 0, p, 0, 0);
-                out[n++] = env(id, p1, ACCEPT, bal, 0, p, 0, 0);
+                out[n++] = env(id, p0, ACCEPT, bal, p);
+                out[n++] = env(id, p1, ACCEPT, bal, p);
             }
             return true;
         }
         case ACCEPT:
             if (bal < s.bal) return false;
             s.bal = bal;
-            s.accepted = 64u | bal << 2 | (e_pcl(e) - 3);
-            out[n++] = env(id, src, ACCEPTED, bal, 0, 0, 0, 0);
+            s.accepted = 128u | bal << 3 | (e_pcl(e) - 3);
+            out[n++] = env(id, src, ACCEPTED, bal, 0);
             return true;
         case ACCEPTED:
             if (bal != s.bal) return false;
             s.accepts |= 1u << src;
             if (__builtin_popcount(s.accepts) == 2) {
                 s.decided = 1;
-                out[n++] = env(id, p0, DECIDED, bal, 0, s.prop, 0, 0);
-                out[n++] = env(id, p1, DECIDED, bal, 0, s.prop, 0, 0);
-                out[n++] = env(id, s.prop, PUTOK, 0, 0, 0, s.prop, 0);  // request id = requester (put_count 1)
+                out[n++] = env(id, p0, DECIDED, bal, s.prop);
+                out[n++] = env(id, p1, DECIDED, bal, s.prop);
+                out[n++] = env(id, s.prop, PUTOK, 0, 0);  // request id = requester (put_count 1)
             }
             return true;
         case DECIDED:
             s.bal = bal;
-            s.accepted = 64u | bal << 2 | (e_pcl(e) - 3);
+            s.accepted = 128u | bal << 3 | (e_pcl(e) - 3);
             s.decided = 1;
             return true;
         default:
@@ -156,8 +171,8 @@ SR_HD bool server_on_msg(u32 id, Srv& s, u32 e, u32* out, int& n) {
 
 // Canonical forms shared with the CPU oracle (oracle/paxos.hpp acc_code / envelope_code).
 inline i64 acc_code(u32 acc) {
-    if (!(acc & 64)) return 0;
-    return 1 + (i64)(acc >> 4 & 3) * 64 + (i64)(acc >> 2 & 3) * 8 + (i64)(acc & 3) + 3;
+    if (!(acc & 128)) return 0;
+    return 1 + (i64)(acc >> 5 & 3) * 64 + (i64)(acc >> 3 & 3) * 8 + (i64)(acc & 7) + 3;
 }
 inline i64 env_code(u32 e) {
     const u32 kind = e_kind(e);
@@ -271,7 +286,7 @@ struct Tables {
 };
 
 inline Tables compile(int C) {
-    if (C < 1 || C > 3) throw Error(SR_ERR_UNSUPPORTED, "paxos: client_count must be in 1..=3");
+    if (C < 1 || C > MAX_CLIENTS) throw Error(SR_ERR_UNSUPPORTED, "paxos: client_count must be in 1..=6");
     Tables T;
     T.C = C;
     T.nev = C * NEV_PER_CLIENT;
@@ -294,8 +309,9 @@ inline Tables compile(int C) {
         for (int ev = 0; ev < T.nev; ++ev) {
             const int c = ev / NEV_PER_CLIENT, kind = ev % NEV_PER_CLIENT;
             // a client's completed-op count is its phase: PutOk is delivered in phase 0 only,
-            // GetOk in phase 1 only (RegisterActor client, src/actor/register.rs:170-200)
-            if ((int)H[k].done[c].size() != (kind == 0 ? 0 : 1)) continue;
+            // GetOk in phase 1 only (RegisterActor client, src/actor/register.rs:170-200); a
+            // GetOk carries no value or one of the C clients' letters
+            if ((int)H[k].done[c].size() != (kind == 0 ? 0 : 1) || kind > 1 + C) continue;
             Hist h = H[k];
             if (kind == 0) {
                 h.ret(c, true, 0);                // PutOk: return WriteOk ...
@@ -344,65 +360,178 @@ inline Tables& tables(int C, int device) {
 
 }  // namespace px
 
-struct Paxos {
-    static constexpr int W = 3 + px::SLOTS / 2, MW = 1, NPROPS = 2;
-    int C = 2;
-    int nev = 0;
-    u32 init_hist = 0;
-    const u16* h_next_d = nullptr;  // device tables
-    const u8* h_lin_d = nullptr;
-    const u16* h_next_h = nullptr;  // host tables (paths, replay)
-    const u8* h_lin_h = nullptr;
-
-    // device < 0: host-only (no device copy of the tables)
-    static Paxos make(int C, int device) {
-        px::Tables& t = px::tables(C, device);
-        Paxos m;
-        m.C = C;
-        m.nev = t.nev;
-        m.init_hist = t.init_hist;
-        if (device >= 0) {
-            m.h_next_d = t.dev.at(device).first;
-            m.h_lin_d = t.dev.at(device).second;
+// The history of LinearizabilityTester<Id, Register<char>> (src/semantics/linearizability.rs:
+// 57-241) under this protocol, stored in the state: client t invokes its Put at init (its `last`
+// vector all -1: nothing has completed), receives PutOk (phase 0 -> 1) and at once invokes its Get,
+// whose `last` vector records how many ops of every other client had completed then (that
+// client's phase: 0, 1 or 2), and receives GetOk(v) (phase 1 -> 2). Per client: phase (2 bits) |
+// Get's returned value (3 bits: 0 = '\0', v = the v-th client's letter) | the Get's `last` entries
+// for the other clients in ascending id (2 bits each). The field is a FUNCTION of the reference's
+// tester state (equal states <=> equal words still holds), so nothing is precomputed per history
+// and any client count fits; `linearizable` runs the tester's serialization search on it.
+struct PaxosHist {
+    u32 C = 2;
+    SR_HD u32 fb() const { return 5 + 2 * (C - 1); }  // bits per client
+    SR_HD static u32 get(u64 lo, u64 hi, u32 off, u32 w) {
+        const u64 v = off >= 64 ? hi >> (off - 64) : (lo >> off) | (off + w > 64 && off ? hi << (64 - off) : 0);
+        return (u32)(v & ((1ull << w) - 1));
+    }
+    SR_HD static void put(u64& lo, u64& hi, u32 off, u32 w, u64 v) {
+        const u64 m = (1ull << w) - 1;
+        if (off >= 64) {
+            hi = (hi & ~(m << (off - 64))) | (v & m) << (off - 64);
+            return;
         }
-        m.h_next_h = t.h_next.data();
-        m.h_lin_h = t.h_lin.data();
+        lo = (lo & ~(m << off)) | (v & m) << off;
+        if (off + w > 64) {
+            const u32 k = 64 - off;  // bits in lo
+            hi = (hi & ~(m >> k)) | (v & m) >> k;
+        }
+    }
+    SR_HD u32 phase(u64 lo, u64 hi, u32 c) const { return get(lo, hi, c * fb(), 2); }
+    SR_HD u32 ret(u64 lo, u64 hi, u32 c) const { return get(lo, hi, c * fb() + 2, 3); }
+    // completed-op count of client u when client t invoked its Get
+    SR_HD u32 last(u64 lo, u64 hi, u32 t, u32 u) const { return get(lo, hi, t * fb() + 5 + 2 * (u < t ? u : u - 1), 2); }
+
+    // LinearizabilityTester::serialized_history().is_some() (linearizability.rs:159-240; the host
+    // restatement is px::Hist::serialize): a depth-first search for an order of every completed
+    // op (and any subset of the in-flight ones) that respects real time and the register. Ops of
+    // client t: 0 = Write(t's letter) (completed from phase 1, with no real-time predecessor),
+    // 1 = Read (in flight in phase 1 with predecessors from `last`, completed in phase 2). Threads
+    // are tried in id order, completed ops before an in-flight one, as the reference does.
+    SR_HD bool linearizable(u64 lo, u64 hi) const {
+        // No completed Read: the completed ops are Writes invoked together at init, unordered in
+        // real time, and any order of them (in-flight ops left out) is a valid serialization.
+        bool any_read = false;
+        for (u32 t = 0; t < C; ++t) any_read |= phase(lo, hi, t) == 2;
+        if (!any_read) return true;
+        u32 done[MAXC], lastv[MAXC][MAXC], rv[MAXC];
+        for (u32 t = 0; t < C; ++t) {
+            done[t] = phase(lo, hi, t);
+            rv[t] = ret(lo, hi, t);
+            for (u32 u = 0; u < C; ++u) lastv[t][u] = u == t ? 0u : last(lo, hi, t, u);
+        }
+        u32 next[MAXC], used[MAXC];
+        for (u32 t = 0; t < C; ++t) next[t] = used[t] = 0;
+        // frames: thread, kind (0 completed op, 1 in-flight op), register before
+        u32 ft[2 * MAXC], fk[2 * MAXC], fr[2 * MAXC];
+        u32 depth = 0, reg = 0, t0 = 0;
+        // op (t, i) may be placed once every op that completed before its invocation is placed
+        auto violates = [&](u32 t, u32 i) {
+            if (i == 0) return false;  // a Put: invoked before anything completed
+            for (u32 u = 0; u < C; ++u)
+                if (u != t && next[u] < done[u] && next[u] < lastv[t][u]) return true;
+            return false;
+        };
+        for (int guard = 0; guard < 1 << 20; ++guard) {
+            bool all = true;
+            for (u32 t = 0; t < C; ++t) all &= next[t] == done[t];
+            if (all) return true;
+            bool found = false;
+            for (u32 t = t0; t < C && !found; ++t) {
+                if (next[t] == done[t]) {
+                    if (done[t] == 2 || used[t] || violates(t, done[t])) continue;  // in-flight op: index done[t]
+                    ft[depth] = t, fk[depth] = 1, fr[depth] = reg, ++depth;
+                    used[t] = 1;
+                    if (done[t] == 0) reg = t + 1;  // a Write takes effect; a Read returns anything
+                    found = true;
+                } else {
+                    const u32 i = next[t];
+                    next[t]++;
+                    const bool ok = !violates(t, i) && (i == 0 || rv[t] == reg);
+                    if (!ok) {
+                        next[t]--;
+                        continue;
+                    }
+                    ft[depth] = t, fk[depth] = 0, fr[depth] = reg, ++depth;
+                    if (i == 0) reg = t + 1;
+                    found = true;
+                }
+            }
+            if (found) {
+                t0 = 0;
+                continue;
+            }
+            if (depth == 0) return false;
+            --depth;
+            const u32 t = ft[depth];
+            if (fk[depth]) used[t] = 0;
+            else next[t]--;
+            reg = fr[depth];
+            t0 = t + 1;
+        }
+        return false;
+    }
+    static constexpr u32 MAXC = px::MAX_CLIENTS;
+};
+
+// W = 11 holds the history of up to 4 clients in the 3 x 17 bits the servers leave free; W = 12
+// adds a word for 5 or 6 clients. The history field's last bit (NOT_LIN_BIT) caches "the history
+// is not linearizable" (a function of the history, so still a function of the state): the search
+// runs when a client delivery changes the history, not for every new state's property check.
+template <int WW>
+struct PaxosT {
+    static constexpr int W = WW, MW = 1, NPROPS = 2;
+    static constexpr int NET0 = W - px::SLOTS / 2;  // first network word
+    static_assert(NET0 == 3 || NET0 == 4, "servers (+ one history word) then the network");
+    static constexpr u32 NOT_LIN_BIT = NET0 == 3 ? 50u : 114u;  // past the clients' fields (44 / 90 bits)
+    int C = 2;
+
+    static PaxosT make(int C) {
+        if (C < 1 || C > max_clients()) throw Error(SR_ERR_UNSUPPORTED, "paxos: client_count out of this encoding's range");
+        PaxosT m;
+        m.C = C;
         return m;
     }
-    SR_HD const u16* h_next() const {
-#if defined(__HIP_DEVICE_COMPILE__)
-        return h_next_d;
-#else
-        return h_next_h;
-#endif
+    static constexpr int max_clients() { return W == 11 ? 4 : px::MAX_CLIENTS; }
+    SR_HD PaxosHist hs() const {
+        PaxosHist h;
+        h.C = (u32)C;
+        return h;
     }
-    SR_HD const u8* h_lin() const {
-#if defined(__HIP_DEVICE_COMPILE__)
-        return h_lin_d;
-#else
-        return h_lin_h;
-#endif
+    // the history field: bits 47..63 of words 0, 1, 2 (then word 3 with W = 12)
+    SR_HD static void hist_get(const u64* s, u64& lo, u64& hi) {
+        constexpr u32 B = 64 - px::SBITS;  // 17
+        lo = (s[0] >> px::SBITS) | (s[1] >> px::SBITS) << B | (s[2] >> px::SBITS) << (2 * B);
+        hi = (s[2] >> px::SBITS) >> (64 - 2 * B);
+        if constexpr (NET0 == 4) {
+            lo |= s[3] << (3 * B);
+            hi |= s[3] >> (64 - 3 * B);
+        }
+    }
+    SR_HD static void hist_set(u64* s, u64 lo, u64 hi) {
+        constexpr u32 B = 64 - px::SBITS;
+        constexpr u64 M = (1ull << B) - 1;
+        s[0] = (s[0] & px::SMASK) | (lo & M) << px::SBITS;
+        s[1] = (s[1] & px::SMASK) | (lo >> B & M) << px::SBITS;
+        s[2] = (s[2] & px::SMASK) | ((lo >> (2 * B) | hi << (64 - 2 * B)) & M) << px::SBITS;
+        if constexpr (NET0 == 4) s[3] = lo >> (3 * B) | hi << (64 - 3 * B);
     }
 
     int max_actions() const { return px::SLOTS; }
     int max_out_degree() const { return px::SLOTS; }
-    SR_HD static u32 slot(const u64* s, int k) { return (u32)(s[3 + k / 2] >> (32 * (k & 1))); }
-    SR_HD static u32 hist(const u64* s) { return (u32)(s[0] >> 48); }
-    SR_HD static u32 phase(const u64* s, int c) { return (u32)(s[0] >> (px::SBITS + 2 * c) & 3); }
+    SR_HD static u32 slot(const u64* s, int k) { return (u32)(s[NET0 + k / 2] >> (32 * (k & 1))); }
+    SR_HD u32 phase(const u64* s, int c) const {
+        u64 lo, hi;
+        hist_get(s, lo, hi);
+        return hs().phase(lo, hi, (u32)c);
+    }
+    SR_HD static u64 server_word(const u64* s, u32 i) { return s[i] & px::SMASK; }
 
     // Every envelope is deliverable (model.rs:238-257), but most deliveries are no-ops
     // (`next_state` = None, src/actor/model.rs:299-301: the actor ignores the message). The mask
     // keeps the slots whose delivery changes the state: the exact complement of apply's `false`
     // returns below, so the successors and their slot order are unchanged, and the load-balanced
     // expansion spends its lanes on real successors only.
-    SR_HD bool delivers(const u64* s, u32 e) const {
+    // phases: client c's phase in bits 2c, 2c+1
+    SR_HD bool delivers(const u64* s, u32 e, u32 phases) const {
         const u32 dst = px::e_dst(e), kind = px::e_kind(e), bal = px::e_bal(e);
-        if (dst >= 3) {
-            const u32 ph = phase(s, (int)(dst - 3)), req = px::e_req(e);
-            return (ph == 0 && kind == px::PUTOK && req == dst) || (ph == 1 && kind == px::GETOK && req == 2 * dst);
+        if (dst >= 3) {  // (request ids are the client's own: e_req)
+            const u32 ph = phases >> (2 * (dst - 3)) & 3;
+            return (ph == 0 && kind == px::PUTOK) || (ph == 1 && kind == px::GETOK);
         }
-        const u64 sw = s[dst] & (dst == 0 ? ((1ull << px::SBITS) - 1) : ~0ull);
-        const u32 sbal = (u32)(sw & 15), sprop = (u32)(sw >> 4 & 7), decided = (u32)(sw >> 41 & 1);
+        const u64 sw = server_word(s, dst);
+        const u32 sbal = (u32)(sw & 15), sprop = (u32)(sw >> 4 & 15), decided = (u32)(sw >> 46 & 1);
         if (decided) return kind == px::GET;  // answered with GetOk, the state untouched
         switch (kind) {
             case px::PUT: return sprop == 0;
@@ -415,11 +544,16 @@ struct Paxos {
         }
     }
     SR_HD void enabled(const u64* s, u64* m) const {
+        u64 hlo, hhi;
+        hist_get(s, hlo, hhi);
+        const PaxosHist h = hs();
+        u32 phases = 0;
+        for (u32 c = 0; c < (u32)C; ++c) phases |= h.phase(hlo, hhi, c) << (2 * c);
         u64 mk = 0;
 #pragma unroll
         for (int k = 0; k < px::SLOTS; ++k) {
             const u32 e = slot(s, k);
-            if (e != px::EMPTY && delivers(s, e)) mk |= 1ull << k;
+            if (e != px::EMPTY && delivers(s, e, phases)) mk |= 1ull << k;
         }
         m[0] = mk;
     }
@@ -435,31 +569,34 @@ struct Paxos {
         const u32 dst = px::e_dst(e);
         u32 out[3] = {0, 0, 0};
         int nout = 0;
-        u64 w0 = s[0], w1 = s[1], w2 = s[2];
+        u64 w[4] = {s[0], s[1], s[2], NET0 == 4 ? s[3] : 0ull};
         if (dst < 3) {
-            const u64 sw = dst == 0 ? (w0 & ((1ull << px::SBITS) - 1)) : dst == 1 ? w1 : w2;
-            px::Srv sv = px::Srv::load(sw);
+            px::Srv sv = px::Srv::load(server_word(s, dst));
             const bool owned = px::server_on_msg(dst, sv, e, out, nout);
             if (!owned && nout == 0) return false;  // is_no_op (src/actor.rs:232-234)
             const u64 nw = sv.store();
-            if (dst == 0) w0 = (w0 & ~((1ull << px::SBITS) - 1)) | nw;
-            else if (dst == 1) w1 = nw;
-            else w2 = nw;
+#pragma unroll
+            for (u32 i = 0; i < 3; ++i)
+                if (i == dst) w[i] = (w[i] & ~px::SMASK) | nw;
         } else {  // RegisterActor::Client::on_msg (src/actor/register.rs:170-200), put_count = 1
-            const u32 c = dst - 3, ph = phase(s, (int)c), kind = px::e_kind(e), req = px::e_req(e);
-            u32 ev;
-            if (ph == 0 && kind == px::PUTOK && req == dst) {
-                out[nout++] = px::env(dst, (dst + 1) % 3, px::GET, 0, 0, 0, 2 * dst, 0);
-                ev = c * px::NEV_PER_CLIENT;
-            } else if (ph == 1 && kind == px::GETOK && req == 2 * dst) {
-                ev = c * px::NEV_PER_CLIENT + 1 + px::e_val(e);
+            const u32 c = dst - 3, kind = px::e_kind(e);
+            const PaxosHist h = hs();
+            u64 lo, hi;
+            hist_get(s, lo, hi);
+            const u32 ph = h.phase(lo, hi, c);
+            if (ph == 0 && kind == px::PUTOK) {
+                // record_returns (WriteOk), then the Get is sent and recorded by record_invocations
+                out[nout++] = px::env(dst, (dst + 1) % 3, px::GET, 0, 0);  // request 2 * id
+                for (u32 u = 0; u < (u32)C; ++u)
+                    if (u != c) PaxosHist::put(lo, hi, c * h.fb() + 5 + 2 * (u < c ? u : u - 1), 2, h.phase(lo, hi, u));
+            } else if (ph == 1 && kind == px::GETOK) {
+                PaxosHist::put(lo, hi, c * h.fb() + 2, 3, px::e_val(e));  // record_returns (ReadOk(v))
             } else {
                 return false;
             }
-            const int off = px::SBITS + 2 * (int)c;
-            w0 = (w0 & ~(3ull << off)) | ((u64)(ph + 1) << off);
-            const u64 h = h_next()[(size_t)hist(s) * nev + ev];  // record_returns, record_invocations
-            w0 = (w0 & ((1ull << 48) - 1)) | h << 48;
+            PaxosHist::put(lo, hi, c * h.fb(), 2, ph + 1);
+            PaxosHist::put(lo, hi, NOT_LIN_BIT, 1, h.linearizable(lo, hi) ? 0u : 1u);
+            hist_set(w, lo, hi);
         }
         // remove the delivered envelope (DuplicatingNetwork::No), then insert what was sent
 #pragma unroll
@@ -478,17 +615,20 @@ struct Paxos {
                 prev = cur;
             }
         }
-        o[0] = w0;
-        o[1] = w1;
-        o[2] = w2;
 #pragma unroll
-        for (int k = 0; k < px::SLOTS / 2; ++k) o[3 + k] = (u64)net[2 * k] | (u64)net[2 * k + 1] << 32;
+        for (int i = 0; i < NET0; ++i) o[i] = w[i];
+#pragma unroll
+        for (int k = 0; k < px::SLOTS / 2; ++k) o[NET0 + k] = (u64)net[2 * k] | (u64)net[2 * k + 1] << 32;
         return true;
     }
 
     SR_HD bool discovers(int p, const u64* s) const {
-        if (p == 0) return !h_lin()[hist(s)];  // always "linearizable" (examples/paxos.rs:251-254)
-        bool any = false;                      // sometimes "value chosen" (examples/paxos.rs:255-261)
+        if (p == 0) {  // always "linearizable" (examples/paxos.rs:251-254): the cached search result
+            u64 lo, hi;
+            hist_get(s, lo, hi);
+            return PaxosHist::get(lo, hi, NOT_LIN_BIT, 1) != 0;
+        }
+        bool any = false;  // sometimes "value chosen" (examples/paxos.rs:255-261)
 #pragma unroll
         for (int k = 0; k < px::SLOTS; ++k) {
             const u32 e = slot(s, k);
@@ -502,12 +642,11 @@ struct Paxos {
         for (int k = 0; k < px::SLOTS; ++k) net[k] = px::EMPTY;
         for (int c = 0; c < C; ++c) {
             const u32 id = 3 + (u32)c;
-            net[c] = px::env(id, id % 3, px::PUT, 0, 0, 0, id, (u32)c + 1);
+            net[c] = px::env(id, id % 3, px::PUT, 0, 0);  // request id and value: the client's
         }
         std::sort(net, net + C);
-        out[0] = (u64)init_hist << 48;
-        out[1] = out[2] = 0;
-        for (int k = 0; k < px::SLOTS / 2; ++k) out[3 + k] = (u64)net[2 * k] | (u64)net[2 * k + 1] << 32;
+        for (int i = 0; i < NET0; ++i) out[i] = 0;  // every Put in flight: all phases 0
+        for (int k = 0; k < px::SLOTS / 2; ++k) out[NET0 + k] = (u64)net[2 * k] | (u64)net[2 * k + 1] << 32;
         return 1;
     }
     int expectation(int p) const { return p == 0 ? ALWAYS : SOMETIMES; }
@@ -517,11 +656,11 @@ struct Paxos {
     void describe(const u64* s, i64* d) const {
         int k = 0;
         for (int i = 0; i < 3; ++i) {
-            const px::Srv v = px::Srv::load(i == 0 ? s[0] & ((1ull << px::SBITS) - 1) : s[i]);
+            const px::Srv v = px::Srv::load(server_word(s, (u32)i));
             d[k++] = v.bal >> 2;
             d[k++] = v.bal & 3;
             d[k++] = v.prop ? (i64)v.prop : -1;
-            for (int j = 0; j < 3; ++j) d[k++] = (v.prep[j] >> 7) ? px::acc_code(v.prep[j] & 127) : -1;
+            for (int j = 0; j < 3; ++j) d[k++] = (v.prep[j] >> 8) ? px::acc_code(v.prep[j] & 255) : -1;
             d[k++] = v.accepts;
             d[k++] = px::acc_code(v.accepted);
             d[k++] = v.decided;
@@ -543,5 +682,7 @@ struct Paxos {
                (kind < 9 ? names[kind] : "?") + " }";
     }
 };
+using Paxos = PaxosT<11>;      // up to 4 clients
+using PaxosWide = PaxosT<12>;  // 5 or 6 clients
 
 }  // namespace sr

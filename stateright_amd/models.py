@@ -72,7 +72,8 @@ class Paxos(_Model):
     (src/actor/model.rs:176-327) with a linearizability history (src/actor/register.rs:37-87).
 
     Action ids are canonical envelope codes (oracle/paxos.hpp `envelope_code`), so a path is
-    comparable with the CPU oracle's."""
+    comparable with the CPU oracle's. client_count 1..6 (the reference's bench.sh checks 6); the
+    linearizability history is kept in the state and checked on the device (csrc/paxos.hpp)."""
     MODEL_ID = N.SR_MODEL_PAXOS
 
     def __init__(self, client_count=2, server_count=3):

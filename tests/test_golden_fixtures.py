@@ -15,6 +15,8 @@ from oracle_lib import OracleRun
 HERE = os.path.dirname(os.path.abspath(__file__))
 with open(os.path.join(HERE, "golden", "bfs_goldens.json")) as f:
     CASES = json.load(f)["cases"]
+with open(os.path.join(HERE, "golden", "paxos_counts.json")) as f:
+    PAXOS_COUNTS = json.load(f)["cases"]
 
 
 def cid(c):
@@ -61,3 +63,21 @@ def test_gpu_reproduces_table(case):
     assert sorted(c.discoveries()) == sorted(case["discoveries"])
     for name, actions in case["discoveries"].items():
         assert c.discovery(name).action_ids == actions
+
+
+def test_paxos_counts_fixture_agrees():
+    # tests/golden/paxos_counts.json (oracle/bfs_cli, client_count 1..6): the rows the FIFO table
+    # also holds agree, the reference's own golden (examples/paxos.rs:268-290) holds, and the
+    # single-threaded oracle reproduces the small rows here (4..6 take minutes on the CPU; the GPU
+    # tests compare against them).
+    by = {r["client_count"]: r for r in PAXOS_COUNTS}
+    assert sorted(by) == [1, 2, 3, 4, 5, 6]
+    assert by[2]["unique_state_count"] == 16668
+    for c in (1, 2):
+        t = _by("paxos", [c])
+        assert (by[c]["unique_state_count"], by[c]["state_count"], by[c]["max_depth"]) == \
+            (t["unique_state_count"], t["state_count"], t["max_depth"])
+    for c in (1, 2, 3):
+        r = OracleRun(7, [c])
+        assert (r.unique_state_count, r.state_count, r.max_depth, r.discovery_names()) == (
+            by[c]["unique_state_count"], by[c]["state_count"], by[c]["max_depth"], by[c]["discoveries"])

@@ -7,6 +7,8 @@ has the reference's (shortest) length.
 """
 import math
 
+import os
+
 import pytest
 
 from oracle_lib import (BINARY_CLOCK, INCREMENT, INCREMENT_LOCK, LINEAR_EQUATION, PAXOS, TWO_PHASE, OracleRun,
@@ -279,6 +281,29 @@ def test_paxos_3_clients_matches_oracle(order):
     assert sorted(c.discoveries()) == ["value chosen"]
     if order == "fifo":
         assert c.discovery("value chosen").action_ids == o.discovery_actions("value chosen")
+
+
+@pytest.mark.parametrize("clients,order", [(4, "fifo"), (4, "fast"), (5, "fast"), (6, "fast"), (6, "fifo")])
+def test_paxos_more_clients(clients, order):
+    # The reference's parameter space (bench.sh:27 checks 6 clients): the encoding keeps the
+    # linearizability history in the state (no precomputed table, whose closure has 558 385
+    # histories at 4 clients), W = 11 up to 4 clients and 12 for 5-6. Counts against the oracle's
+    # (tests/golden/paxos_counts.json), the discovery path replays on the CPU model, and at 4
+    # clients the FIFO path equals the single-threaded oracle's.
+    import json
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "paxos_counts.json")) as f:
+        want = next(r for r in json.load(f)["cases"] if r["client_count"] == clients)
+    c, _ = gpu(PAXOS, [clients], order)
+    assert (c.unique_state_count(), c.state_count(), c.max_depth()) == \
+        (want["unique_state_count"], want["state_count"], want["max_depth"])
+    assert sorted(c.discoveries()) == want["discoveries"]
+    c.assert_properties()
+    path = c.discovery("value chosen")
+    r = replay(PAXOS, [clients], path.action_ids, n_props=2)
+    assert r is not None and r[1][1] == 1
+    if clients == 4 and order == "fifo":
+        o = oracle(PAXOS, [4])
+        assert path.action_ids == o.discovery_actions("value chosen")
 
 
 @pytest.mark.parametrize("grid", ["1", "2"])
