@@ -20,7 +20,7 @@ namespace sr {
 // the trade-off). SR_OWNER_RMS overrides it; 0 owns states by fingerprint.
 static int two_phase_owner_rms(int n) {
     if (const char* e = std::getenv("SR_OWNER_RMS")) return std::max(0, std::min(n, std::atoi(e)));
-    return std::min(6, (n + 1) / 2);
+    return n <= 7 ? (n + 1) / 2 : 4;  // N=11 at T=8: 0.33 of successors cross, per-level balance 1.14
 }
 
 // The registry below instantiates `E<Model>` for every model; the single-GPU engine and the

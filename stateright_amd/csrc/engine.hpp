@@ -490,14 +490,17 @@ class Engine final : public EngineBase {
     // probe limit). If an entry does not fit the new table's probe limit, the rehash starts over
     // from the old table into one twice as large again. In FIFO order the level's candidate slots
     // (cand) are remapped to the new table, since the rehash moves every entry.
-    void grow_table(u32* cand = nullptr, u64 cand_n = 0) {
+    // min_slots: grow to at least this many slots (one rehash, however many doublings that is).
+    void grow_table(u32* cand = nullptr, u64 cand_n = 0, u64 min_slots = 0) {
         DBuf<u64> ok, om;
         ok.swap(keys_);
         if (fifo_) om.swap(meta_);
         const TableView from = make_table_view(m_, ok.p, fifo_ ? om.p : nullptr, cap_);
         const u64 old_cap = cap_;
         if (!aux_.p) aux_.alloc(o_.device, 2);
-        for (u64 f = 2;; f *= 2) {
+        u64 f0 = 2;
+        while (old_cap * f0 < min_slots) f0 *= 2;
+        for (u64 f = f0;; f *= 2) {
             alloc_table(old_cap * f);
             SR_HIP(hipMemsetAsync(aux_.p, 0, sizeof(u32), stream_));
             rehash<<<blocks_for(old_cap, 256), 256, 0, stream_>>>(from, old_cap, view(), aux_.p);
@@ -515,6 +518,20 @@ class Engine final : public EngineBase {
         SR_HIP(stream_sync(stream_));
         stats.rehashes++;
     }
+
+    // Growth during a check (no capacity hint, or one too small: the path a user of the reference
+    // gets, whose DashMap grows as it goes, src/checker/bfs.rs:26) takes a few large steps rather
+    // than doublings: every growth stops the level pipeline, and a table growth rehashes every
+    // entry. A step multiplies the size by SR_GROW_STEP (default 8), within a share of the free
+    // device memory (never below what the level needs).
+    u64 growth_slots(u64 need_slots) const {
+        u64 target = std::max<u64>(need_slots, cap_ * grow_step_);
+        size_t free_b = 0, total_b = 0;
+        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b) target = std::min<u64>(target, std::max<u64>(need_slots, free_b / 4 / 8));
+        return target;
+    }
+    u64 grow_step_ = std::getenv("SR_GROW_STEP") && std::atoi(std::getenv("SR_GROW_STEP")) >= 2
+                         ? (u64)std::atoi(std::getenv("SR_GROW_STEP")) : 8u;
 
     // The growth threshold of the visited set: 0.8 load, or lower for a quotient-mode table whose
     // probe limit (set by its displacement bits) would otherwise be reached by the longest
@@ -545,7 +562,8 @@ class Engine final : public EngineBase {
     // by copying the used prefix.
     void ensure_arena(u64 states, u64 used) {
         if (arena_cap_ >= states) return;
-        u64 cap = std::max<u64>(states, arena_cap_ * 2);
+        // (growth steps of 4: each copies the arena so far and stops the level pipeline)
+        u64 cap = std::max<u64>(states, arena_cap_ * (arena_cap_ ? 4 : 1));
         DBuf<u64> na;
         DBuf<u32> np, ne;
         na.alloc(o_.device, cap * W);
@@ -746,7 +764,7 @@ class Engine final : public EngineBase {
         // hinted: room for every state plus one level's worth of planning slack (a regrowth copies
         // the whole arena mid-run)
         const u64 slack = huge ? o_.capacity_hint / 10 * 3 : o_.capacity_hint / 2;
-        ensure_arena(std::max<u64>(1u << 16, (o_.capacity_hint + slack + 1024) * grow_factor_), 0);
+        ensure_arena(std::max<u64>(std::max<u64>(1u << 16, (1u << 20) / W), (o_.capacity_hint + slack + 1024) * grow_factor_), 0);
         lstart_.assign({0, (u64)k});
         lvisited_.clear();
         const u32 und0 = ((1u << M::NPROPS) - 1) & ~emask_;
@@ -1066,7 +1084,8 @@ class Engine final : public EngineBase {
     // the visited set and the arena are grown first if the level might not fit.
     u32 launch_sync(u64 n, u32 undiscovered) {
         const u64 d_eff = pessimistic_ ? D_ : std::min<u64>(D_, (u64)std::ceil(2.0 * ratio_ + 1.0));
-        while ((double)(unique + n * d_eff) > lmax_ * (double)cap_) grow_table();
+        const double need = (double)(unique + n * d_eff);
+        if (need > lmax_ * (double)cap_) grow_table(nullptr, 0, growth_slots((u64)(need / lmax_) + 1));
         const u64 fbase = lstart_[lstart_.size() - 2];
         ensure_arena(fbase + n + n * d_eff, fbase + n);
         return launch_expand(fbase, (u32)n, false, n, undiscovered);

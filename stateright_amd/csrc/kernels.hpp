@@ -669,8 +669,10 @@ __device__ u64* g_timeline;
 // STATS = 1 also counts visited-set probes and CAS attempts (sr_opts.counters): a separate
 // instantiation, because the per-lane counters cost registers (SGPR spills 8 -> 47) and ~20% of
 // the kernel's time.
+// Wide states (W >= 4: paxos, the actor models) run three waves per SIMD (<= 168 VGPRs): their
+// levels are latency-bound, and paxos' device-side history search had pushed them to two.
 template <class M, int PB, int POL, bool STATS = false>
-__global__ void __launch_bounds__(256) expand_fast(M m, const u64* __restrict__ frontier, u32 lo, u32 hi,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W >= 4 ? 3 : 1))) expand_fast(M m, const u64* __restrict__ frontier, u32 lo, u32 hi,
                                                    TableView t, u64* __restrict__ next, u32* __restrict__ next_par,
                                                    u32 next_cap, LevelCounters* lc, u32 undiscovered,
                                                    HostCounters* hc, u32 seq, u32 reset, u32 ppw_log2,

@@ -402,49 +402,51 @@ struct PaxosHist {
     SR_HD bool linearizable(u64 lo, u64 hi) const {
         // No completed Read: the completed ops are Writes invoked together at init, unordered in
         // real time, and any order of them (in-flight ops left out) is a valid serialization.
-        bool any_read = false;
-        for (u32 t = 0; t < C; ++t) any_read |= phase(lo, hi, t) == 2;
-        if (!any_read) return true;
-        u32 done[MAXC], lastv[MAXC][MAXC], rv[MAXC];
+        // Packed scalars only (2-bit fields per client, 8-bit frames): an array indexed by client
+        // would live in scratch memory and raise the registers of every kernel this inlines into.
+        u32 done = 0, any_read = 0;  // phase of client t at bits 2t
         for (u32 t = 0; t < C; ++t) {
-            done[t] = phase(lo, hi, t);
-            rv[t] = ret(lo, hi, t);
-            for (u32 u = 0; u < C; ++u) lastv[t][u] = u == t ? 0u : last(lo, hi, t, u);
+            const u32 p = phase(lo, hi, t);
+            done |= p << (2 * t);
+            any_read |= p == 2;
         }
-        u32 next[MAXC], used[MAXC];
-        for (u32 t = 0; t < C; ++t) next[t] = used[t] = 0;
-        // frames: thread, kind (0 completed op, 1 in-flight op), register before
-        u32 ft[2 * MAXC], fk[2 * MAXC], fr[2 * MAXC];
+        if (!any_read) return true;
+        auto f2 = [](u32 v, u32 t) { return v >> (2 * t) & 3u; };
+        u32 next = 0, used = 0;  // next op of client t at bits 2t; in-flight op used: bit t
+        u64 fl = 0, fh = 0;      // frames (8 bits each): thread | kind << 3 | register before << 4
         u32 depth = 0, reg = 0, t0 = 0;
         // op (t, i) may be placed once every op that completed before its invocation is placed
         auto violates = [&](u32 t, u32 i) {
             if (i == 0) return false;  // a Put: invoked before anything completed
             for (u32 u = 0; u < C; ++u)
-                if (u != t && next[u] < done[u] && next[u] < lastv[t][u]) return true;
+                if (u != t && f2(next, u) < f2(done, u) && f2(next, u) < last(lo, hi, t, u)) return true;
             return false;
         };
+        auto push = [&](u32 t, u32 kind) {
+            const u64 f = (u64)(t | kind << 3 | reg << 4);
+            if (depth < 8) fl |= f << (8 * depth);
+            else fh |= f << (8 * (depth - 8));
+            ++depth;
+        };
         for (int guard = 0; guard < 1 << 20; ++guard) {
-            bool all = true;
-            for (u32 t = 0; t < C; ++t) all &= next[t] == done[t];
-            if (all) return true;
+            if (next == done) return true;  // every completed op placed
             bool found = false;
             for (u32 t = t0; t < C && !found; ++t) {
-                if (next[t] == done[t]) {
-                    if (done[t] == 2 || used[t] || violates(t, done[t])) continue;  // in-flight op: index done[t]
-                    ft[depth] = t, fk[depth] = 1, fr[depth] = reg, ++depth;
-                    used[t] = 1;
-                    if (done[t] == 0) reg = t + 1;  // a Write takes effect; a Read returns anything
+                const u32 n = f2(next, t), d = f2(done, t);
+                if (n == d) {
+                    if (d == 2 || (used >> t & 1) || violates(t, d)) continue;  // in-flight op: index d
+                    push(t, 1);
+                    used |= 1u << t;
+                    if (d == 0) reg = t + 1;  // a Write takes effect; a Read returns anything
                     found = true;
                 } else {
-                    const u32 i = next[t];
-                    next[t]++;
-                    const bool ok = !violates(t, i) && (i == 0 || rv[t] == reg);
-                    if (!ok) {
-                        next[t]--;
+                    next += 1u << (2 * t);
+                    if (violates(t, n) || (n == 1 && ret(lo, hi, t) != reg)) {
+                        next -= 1u << (2 * t);
                         continue;
                     }
-                    ft[depth] = t, fk[depth] = 0, fr[depth] = reg, ++depth;
-                    if (i == 0) reg = t + 1;
+                    push(t, 0);
+                    if (n == 0) reg = t + 1;
                     found = true;
                 }
             }
@@ -454,10 +456,13 @@ struct PaxosHist {
             }
             if (depth == 0) return false;
             --depth;
-            const u32 t = ft[depth];
-            if (fk[depth]) used[t] = 0;
-            else next[t]--;
-            reg = fr[depth];
+            const u32 f = (u32)((depth < 8 ? fl >> (8 * depth) : fh >> (8 * (depth - 8))) & 0xff);
+            if (depth < 8) fl &= ~(0xffull << (8 * depth));
+            else fh &= ~(0xffull << (8 * (depth - 8)));
+            const u32 t = f & 7;
+            if (f >> 3 & 1) used &= ~(1u << t);
+            else next -= 1u << (2 * t);
+            reg = f >> 4;
             t0 = t + 1;
         }
         return false;
