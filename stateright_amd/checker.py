@@ -201,9 +201,9 @@ class CheckerBuilder:
     def spawn_bfs(self):
         """`spawn_bfs` (src/checker.rs:124-129): non-blocking; call `join()`."""
         if self._comm is not None or self._partitions > 1:
-            if self._visitor is not None:
-                raise NotImplementedError("visit recording is a single-GPU feature")
-            return GpuBfsChecker(self._model, self._opts, None, comm=self._comm, partitions=self._partitions)
+            # (a visitor's record is gathered from every partition at join, collectively: every
+            # rank of a communicator passes a visitor)
+            return GpuBfsChecker(self._model, self._opts, self._visitor, comm=self._comm, partitions=self._partitions)
         return GpuBfsChecker(self._model, self._opts, self._visitor)
 
     spawn_gpu_bfs = spawn_bfs

@@ -41,6 +41,7 @@
 #include <mutex>
 #include <set>
 #include <tuple>
+#include <unordered_map>
 
 #include "kernels_dist.hpp"
 
@@ -965,7 +966,52 @@ class DistEngine final : public EngineBase {
                 std::vector<i64>& states) const override {
         return explore_model(base_model(m_), fps, n, action, has, fp, states);
     }
-    std::vector<i64> visits() const override { return {}; }
+    // The visit record (sr_opts.record_visits: the StateRecorder / PathRecorder / Fn(Path)
+    // visitors, src/checker/visitor.rs:19-99, called at every pop by src/checker/bfs.rs:187-189),
+    // gathered on every rank at join (gather_visits): the states level by level, a level in
+    // partition order and each partition's part in its arena (FAST) order.
+    std::vector<i64> visits() const override {
+        const int wd = m_.describe_width();
+        std::vector<i64> out(vst_.size() / W * wd);
+        for (size_t i = 0; i < vst_.size() / W; ++i) m_.describe(&vst_[i * W], &out[i * wd]);
+        return out;
+    }
+    // Each visited state's parent: the FIRST generator of it in the previous level's visit order,
+    // by the first action in `actions()` order (a FAST-order BFS tree: any generator is a valid
+    // parent, src/checker/path.rs:55-79), found on the host model from the gathered states.
+    bool visit_tree(std::vector<i64>& parent, std::vector<i64>& action) const override {
+        if (!o_.record_visits) return false;
+        parent.clear();
+        action.clear();
+        std::unordered_map<u64, std::pair<i64, i64>> first;  // fingerprint -> (parent visit index, action id)
+        i64 base = 0, prev_base = 0;
+        for (size_t d = 0; d < vlev_.size(); ++d) {
+            const i64 nv = (i64)vlev_[d];
+            if (d > 0) {
+                first.clear();
+                for (i64 i = prev_base; i < base; ++i) {
+                    const u64* ps = &vst_[(size_t)i * W];
+                    for_each_successor(m_, ps, [&](int a, const u64* ns) {
+                        first.emplace(fingerprint<W>(ns), std::make_pair(i, m_.action_id(ps, a)));
+                    });
+                }
+            }
+            for (i64 i = 0; i < nv; ++i) {
+                if (d == 0) {
+                    parent.push_back(-1);
+                    action.push_back(-1);
+                    continue;
+                }
+                auto it = first.find(fingerprint<W>(&vst_[(size_t)(base + i) * W]));
+                if (it == first.end()) throw Error(SR_ERR_NONDETERMINISM, "Unable to reconstruct a `Path` for a visited state");
+                parent.push_back(it->second.first);
+                action.push_back(it->second.second);
+            }
+            prev_base = base;
+            base += nv;
+        }
+        return true;
+    }
     int partitions() const { return (int)T_; }
     bool early_exit() const { return early_exit_; }
 
@@ -1031,11 +1077,13 @@ class DistEngine final : public EngineBase {
                 }
                 if (hi == 0) {
                     gather_paths();
+                    gather_visits();
                     return;
                 }
                 if (attempt >= 3) throw Error(ecode, what);
             } else if (code == 0) {
                 gather_paths();
+                gather_visits();
                 return;
             }
             // capacity: every rank saw it at the same level (the rows are the same everywhere)
@@ -1104,6 +1152,61 @@ class DistEngine final : public EngineBase {
         }
         paths_ready_ = true;
     }
+    // Every visited state to every rank (record_visits; collective: every rank runs it at join):
+    // the replicated head's levels from rank 0's head arena, then each partitioned level from
+    // every partition's arena (a partition's whole arena prefix broadcast by its owner rank).
+    void gather_visits() {
+        vst_.clear();
+        vlev_.clear();
+        if (!o_.record_visits) return;
+        const u32 last = max_depth;  // levels 0..max_depth hold states
+        auto fetch = [&](const u64* dev, u64 words, int root) {
+            std::vector<u64> h(words);
+            if (!words) return h;
+            if (!comm_) {
+                SR_HIP(hipMemcpy(h.data(), dev, words * 8, hipMemcpyDeviceToHost));
+                return h;
+            }
+            DBuf<u64> buf;
+            buf.alloc(o_.device, words);
+            if (comm_->rank == root) SR_HIP(hipMemcpyAsync(buf.p, dev, words * 8, hipMemcpyDeviceToDevice, stream_));
+            comm_->broadcast(buf.p, words, root, stream_);
+            SR_HIP(hipMemcpyAsync(h.data(), buf.p, words * 8, hipMemcpyDeviceToHost, stream_));
+            SR_HIP(stream_sync(stream_));
+            return h;
+        };
+        SR_HIP(stream_sync(stream_));
+        const u32 head_levels = head_done_ ? last + 1 : lvl0_;
+        if (head_levels) {
+            const u64 hn = hlstart_[std::min<size_t>(head_levels, hlstart_.size() - 1)];
+            const std::vector<u64> h = fetch(harena_.p, hn * W, 0);
+            for (u32 d = 0; d < head_levels && d + 1 < hlstart_.size(); ++d) {
+                vlev_.push_back(hlstart_[d + 1] - hlstart_[d]);
+                vst_.insert(vst_.end(), h.begin() + (i64)(hlstart_[d] * W), h.begin() + (i64)(hlstart_[d + 1] * W));
+            }
+        }
+        if (head_done_) return;
+        std::vector<std::vector<u64>> arenas(T_);
+        for (u32 q = 0; q < T_; ++q) {
+            const Part* pp = nullptr;
+            for (auto& p : parts_)
+                if (p.id == q) pp = &p;
+            arenas[q] = fetch(pp ? pp->arena.p : nullptr, gl_off_[q] * W, (int)q);
+        }
+        for (u32 d = lvl0_; d <= last; ++d) {
+            u64 n = 0;
+            for (u32 q = 0; q < T_; ++q) {
+                const size_t k = d - lvl0_;
+                const u64 lo = gl_lstart_[q][k], hi = k + 1 < gl_lstart_[q].size() ? gl_lstart_[q][k + 1] : gl_off_[q];
+                vst_.insert(vst_.end(), arenas[q].begin() + (i64)(lo * W), arenas[q].begin() + (i64)(hi * W));
+                n += hi - lo;
+            }
+            vlev_.push_back(n);
+        }
+    }
+    std::vector<u64> vst_;   // visited states (gather_visits)
+    std::vector<u64> vlev_;  // visited states per level
+
     bool path_states(int p, std::vector<u64>& st) {
         if (p < 0 || p >= M::NPROPS) return false;
         if (paths_ready_) {

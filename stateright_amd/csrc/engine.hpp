@@ -741,7 +741,9 @@ class Engine final : public EngineBase {
         seq_launch_.clear();
 
         // Visited set sized for <= table_load_ load at the hinted unique count.
-        u64 cap = std::max<u64>((u64)(1u << 20) * grow_factor_, min_table_cap(m_));
+        // (without a hint: 2^22 slots, 32 MiB, a few us to clear and recycled between checks; the
+        // table then grows in steps of SR_GROW_STEP)
+        u64 cap = std::max<u64>((u64)(1u << 22) * grow_factor_, min_table_cap(m_));
         // Hints beyond 2^31 states (increment_lock N=12: 5.2e9) size the table for <= 0.75 load and
         // the arena with 30% slack, so that table + arena fit one MI355X's 288 GB.
         const bool huge = o_.capacity_hint > (1ull << 31);
@@ -764,7 +766,7 @@ class Engine final : public EngineBase {
         // hinted: room for every state plus one level's worth of planning slack (a regrowth copies
         // the whole arena mid-run)
         const u64 slack = huge ? o_.capacity_hint / 10 * 3 : o_.capacity_hint / 2;
-        ensure_arena(std::max<u64>(std::max<u64>(1u << 16, (1u << 20) / W), (o_.capacity_hint + slack + 1024) * grow_factor_), 0);
+        ensure_arena(std::max<u64>(std::max<u64>(1u << 16, (1u << 22) / W), (o_.capacity_hint + slack + 1024) * grow_factor_), 0);
         lstart_.assign({0, (u64)k});
         lvisited_.clear();
         const u32 und0 = ((1u << M::NPROPS) - 1) & ~emask_;

@@ -489,7 +489,7 @@ __device__ __forceinline__ u64 find_slot(const TableView& t, const ProbeKey& k) 
 }
 
 template <class M, class F>
-__device__ __forceinline__ void for_each_successor(const M& m, const u64* s, F&& f) {
+__host__ __device__ __forceinline__ void for_each_successor(const M& m, const u64* s, F&& f) {
     u64 mask[M::MW];
     m.enabled(s, mask);
 #pragma unroll

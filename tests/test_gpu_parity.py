@@ -252,11 +252,17 @@ def test_2pc_8_fifo_matches_fast():
     assert (a.unique_state_count(), a.state_count(), a.max_depth()) == (b.unique_state_count(), b.state_count(), b.max_depth())
 
 
-def test_growth_from_small_table():
-    # No capacity hint: the visited set must rehash several times mid-level and stay exact.
-    c = sr.TwoPhaseSys(8).checker().order("fast").spawn_bfs().join()
-    assert c.unique_state_count() == 6 ** 8 + 4 ** 8 + 2 ** 8
-    assert c.stats()["rehashes"] >= 1
+@pytest.mark.parametrize("step", ["2", "8"])
+def test_growth_from_small_table(step, monkeypatch):
+    # No capacity hint (the path a reference user gets): the visited set and the arena grow during
+    # the check, in steps of SR_GROW_STEP (default 8; 2 = doublings, several rehashes), and the
+    # counts stay exact.
+    monkeypatch.setenv("SR_GROW_STEP", step)
+    n = 9
+    c = sr.TwoPhaseSys(n).checker().order("fast").spawn_bfs().join()
+    assert c.unique_state_count() == 6 ** n + 4 ** n + 2 ** n
+    assert 3 * c.state_count() == 4 * n * 6 ** n + 3 * (n + 1) * 4 ** n + 3 * n * 2 ** n + 6
+    assert c.stats()["rehashes"] >= (2 if step == "2" else 1)
 
 
 def test_paxos_golden():

@@ -65,6 +65,44 @@ def test_fast_visitor_paths_replay():
     assert all(len(p) == depth[p.last_state()] for p in seen)
 
 
-def test_visitor_rejected_by_partitioned_search():
-    with pytest.raises(NotImplementedError):
-        sr.TwoPhaseSys(3).checker().partitions(2).visitor(lambda p: None).spawn_bfs()
+@pytest.mark.parametrize("head", ["0", "65536"])
+@pytest.mark.parametrize("parts", [2, 3])
+def test_partitioned_visitors(parts, head, monkeypatch):
+    # The partitioned search gathers every partition's visited states at join (visit order: level
+    # by level, partitions in turn, FAST order inside): the StateRecorder sees exactly the oracle's
+    # visited set, and every PathRecorder path replays on the CPU model with its BFS depth.
+    monkeypatch.setenv("SR_HEAD_MAX", head)
+    n = 5
+    o = OracleRun(TWO_PHASE, [n], record_visits=True)
+    rec = sr.StateRecorder()
+    c = sr.TwoPhaseSys(n).checker().partitions(parts).visitor(rec).spawn_bfs().join()
+    assert len(rec.states) == c.unique_state_count() == len(o.visits())
+    assert set(rec.states) == set(o.visits())
+    seen = []
+    sr.TwoPhaseSys(n).checker().partitions(parts).visitor(seen.append).spawn_bfs().join()
+    depth = {s: len(a) for s, a in zip(o.visits(), o.visit_paths())}
+    assert len(seen) == len(o.visits())
+    for p in seen:
+        states, _ = replay(TWO_PHASE, [n], p.action_ids, n_props=3)
+        width = len(p.last_state())
+        assert tuple(states[-width:]) == p.last_state()
+        assert len(p) == depth[p.last_state()]
+
+
+def test_partitioned_visitors_ranks():
+    # the same on in-process ranks (collective gathering at join; any rank holds the record)
+    from stateright_amd.distributed import Communicator
+    n = 4
+    o = OracleRun(TWO_PHASE, [n], record_visits=True)
+    comms = Communicator.local_group(2)
+    try:
+        recs = [sr.StateRecorder() for _ in comms]
+        cs = [sr.TwoPhaseSys(n).checker().comm(cm).visitor(r).spawn_bfs() for cm, r in zip(comms, recs)]
+        for ch in cs:
+            ch.join()
+        for r in recs:
+            assert sorted(r.states) == sorted(o.visits())
+        cs.clear()
+    finally:
+        for cm in comms:
+            cm.close()
