@@ -332,9 +332,13 @@ class Engine final : public EngineBase {
         bind(lease.c);
         int order = o_.order;
         if (order == SR_ORDER_AUTO) order = o_.target_state_count ? SR_ORDER_FIFO : SR_ORDER_FAST;
-        // `eventually` discoveries depend on the visit order (terminal-state overwrites), so such
-        // models always run in the reference's FIFO order.
-        if (emask_) order = SR_ORDER_FIFO;
+        // `eventually` discoveries depend on the visit order (which generator passes its bits on,
+        // which terminal state overwrites), so by default such models run in the reference's
+        // single-threaded FIFO order. An explicit FAST order is honoured: each state takes the
+        // bits of the generator that claims it, as in one of the reference's multi-threaded
+        // orders (`threads(n)`, src/checker/bfs.rs:75-152), and the discoveries are valid
+        // counterexamples of that order (the reference's false negatives may differ).
+        if (emask_ && o_.order != SR_ORDER_FAST) order = SR_ORDER_FIFO;
         bool order_dependent = run_with_restart(order);
         if (order_dependent && o_.order == SR_ORDER_AUTO && order == SR_ORDER_FAST) {
             // An early exit inside a level makes counts depend on the visit order: redo the
@@ -1202,6 +1206,10 @@ class Engine final : public EngineBase {
                     const u32 grid = std::min(expand_grid_cap(), blocks_for((c + (1u << ppw_log2) - 1) >> ppw_log2, 4));
                     SlotWork sw{};
                     sw.flags = repair ? SLOT_REPAIR : 0u;
+                    if (emask_ && peb) {
+                        sw.peb = peb;
+                        sw.naeb = aeb_.p + nbase;
+                    }
                     timed([&] {
                         auto launch = [&](auto kern) {
                             kern<<<grid, 256, filt_log2_ ? (8u << filt_log2_) : 0u, stream_>>>(

@@ -385,6 +385,11 @@ struct SlotWork {
     u32 seq;                    // its launch's sequence number
     LevelCounters* zero;        // slot to reset (nullptr: none)
     u32 flags = 0;              // SlotFlags
+    // `eventually` properties in FAST order: the EventuallyBits each parent passes on (by frontier
+    // rank) and those of the states appended, written by whichever generator claims a state (the
+    // reference's first insertion, src/checker/bfs.rs:246-263, in a multi-threaded order)
+    const u32* peb = nullptr;
+    u32* naeb = nullptr;
 };
 
 // One wave (lane = 0..63): publish sw.pub to sw.hc, then reset sw.zero.
@@ -958,6 +963,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W >
                     if (pos < next_cap) {
                         store_state<W>(next, pos, ns[j]);
                         next_par[pos] = pr;
+                        if (sw.naeb) sw.naeb[pos] = sw.peb[pr];
                     } else {
                         atomicOr(&lc->err, (u32)ERR_FRONTIER_OVERFLOW);
                     }
@@ -984,6 +990,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W >
                 if (pos < next_cap) {
                     store_state<W>(next, pos, ns);
                     next_par[pos] = stage_par[i];
+                    if (sw.naeb) sw.naeb[pos] = sw.peb[stage_par[i]];
                 } else {
                     atomicOr(&lc->err, (u32)ERR_FRONTIER_OVERFLOW);
                 }
@@ -1019,6 +1026,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W >
         if (pos < next_cap) {
             store_state<W>(next, pos, ns);
             next_par[pos] = stage_par[i];
+            if (sw.naeb) sw.naeb[pos] = sw.peb[stage_par[i]];
         } else {
             atomicOr(&lc->err, (u32)ERR_FRONTIER_OVERFLOW);
         }

@@ -2,8 +2,10 @@
 the reference's own tests (src/checker.rs:349-414) and the CPU oracle on random graphs.
 
 The GPU keeps one EventuallyBits word per frontier state, finds each level's terminal states, and
-reproduces the reference's overwrite-at-terminal semantics in its FIFO order (eventually models
-always run in FIFO order).
+reproduces the reference's overwrite-at-terminal semantics in its FIFO order (the default for
+eventually models). An explicit FAST order gives each state the bits of the generator that claims
+it, one of the reference's multi-threaded orders: its discoveries are valid counterexamples, and
+on graphs without joins (where no order can lose one) the same as the oracle's.
 """
 import random
 
@@ -102,3 +104,43 @@ def test_replay_trace_conditions_every_state():
     c = odd([0, 1, 4, 6], [2, 4, 8])
     per_state, terminal = c.replay_trace([1, 4, 6], init_index=0)  # 0 -> 1 -> 4 -> 6
     assert [s[0] for s in per_state] == [0, 1, 0, 0] and terminal
+
+
+def _chains(rng):
+    # disjoint chains: no state has two generators, so no visit order can lose a counterexample
+    labels = rng.sample(range(0, 200), 40)
+    paths, k = [], 0
+    for _ in range(rng.randint(1, 6)):
+        n = rng.randint(1, 6)
+        paths.append(labels[k:k + n])
+        k += n
+    return paths
+
+
+def test_fast_order_eventually_matches_oracle_without_joins():
+    rng = random.Random(77)
+    for _ in range(60):
+        paths = _chains(rng)
+        o = OracleRun(DGRAPH, dgraph_params(EVENTUALLY, paths))
+        g = sr.DGraph.with_property(EVENTUALLY)
+        for p in paths:
+            g = g.with_path(p)
+        c = g.checker().order("fast").spawn_bfs().join()
+        assert c.stats()["order_used"] == 2, paths  # FAST honoured
+        assert sorted(c.discoveries()) == o.discovery_names(), paths
+        for name, path in c.discoveries().items():
+            c.assert_discovery(name, path.action_ids)
+
+
+def test_fast_order_eventually_discoveries_are_valid():
+    # graphs with joins (the reference's known false negatives depend on the order): whatever FAST
+    # reports is a valid counterexample (never satisfied along the path, ending at a terminal state)
+    rng = random.Random(4321)
+    for _ in range(60):
+        paths = _random_graph(rng)
+        g = sr.DGraph.with_property(EVENTUALLY)
+        for p in paths:
+            g = g.with_path(p)
+        c = g.checker().order("fast").spawn_bfs().join()
+        for name, path in c.discoveries().items():
+            c.assert_discovery(name, path.action_ids)
