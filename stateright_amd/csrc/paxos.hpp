@@ -371,7 +371,11 @@ inline Tables& tables(int C, int device) {
 // and any client count fits; `linearizable` runs the tester's serialization search on it.
 struct PaxosHist {
     u32 C = 2;
-    SR_HD u32 fb() const { return 5 + 2 * (C - 1); }  // bits per client
+    // Layout: every client's phase first (2 bits each: they sit in word 0's spare bits, where
+    // `enabled` reads them with one shift), then the returned values (3 bits each), then each
+    // client's Get `last` entries (2 bits per other client).
+    SR_HD u32 ret_off(u32 c) const { return 2 * C + 3 * c; }
+    SR_HD u32 last_off(u32 t, u32 u) const { return 5 * C + 2 * (C - 1) * t + 2 * (u < t ? u : u - 1); }
     SR_HD static u32 get(u64 lo, u64 hi, u32 off, u32 w) {
         const u64 v = off >= 64 ? hi >> (off - 64) : (lo >> off) | (off + w > 64 && off ? hi << (64 - off) : 0);
         return (u32)(v & ((1ull << w) - 1));
@@ -388,10 +392,10 @@ struct PaxosHist {
             hi = (hi & ~(m >> k)) | (v & m) >> k;
         }
     }
-    SR_HD u32 phase(u64 lo, u64 hi, u32 c) const { return get(lo, hi, c * fb(), 2); }
-    SR_HD u32 ret(u64 lo, u64 hi, u32 c) const { return get(lo, hi, c * fb() + 2, 3); }
+    SR_HD u32 phase(u64 lo, u64, u32 c) const { return (u32)(lo >> (2 * c)) & 3u; }  // 2C <= 12 bits
+    SR_HD u32 ret(u64 lo, u64 hi, u32 c) const { return get(lo, hi, ret_off(c), 3); }
     // completed-op count of client u when client t invoked its Get
-    SR_HD u32 last(u64 lo, u64 hi, u32 t, u32 u) const { return get(lo, hi, t * fb() + 5 + 2 * (u < t ? u : u - 1), 2); }
+    SR_HD u32 last(u64 lo, u64 hi, u32 t, u32 u) const { return get(lo, hi, last_off(t, u), 2); }
 
     // LinearizabilityTester::serialized_history().is_some() (linearizability.rs:159-240; the host
     // restatement is px::Hist::serialize): a depth-first search for an order of every completed
@@ -471,15 +475,14 @@ struct PaxosHist {
 };
 
 // W = 11 holds the history of up to 4 clients in the 3 x 17 bits the servers leave free; W = 12
-// adds a word for 5 or 6 clients. The history field's last bit (NOT_LIN_BIT) caches "the history
-// is not linearizable" (a function of the history, so still a function of the state): the search
-// runs when a client delivery changes the history, not for every new state's property check.
+// adds a word for 5 or 6 clients. `linearizable` runs the search once per new state (its property
+// check); caching its result in the state, computed at every client delivery, was no faster at 3
+// clients and 9 % slower at 6 (profiles/r04_paxos_lin_ab.txt).
 template <int WW>
 struct PaxosT {
     static constexpr int W = WW, MW = 1, NPROPS = 2;
     static constexpr int NET0 = W - px::SLOTS / 2;  // first network word
     static_assert(NET0 == 3 || NET0 == 4, "servers (+ one history word) then the network");
-    static constexpr u32 NOT_LIN_BIT = NET0 == 3 ? 50u : 114u;  // past the clients' fields (44 / 90 bits)
     int C = 2;
 
     static PaxosT make(int C) {
@@ -516,11 +519,7 @@ struct PaxosT {
     int max_actions() const { return px::SLOTS; }
     int max_out_degree() const { return px::SLOTS; }
     SR_HD static u32 slot(const u64* s, int k) { return (u32)(s[NET0 + k / 2] >> (32 * (k & 1))); }
-    SR_HD u32 phase(const u64* s, int c) const {
-        u64 lo, hi;
-        hist_get(s, lo, hi);
-        return hs().phase(lo, hi, (u32)c);
-    }
+    SR_HD u32 phase(const u64* s, int c) const { return (u32)(s[0] >> (px::SBITS + 2 * c)) & 3u; }
     SR_HD static u64 server_word(const u64* s, u32 i) { return s[i] & px::SMASK; }
 
     // Every envelope is deliverable (model.rs:238-257), but most deliveries are no-ops
@@ -549,11 +548,7 @@ struct PaxosT {
         }
     }
     SR_HD void enabled(const u64* s, u64* m) const {
-        u64 hlo, hhi;
-        hist_get(s, hlo, hhi);
-        const PaxosHist h = hs();
-        u32 phases = 0;
-        for (u32 c = 0; c < (u32)C; ++c) phases |= h.phase(hlo, hhi, c) << (2 * c);
+        const u32 phases = (u32)(s[0] >> px::SBITS);  // the history field starts with the phases
         u64 mk = 0;
 #pragma unroll
         for (int k = 0; k < px::SLOTS; ++k) {
@@ -593,20 +588,21 @@ struct PaxosT {
                 // record_returns (WriteOk), then the Get is sent and recorded by record_invocations
                 out[nout++] = px::env(dst, (dst + 1) % 3, px::GET, 0, 0);  // request 2 * id
                 for (u32 u = 0; u < (u32)C; ++u)
-                    if (u != c) PaxosHist::put(lo, hi, c * h.fb() + 5 + 2 * (u < c ? u : u - 1), 2, h.phase(lo, hi, u));
+                    if (u != c) PaxosHist::put(lo, hi, h.last_off(c, u), 2, h.phase(lo, hi, u));
             } else if (ph == 1 && kind == px::GETOK) {
-                PaxosHist::put(lo, hi, c * h.fb() + 2, 3, px::e_val(e));  // record_returns (ReadOk(v))
+                PaxosHist::put(lo, hi, h.ret_off(c), 3, px::e_val(e));  // record_returns (ReadOk(v))
             } else {
                 return false;
             }
-            PaxosHist::put(lo, hi, c * h.fb(), 2, ph + 1);
-            PaxosHist::put(lo, hi, NOT_LIN_BIT, 1, h.linearizable(lo, hi) ? 0u : 1u);
+            PaxosHist::put(lo, hi, 2 * c, 2, ph + 1);
             hist_set(w, lo, hi);
         }
         // remove the delivered envelope (DuplicatingNetwork::No), then insert what was sent
 #pragma unroll
         for (int k = 0; k < px::SLOTS; ++k) net[k] = k < a ? net[k] : (k + 1 < px::SLOTS ? net[k + 1] : px::EMPTY);
-        for (int j = 0; j < nout; ++j) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {  // (unrolled: out[] and net[] stay in registers)
+            if (j >= nout) break;
             const u32 x = out[j];
             bool dup = false;
 #pragma unroll
@@ -628,10 +624,10 @@ struct PaxosT {
     }
 
     SR_HD bool discovers(int p, const u64* s) const {
-        if (p == 0) {  // always "linearizable" (examples/paxos.rs:251-254): the cached search result
+        if (p == 0) {  // always "linearizable" (examples/paxos.rs:251-254): once per new state
             u64 lo, hi;
             hist_get(s, lo, hi);
-            return PaxosHist::get(lo, hi, NOT_LIN_BIT, 1) != 0;
+            return !hs().linearizable(lo, hi);
         }
         bool any = false;  // sometimes "value chosen" (examples/paxos.rs:255-261)
 #pragma unroll
