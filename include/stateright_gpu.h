@@ -219,7 +219,8 @@ int64_t sr_gpu_bfs_visits(const sr_bfs* bfs, int64_t* out, int64_t cap);
  * state, src/checker/bfs.rs:187-189, src/checker/visitor.rs:19-66): per visit, in the order of
  * sr_gpu_bfs_visits, the visit index of its BFS-tree parent and the canonical id of the first
  * action leading from that parent to it (-1 and -1 for init states). Returns the visit count,
- * or SR_ERR_UNSUPPORTED for the partitioned search. */
+ * or SR_ERR_UNSUPPORTED when the check kept no visit record (record_visits=0). The partitioned
+ * search gathers every rank's records at join, so its tree is global on every rank. */
 int64_t sr_gpu_bfs_visit_tree(const sr_bfs* bfs, int64_t* parent, int64_t* action, int64_t cap);
 void sr_gpu_bfs_free(sr_bfs* bfs);
 

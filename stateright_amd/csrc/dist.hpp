@@ -927,7 +927,7 @@ class DistEngine final : public EngineBase {
         disc.resize(M::NPROPS);
         (void)init_states_of(m_);  // a model with more init states than it declares fails at spawn
         if (model_emask(m))
-            throw Error(SR_ERR_UNSUPPORTED, "partitioned search: `eventually` properties need the FIFO order of one GPU");
+            throw Error(SR_ERR_UNSUPPORTED, "partitioned search: `eventually` properties need a one-GPU check (FIFO or FAST order)");
         T_ = comm_ ? (u32)comm_->world : (u32)std::max(1, virtual_parts);
         if (T_ > (u32)MAX_PARTS) throw Error(SR_ERR_ARG, "at most 64 partitions");
         const u32 L = comm_ ? 1 : T_;
@@ -957,7 +957,7 @@ class DistEngine final : public EngineBase {
     int width() const override { return m_.describe_width(); }
     std::string action_name(i64 id) const override { return m_.action_name(id); }
     i64 action_id_bound() const override { return m_.action_id_bound(); }
-    int init_count() const override { return (int)(init_states_of(base_model(m_)).size() / W); }
+    int init_count() const override { return (int)(init_states_of(base_model(m_)).size() / std::decay_t<decltype(base_model(m_))>::W); }
     int replay(int init, const i64* ids, int n, std::vector<i64>& states, std::vector<int>& conds,
                std::vector<int>* all_conds, int* terminal) const override {
         return replay_model(base_model(m_), init, ids, n, states, conds, all_conds, terminal);
@@ -992,7 +992,7 @@ class DistEngine final : public EngineBase {
                 for (i64 i = prev_base; i < base; ++i) {
                     const u64* ps = &vst_[(size_t)i * W];
                     for_each_successor(m_, ps, [&](int a, const u64* ns) {
-                        first.emplace(fingerprint<W>(ns), std::make_pair(i, m_.action_id(ps, a)));
+                        first.emplace(state_fp<M>(ns), std::make_pair(i, m_.action_id(ps, a)));
                     });
                 }
             }
@@ -1002,7 +1002,7 @@ class DistEngine final : public EngineBase {
                     action.push_back(-1);
                     continue;
                 }
-                auto it = first.find(fingerprint<W>(&vst_[(size_t)(base + i) * W]));
+                auto it = first.find(state_fp<M>(&vst_[(size_t)(base + i) * W]));
                 if (it == first.end()) throw Error(SR_ERR_NONDETERMINISM, "Unable to reconstruct a `Path` for a visited state");
                 parent.push_back(it->second.first);
                 action.push_back(it->second.second);
@@ -1328,6 +1328,8 @@ class DistEngine final : public EngineBase {
         state_count = 0;
         unique = 0;
         max_depth = 0;
+        reference_done = false;
+        early_exit_ = false;
         for (auto& d : disc) d = DiscoveryRec{};
         disc_at_.assign(M::NPROPS, DiscAt{});
         stats = sr_stats{};
@@ -1532,7 +1534,10 @@ class DistEngine final : public EngineBase {
                 stats.records_routed += recs;
             }
             prev_glob_n = glob_n;
-            if (glob_n == 0) break;  // frontier exhausted everywhere
+            if (glob_n == 0) {  // frontier exhausted everywhere: `is_done` (bfs.rs:307-311)
+                reference_done = true;
+                break;
+            }
             if (level > lvl0_) unique_total += glob_n;  // every state is in exactly one frontier
             max_depth = level;
             unique = unique_total;
@@ -2100,7 +2105,10 @@ class DistEngine final : public EngineBase {
                 have_rows = true;
             }
             glob_prev_ = glob_n;
-            if (glob_n == 0) break;  // frontier exhausted everywhere
+            if (glob_n == 0) {  // frontier exhausted everywhere: `is_done` (bfs.rs:307-311)
+                reference_done = true;
+                break;
+            }
             if (level > lvl0_) unique_total += glob_n;
             max_depth = level;
             unique = unique_total;

@@ -25,6 +25,15 @@ static int two_phase_owner_rms(int n) {
 
 // The registry below instantiates `E<Model>` for every model; the single-GPU engine and the
 // partitioned engine share it.
+// A model with `eventually` properties runs partitioned as EvBits<Model> (models.hpp).
+template <template <class> class E, class M, class... Args>
+static std::unique_ptr<EngineBase> engine_for(const M& m, const sr_opts& o, Args... args) {
+    if constexpr (std::is_same<E<M>, DistEngine<M>>::value && has_emask<M>::value) {
+        if (model_emask(m)) return std::make_unique<DistEngine<EvBits<M>>>(EvBits<M>(m), o, args...);
+    }
+    return std::make_unique<E<M>>(m, o, args...);
+}
+
 template <template <class> class E, class... Args>
 static std::unique_ptr<EngineBase> make_model_engine(int model, const i64* p, int np, const sr_opts& o, Args... args) {
     auto need = [&](int k) {
@@ -60,7 +69,7 @@ static std::unique_ptr<EngineBase> make_model_engine(int model, const i64* p, in
             if (p[0] <= Paxos::max_clients()) return std::make_unique<E<Paxos>>(Paxos::make((int)p[0]), o, args...);
             return std::make_unique<E<PaxosWide>>(PaxosWide::make((int)p[0]), o, args...);
         case SR_MODEL_DGRAPH:
-            return std::make_unique<E<DGraph>>(DGraph::make(p, np, o.device), o, args...);
+            return engine_for<E>(DGraph::make(p, np, o.device), o, args...);
         case SR_MODEL_PINGPONG: {
             need(1);
             if (p[0] < 0 || p[0] > 7) throw Error(SR_ERR_UNSUPPORTED, "ping-pong: max_nat must be in 0..=7 (16 network slots)");
@@ -69,7 +78,7 @@ static std::unique_ptr<EngineBase> make_model_engine(int model, const i64* p, in
             m.lossy = np > 1 && p[1] != 0;
             m.duplicating = np > 2 ? p[2] != 0 : true;
             m.maintains_history = np > 3 && p[3] != 0;
-            return std::make_unique<E<PingPong>>(m, o, args...);
+            return engine_for<E>(m, o, args...);
         }
         case SR_MODEL_ACTOR_FIXTURE: {
             need(1);
@@ -489,7 +498,7 @@ int64_t sr_gpu_bfs_visit_tree(const sr_bfs* b, int64_t* parent, int64_t* action,
         if (!b) return SR_ERR_ARG;
         std::vector<i64> p, a;
         if (!b->e->visit_tree(p, a)) {
-            set_error("this engine keeps no visit record (partitioned search)");
+            set_error("this check kept no visit record (sr_opts.record_visits = 0)");
             return SR_ERR_UNSUPPORTED;
         }
         const size_t n = std::min<size_t>((size_t)std::max<int64_t>(cap, 0), p.size());

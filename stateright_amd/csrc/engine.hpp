@@ -165,7 +165,7 @@ int explore_model(const M& m, const u64* fps, int n, std::vector<i64>& action, s
     auto emit = [&](i64 a, const u64* s) {
         action.push_back(a);
         has.push_back(s ? 1 : 0);
-        fp_out.push_back(s ? fingerprint<W>(s) : 0);
+        fp_out.push_back(s ? state_fp<M>(s) : 0);
         const size_t o = states.size();
         states.resize(o + wd, 0);
         if (s) m.describe(s, &states[o]);
@@ -178,7 +178,7 @@ int explore_model(const M& m, const u64* fps, int n, std::vector<i64>& action, s
     }
     std::vector<u64> cur;
     for (int i = 0; i < k && cur.empty(); ++i)
-        if (fingerprint<W>(&inits[i * W]) == fps[0]) cur.assign(&inits[i * W], &inits[i * W] + W);
+        if (state_fp<M>(&inits[i * W]) == fps[0]) cur.assign(&inits[i * W], &inits[i * W] + W);
     if (cur.empty()) return -1;
     for (int j = 1; j < n; ++j) {
         u64 mask[M::MW];
@@ -188,7 +188,7 @@ int explore_model(const M& m, const u64* fps, int n, std::vector<i64>& action, s
             for (u64 bits = mask[w]; bits && !found; bits &= bits - 1) {
                 const int a = w * 64 + __builtin_ctzll(bits);
                 u64 ns[W];
-                if (m.apply(cur.data(), a, ns) && fingerprint<W>(ns) == fps[j]) {
+                if (m.apply(cur.data(), a, ns) && state_fp<M>(ns) == fps[j]) {
                     cur.assign(ns, ns + W);
                     found = true;
                 }
@@ -211,10 +211,11 @@ int explore_model(const M& m, const u64* fps, int n, std::vector<i64>& action, s
 
 // The model a host-side walk runs on: the original model under the canonical symmetry reduction
 // (Canon<M> steps through orbit representatives; replay, the Explorer and discovery paths speak of
-// concrete states of the original model), the model itself otherwise.
+// concrete states of the original model) and under EvBits<M> (whose extra word is the search's
+// bookkeeping), the model itself otherwise.
 template <class M>
 decltype(auto) base_model(const M& m) {
-    if constexpr (is_canon<M>::value) return m.base();
+    if constexpr (is_canon<M>::value || is_evbits<M>::value) return m.base();
     else return (m);
 }
 
@@ -290,7 +291,7 @@ int fingerprint_chain(const M& m, const std::vector<u64>& st, std::vector<u64>& 
     } else {
         raw = st;
     }
-    for (size_t i = 0; i < raw.size() / W; ++i) out.push_back(fingerprint<W>(&raw[i * W]));
+    for (size_t i = 0; i < raw.size() / W; ++i) out.push_back(state_fp<M>(&raw[i * W]));
     return (int)out.size();
 }
 
@@ -406,7 +407,7 @@ class Engine final : public EngineBase {
     }
 
     i64 action_id_bound() const override { return m_.action_id_bound(); }
-    int init_count() const override { return (int)(init_states_of(base_model(m_)).size() / W); }
+    int init_count() const override { return (int)(init_states_of(base_model(m_)).size() / std::decay_t<decltype(base_model(m_))>::W); }
     // replay and the Explorer walk concrete states of the original model (under Canon<M> too)
     int replay(int init, const i64* ids, int n, std::vector<i64>& states, std::vector<int>& conds,
                std::vector<int>* all_conds, int* terminal) const override {
@@ -443,7 +444,7 @@ class Engine final : public EngineBase {
                 const u64 pr = par[i];
                 if (pr >= prev_states.size() / W) throw Error(SR_ERR_NONDETERMINISM, "visit parent outside the visited prefix");
                 const u64* ps = &prev_states[pr * W];
-                const u64 want = fingerprint<W>(&st[i * W]);
+                const u64 want = state_fp<M>(&st[i * W]);
                 u64 mask[M::MW];
                 m_.enabled(ps, mask);
                 i64 id = -1;
@@ -451,7 +452,7 @@ class Engine final : public EngineBase {
                     for (u64 bits = mask[w]; bits && id < 0; bits &= bits - 1) {
                         const int a = w * 64 + __builtin_ctzll(bits);
                         u64 ns[W];
-                        if (m_.apply(ps, a, ns) && fingerprint<W>(ns) == want) id = m_.action_id(ps, a);
+                        if (m_.apply(ps, a, ns) && state_fp<M>(ns) == want) id = m_.action_id(ps, a);
                     }
                 if (id < 0) throw Error(SR_ERR_NONDETERMINISM, "Unable to reconstruct a `Path` for a visited state");
                 parent.push_back(prev_base + (i64)pr);
@@ -1362,7 +1363,7 @@ int described_fingerprint(const M& m, const i64* d, int width, u64* fp) {
         if (!d || !fp || width != m.describe_width()) return SR_ERR_ARG;
         u64 s[M::W];
         m.undescribe(d, s);
-        *fp = fingerprint<M::W>(s);
+        *fp = state_fp<M>(s);
         return SR_OK;
     } else {
         (void)m, (void)d, (void)width, (void)fp;
@@ -1395,7 +1396,10 @@ void* plugin_create(Make make, const int64_t* p, int32_t np, const sr_opts* opts
                 throw Error(SR_ERR_UNSUPPORTED, "symmetry reduction: the plugin model has no `canonical`");
             }
         } else if (comm || vparts > 1) {
-            e = new DistEngine<M>(m, o, static_cast<Comm*>(comm), (int)vparts);
+            if constexpr (has_emask<M>::value) {
+                if (model_emask(m)) e = new DistEngine<EvBits<M>>(EvBits<M>(m), o, static_cast<Comm*>(comm), (int)vparts);
+            }
+            if (!e) e = new DistEngine<M>(m, o, static_cast<Comm*>(comm), (int)vparts);
         } else {
             e = new Engine<M>(m, o);
         }

@@ -174,7 +174,7 @@ SR_HD ProbeKey probe_key(const M& m, const TableView& t, const u64* s) {
     if constexpr (has_qkey<M>::value && M::W >= 2) {
         if (t.qbits) return quot_probe(t, qperm(m.qkey(s), t.bbits));
     }
-    return fp_probe(t, fingerprint<M::W>(s));
+    return fp_probe(t, state_fp<M>(s));
 }
 
 constexpr u32 NO_PARENT = 0xffffffffu;

@@ -380,7 +380,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W <
                 // (the same value in fingerprint mode; the host turns the filter and the sent
                 // cache off for a quotient-mode table)
                 pk[j] = ok[j] ? probe_key(m, t, ns[j]) : ProbeKey{0, 0};
-                key[j] = !ok[j] ? 0 : t.qbits ? fingerprint<W>(ns[j]) : pk[j].tag;
+                key[j] = !ok[j] ? 0 : t.qbits ? state_fp<M>(ns[j]) : pk[j].tag;
                 if (fmask && ok[j]) {  // block-local duplicate filter (see expand_fast)
                     const u64 old = atomicExch(reinterpret_cast<unsigned long long*>(&filt[(u32)(key[j] >> 40) & fmask]),
                                                (unsigned long long)key[j]);
@@ -895,7 +895,7 @@ __global__ void insert_roots_part(M m, TableView t, const u64* states, u32 n, u3
     for (u32 r = 0; r < n; ++r) {
         u64 s[M::W];
         load_state<M::W>(states, r, s);
-        u64 key = fingerprint<M::W>(s);
+        u64 key = state_fp<M>(s);
         if (part_of(m, s, key, nparts) != my_part) continue;
         bool is_new;
         find_or_claim(t, probe_key(m, t, s), &is_new, &lc->err);
@@ -920,7 +920,7 @@ __global__ void take_owned(M m, const u64* __restrict__ hstates, u32 total, u32 
     u64 s[M::W];
     if (i < total) {
         load_state<M::W>(hstates, i, s);
-        const u64 fp = fingerprint<M::W>(s);
+        const u64 fp = state_fp<M>(s);
         mine = part_of(m, s, fp, nparts) == my_part;
         if (mine) find_or_claim(t, probe_key(m, t, s), &nw, &lc->err);
     }

@@ -156,6 +156,75 @@ SR_HD u64 fingerprint(const u64* s) {
     }
 }
 
+// Words of a state that its fingerprint covers: M::FPW when the model declares it (EvBits<M>: the
+// last word is bookkeeping that rides with the state but is not part of it), else all W. Every
+// fingerprint the engines compute (visited set, partition owner, discovery chains) goes through
+// state_fp, so an EvBits<M> state has the fingerprint of the M state it wraps.
+template <class M, class = void>
+struct fp_words_of : std::integral_constant<int, M::W> {};
+template <class M>
+struct fp_words_of<M, std::void_t<decltype(M::FPW)>> : std::integral_constant<int, M::FPW> {};
+template <class M>
+SR_HD u64 state_fp(const u64* s) {
+    return fingerprint<fp_words_of<M>::value>(s);
+}
+
+// `eventually` properties for the PARTITIONED search (src/checker/bfs.rs:52-60,212-222,265-272):
+// the EventuallyBits of a pending state ride in one extra word of it, so the records the ranks
+// exchange carry them and the owner's claim keeps the claiming generator's bits (the FAST order's
+// rule of the one-GPU engine, kernels.hpp expand_fast naeb). A successor gets its parent's bits
+// minus the eventually properties whose condition holds at the parent (the parent's pop), and an
+// eventually property is discovered at a state that still carries its bit, where its condition
+// does not hold and that has no successor within boundary (a terminal state, bfs.rs:265-272).
+// The engine sees no `eventually` property (emask() == 0): such a discovery is an ordinary
+// discovery of the new state, with its path.  The visited set and every fingerprint cover the
+// wrapped state only (FPW), so a state reached with two different bit words is ONE state, as in
+// the reference (bfs.rs:235-246: the first generator's bits win).
+template <class M>
+struct EvBits : M {
+    static constexpr int W = M::W + 1, FPW = M::W;
+    u32 ev_props_ = 0;  // the wrapped model's eventually properties
+    EvBits() = default;
+    explicit EvBits(const M& m) : M(m), ev_props_(model_emask(m)) {}
+    const M& base() const { return *this; }
+    u32 emask() const { return 0; }
+    SR_HD u32 holds(const u64* s) const {
+        u32 h = 0;
+        for (u32 e = ev_props_; e; e &= e - 1)
+            if (M::discovers(__builtin_ctz(e), s)) h |= 1u << __builtin_ctz(e);
+        return h;
+    }
+    SR_HD bool apply(const u64* s, int a, u64* o) const {
+        if (!M::apply(s, a, o)) return false;
+        o[M::W] = s[M::W] & ~(u64)holds(s);
+        return true;
+    }
+    SR_HD bool discovers(int p, const u64* s) const {
+        if (!(ev_props_ >> p & 1)) return M::discovers(p, s);
+        if (!(s[M::W] >> p & 1) || M::discovers(p, s)) return false;
+        u64 mask[M::MW];
+        M::enabled(s, mask);
+        for (int w = 0; w < M::MW; ++w)
+            for (u64 bits = mask[w]; bits; bits &= bits - 1) {
+                u64 t[M::W];
+                if (M::apply(s, w * 64 + __builtin_ctzll(bits), t)) return false;
+            }
+        return true;
+    }
+    int init_states(u64* out) const {
+        const int k = M::init_states(out);
+        for (int i = k - 1; i >= 0; --i) {
+            for (int w = M::W - 1; w >= 0; --w) out[i * W + w] = out[i * M::W + w];
+            out[i * W + M::W] = ev_props_;
+        }
+        return k;
+    }
+};
+template <class M>
+struct is_evbits : std::false_type {};
+template <class M>
+struct is_evbits<EvBits<M>> : std::true_type {};
+
 SR_HD u64 getb(const u64* s, int off, int width) {
     // bit field [off, off+width) of a little-endian multi-word state; width <= 8, no word crossing
     return (s[off >> 6] >> (off & 63)) & ((1ull << width) - 1);

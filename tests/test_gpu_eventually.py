@@ -5,7 +5,9 @@ The GPU keeps one EventuallyBits word per frontier state, finds each level's ter
 reproduces the reference's overwrite-at-terminal semantics in its FIFO order (the default for
 eventually models). An explicit FAST order gives each state the bits of the generator that claims
 it, one of the reference's multi-threaded orders: its discoveries are valid counterexamples, and
-on graphs without joins (where no order can lose one) the same as the oracle's.
+on graphs without joins (where no order can lose one) the same as the oracle's. The partitioned
+search carries the bits in an extra word of every state and record (models.hpp EvBits), with the
+same claiming-generator rule.
 """
 import random
 
@@ -78,10 +80,78 @@ def test_random_graphs_match_oracle(expectation):
             assert c.discovery("odd").into_states() == o.discovery_states("odd"), paths
 
 
-def test_partitioned_rejects_eventually():
-    g = sr.DGraph.with_property(EVENTUALLY).with_path([0, 1])
-    with pytest.raises(sr.CheckerError):
-        g.checker().partitions(2).spawn_bfs().join()
+def _graph(paths):
+    g = sr.DGraph.with_property(EVENTUALLY)
+    for p in paths:
+        g = g.with_path(p)
+    return g
+
+
+@pytest.mark.parametrize("head", ["0", "65536"])
+@pytest.mark.parametrize("parts", [2, 3])
+def test_partitioned_eventually_matches_oracle_without_joins(parts, head, monkeypatch):
+    # The partitioned search carries each state's EventuallyBits in an extra word of its records
+    # (models.hpp EvBits): the claiming generator's bits, as in FAST order on one GPU. On graphs
+    # without joins every order finds the oracle's discoveries; a check without one explores
+    # everything, with the oracle's counts.
+    monkeypatch.setenv("SR_HEAD_MAX", head)
+    rng = random.Random(99 + parts)
+    for _ in range(40):
+        paths = _chains(rng)
+        o = OracleRun(DGRAPH, dgraph_params(EVENTUALLY, paths))
+        c = _graph(paths).checker().partitions(parts).spawn_bfs().join()
+        assert sorted(c.discoveries()) == o.discovery_names(), paths
+        for name, path in c.discoveries().items():
+            c.assert_discovery(name, path.action_ids)
+        if not o.discovery_names():
+            assert (c.unique_state_count(), c.state_count(), c.max_depth()) == (
+                o.unique_state_count, o.state_count, o.max_depth), paths
+
+
+def test_partitioned_eventually_reference_cases(monkeypatch):
+    # src/checker.rs:358-398 on 2 and 3 partitions, from level 0 (no replicated head)
+    monkeypatch.setenv("SR_HEAD_MAX", "0")
+    for parts in (2, 3):
+        _graph([[1], [2, 3], [2, 6, 7], [4, 9, 10]]).checker().partitions(parts).spawn_bfs().join().assert_properties()
+        for paths, last in ([[[0, 1], [0, 2]], 2], [[[0, 1], [2, 4]], 4]):
+            c = _graph(paths).checker().partitions(parts).spawn_bfs().join()
+            assert c.discovery("odd").last_state() == (last,)
+            c.assert_discovery("odd", c.discovery("odd").action_ids)
+        c = _graph([[0, 1, 4, 6], [2, 4, 8]]).checker().partitions(parts).spawn_bfs().join()
+        assert c.discovery("odd").last_state() in ((6,), (8,))
+        c.assert_discovery("odd", c.discovery("odd").action_ids)
+
+
+@pytest.mark.parametrize("parts", [2, 4])
+def test_partitioned_eventually_discoveries_are_valid(parts, monkeypatch):
+    # graphs with joins: whatever the partitioned order reports is a valid counterexample
+    monkeypatch.setenv("SR_HEAD_MAX", "0")
+    rng = random.Random(2024 + parts)
+    for _ in range(40):
+        paths = _random_graph(rng)
+        c = _graph(paths).checker().partitions(parts).spawn_bfs().join()
+        for name, path in c.discoveries().items():
+            c.assert_discovery(name, path.action_ids)
+
+
+def test_partitioned_eventually_ranks(monkeypatch):
+    # in-process ranks (the exchange between ranks carries the bit word with the state)
+    monkeypatch.setenv("SR_HEAD_MAX", "0")
+    from stateright_amd.distributed import Communicator
+    paths = [[0, 2, 4, 6], [1, 3], [8, 10, 12]]
+    o = OracleRun(DGRAPH, dgraph_params(EVENTUALLY, paths))
+    comms = Communicator.local_group(2)
+    try:
+        cs = [_graph(paths).checker().comm(cm).spawn_bfs() for cm in comms]
+        for c in cs:
+            c.join()
+        for c in cs:
+            assert sorted(c.discoveries()) == o.discovery_names()
+            c.assert_discovery("odd", c.discovery("odd").action_ids)
+        cs.clear()
+    finally:
+        for cm in comms:
+            cm.close()
 
 
 def test_assert_discovery_eventually():

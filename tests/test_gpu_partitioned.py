@@ -46,6 +46,7 @@ def test_partitioned_counts_match_oracle(case, parts):
     assert c.state_count() == o.state_count
     assert c.max_depth() == o.max_depth
     assert sorted(c.discoveries()) == o.discovery_names()
+    assert c.is_done() == o.is_done  # explored everything, or discovered every property
 
 
 @pytest.mark.parametrize("parts", [2, 3, 8])
