@@ -5,6 +5,7 @@
 
 #include <chrono>
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -117,12 +118,18 @@ class DevicePool {
         auto raw = [&]() {
             return kind == 1 ? hipExtMallocWithFlags(&p, bytes, hipDeviceMallocFinegrained) : hipMalloc(&p, bytes);
         };
+        const auto t0 = std::chrono::steady_clock::now();
         hipError_t e = raw();
-        if (e != hipSuccess) {
+        const bool retried = e != hipSuccess;
+        if (retried) {
             release_all(dev);  // retry once with the cache emptied
             (void)hipGetLastError();
             SR_HIP(raw());
         }
+        if (trace())
+            std::fprintf(stderr, "[pool] device %d: %zu bytes (kind %d) fresh%s in %.3f ms\n", dev, bytes, kind,
+                         retried ? " after emptying the cache" : "",
+                         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
         return p;
     }
     void free(int dev, void* p, size_t bytes, int kind = 0) {
@@ -182,6 +189,12 @@ class DevicePool {
                 }
                 v.clear();
             }
+    }
+    // SR_POOL_TRACE=1: every fresh device allocation on stderr (size, whether the cache had to be
+    // emptied first, and its duration).
+    static bool trace() {
+        static const bool on = std::getenv("SR_POOL_TRACE") && std::atoi(std::getenv("SR_POOL_TRACE")) != 0;
+        return on;
     }
     static size_t round(size_t b) {
         if (b < 256) return 256;

@@ -497,6 +497,7 @@ class Engine final : public EngineBase {
     // (cand) are remapped to the new table, since the rehash moves every entry.
     // min_slots: grow to at least this many slots (one rehash, however many doublings that is).
     void grow_table(u32* cand = nullptr, u64 cand_n = 0, u64 min_slots = 0) {
+        const auto tg = Clock::now();
         DBuf<u64> ok, om;
         ok.swap(keys_);
         if (fifo_) om.swap(meta_);
@@ -522,6 +523,9 @@ class Engine final : public EngineBase {
         }
         SR_HIP(stream_sync(stream_));
         stats.rehashes++;
+        if (o_.verbose)
+            std::fprintf(stderr, "[sr] visited set %llu -> %llu slots in %.3f ms\n", (unsigned long long)old_cap,
+                         (unsigned long long)cap_, secs(tg, Clock::now()) * 1e3);
     }
 
     // Growth during a check (no capacity hint, or one too small: the path a user of the reference
@@ -567,6 +571,7 @@ class Engine final : public EngineBase {
     // by copying the used prefix.
     void ensure_arena(u64 states, u64 used) {
         if (arena_cap_ >= states) return;
+        const auto ta = Clock::now();
         // (growth steps of 4: each copies the arena so far and stops the level pipeline)
         u64 cap = std::max<u64>(states, arena_cap_ * (arena_cap_ ? 4 : 1));
         DBuf<u64> na;
@@ -574,6 +579,7 @@ class Engine final : public EngineBase {
         na.alloc(o_.device, cap * W);
         np.alloc(o_.device, cap);
         if (emask_) ne.alloc(o_.device, cap);
+        const double alloc_ms = secs(ta, Clock::now()) * 1e3;
         if (used) {
             SR_HIP(hipMemcpyAsync(na.p, arena_.p, used * W * sizeof(u64), hipMemcpyDeviceToDevice, stream_));
             SR_HIP(hipMemcpyAsync(np.p, apar_.p, used * sizeof(u32), hipMemcpyDeviceToDevice, stream_));
@@ -587,6 +593,9 @@ class Engine final : public EngineBase {
         // the old buffers go back to the pool when na/np/ne leave scope: wait until no enqueued work
         // reads them (a first allocation has none, and the start of a check does not wait here)
         if (had) SR_HIP(stream_sync(stream_));
+        if (o_.verbose && had)
+            std::fprintf(stderr, "[sr] arena -> %llu states (%llu copied) in %.3f ms (allocation %.3f ms)\n",
+                         (unsigned long long)cap, (unsigned long long)used, secs(ta, Clock::now()) * 1e3, alloc_ms);
     }
 
     void bind(Ctx* c) {
@@ -657,8 +666,9 @@ class Engine final : public EngineBase {
         }
         std::atomic_thread_fence(std::memory_order_acquire);
         std::memcpy(&lc_, (const void*)&ctx_->hc[seq & 1], sizeof(lc_));
-        if (recoverable && lc_.err == ERR_TABLE_FULL) return false;
+        if (recoverable && (lc_.err == ERR_TABLE_FULL || lc_.err == ERR_DEFERRED)) return false;
         if (lc_.err & ERR_TABLE_FULL) throw Error(SR_ERR_CAPACITY, "visited set probe limit exceeded");
+        if (lc_.err & ERR_DEFERRED) throw Error(SR_ERR_CAPACITY, "deferred level");
         if (lc_.err & ERR_FRONTIER_OVERFLOW) throw Error(SR_ERR_CAPACITY, "frontier overflow");
         return true;
     }
@@ -757,6 +767,7 @@ class Engine final : public EngineBase {
         if (o_.capacity_hint)
             while ((double)cap * std::min(load, max_load(cap)) < (double)o_.capacity_hint * grow_factor_) cap <<= 1;
         ratio_ = (double)D_;
+        nratio_ = 0;
         en_ratio_ = std::max(1.0, (double)D_ / 2.0);
         alloc_table(cap);
 
@@ -995,12 +1006,13 @@ class Engine final : public EngineBase {
             stats.algorithmic_bytes += n * 8 * W + c.successors * 8 + produced * (16 + 8 * W);
             stats.levels++;
             ratio_ = (double)produced / (double)n;
+            note_ratio(ratio_);
             en_ratio_ = std::max(1.0, (double)c.enabled / (double)n);
             lvisited_.push_back(n);
             if (o_.verbose)
-                std::fprintf(stderr, "[sr] level %u: frontier %llu succ %llu new %llu unique %llu cap %llu%s\n", level,
+                std::fprintf(stderr, "[sr] level %u: frontier %llu succ %llu new %llu unique %llu cap %llu%s at %.3f ms\n", level,
                              (unsigned long long)n, (unsigned long long)c.successors, (unsigned long long)produced,
-                             (unsigned long long)unique.load(), (unsigned long long)cap_, how);
+                             (unsigned long long)unique.load(), (unsigned long long)cap_, how, secs(vt0_, Clock::now()) * 1e3);
             if (produced == 0) {  // exhausted (a speculative launch saw an empty frontier)
                 reference_done = true;
                 return false;
@@ -1024,6 +1036,7 @@ class Engine final : public EngineBase {
             return true;
         };
         u32 sq = sq_level0;  // enqueued before the roots' outcome was read
+        vt0_ = Clock::now();
         for (;;) {
             // enqueue the next level before waiting for this one
             const double g = std::max(ratio_, 1.0) * 1.5;
@@ -1039,9 +1052,22 @@ class Engine final : public EngineBase {
 
             bool spec_ok = spec;
             if (!wait_publish(sq, true)) {  // lc_ = this level's counters
-                // the level overflowed the probe limit: double the table, finish the level on it;
+                if (lc_.err == ERR_DEFERRED) {
+                    // a speculative launch whose frontier outgrew the room planned for it expanded
+                    // nothing: the table and the arena are grown for it and it runs again
+                    SR_HIP(stream_sync(stream_));
+                    init_counters();
+                    if (o_.verbose)
+                        std::fprintf(stderr, "[sr] level of %llu states outgrew the room planned for it: deferred\n",
+                                     (unsigned long long)n);
+                    const u32 s2 = launch_sync(n, undiscovered);
+                    publish_pending_slot();
+                    if (!wait_publish(s2, true)) repair_level(lstart_[lstart_.size() - 2], n, undiscovered);
+                } else {
+                    // the level overflowed the probe limit: double the table, finish the level on it
+                    repair_level(lstart_[lstart_.size() - 2], n, undiscovered);
+                }
                 // the enqueued next level saw the error and expanded nothing
-                repair_level(lstart_[lstart_.size() - 2], n, undiscovered);
                 spec_ok = false;
             }
             auto it = seq_launch_.find(sq);
@@ -1090,7 +1116,7 @@ class Engine final : public EngineBase {
     // Launch of the level whose frontier (n states) ends the arena, after the previous one is done:
     // the visited set and the arena are grown first if the level might not fit.
     u32 launch_sync(u64 n, u32 undiscovered) {
-        const u64 d_eff = pessimistic_ ? D_ : std::min<u64>(D_, (u64)std::ceil(2.0 * ratio_ + 1.0));
+        const u64 d_eff = pessimistic_ ? D_ : std::min<u64>(D_, (u64)std::ceil(2.0 * recent_ratio() + 1.0));
         const double need = (double)(unique + n * d_eff);
         if (need > lmax_ * (double)cap_) grow_table(nullptr, 0, growth_slots((u64)(need / lmax_) + 1));
         const u64 fbase = lstart_[lstart_.size() - 2];
@@ -1128,6 +1154,11 @@ class Engine final : public EngineBase {
         // a slotted launch: it counts into its own slot and is published by its successor
         SlotWork sw = slot_work(dev_n);
         sw.flags = flags;
+        if (dev_n) {  // speculative: the device checks its frontier against the room left (ERR_DEFERRED)
+            const double room = lmax_ * (double)cap_ - (double)unique.load();
+            sw.room = room > 0 ? (u64)room : 0ull;
+            sw.gmul = (u32)std::min(64.0 * 256.0, std::ceil(std::max(recent_ratio(), 1.0) * 1.5 * 256.0));
+        }
         LevelCounters* lc = slot(slot_k_);
         const u32 svc = sw.pub || sw.zero ? 1u : 0u;  // the extra service workgroup (SlotWork)
         timed([&] {
@@ -1329,6 +1360,14 @@ class Engine final : public EngineBase {
     bool pessimistic_ = false;  // size chunks for max out-degree new states per parent
     u64 grow_factor_ = 1;       // initial-capacity multiplier after a capacity restart
     double ratio_ = 1.0;        // new states per expanded parent in the last level
+    double ratios_[4] = {};     // ... in the last four levels (a model's growth can be periodic:
+    u32 nratio_ = 0;            // increment_lock grows x5 every fourth level)
+    void note_ratio(double r) { ratios_[nratio_++ & 3] = r; }
+    double recent_ratio() const {
+        double m = ratio_;
+        for (u32 i = 0; i < std::min<u32>(nratio_, 4); ++i) m = std::max(m, ratios_[i]);
+        return m;
+    }
     double en_ratio_ = 8.0;     // enabled action slots per expanded parent in the last level
     double table_load_ = 0.5;
     bool load_env_ = false;
@@ -1339,6 +1378,7 @@ class Engine final : public EngineBase {
     u64 cap_ = 0;
     DBuf<u64> keys_, meta_;      // visited set
     double lmax_ = 0.8;          // growth threshold of the current table (max_load)
+    Clock::time_point vt0_{};    // verbose log: start of the level loop
     DBuf<u32> aux_;              // [0] rehash error bits, [1] max displacement (displacement_stats)
     DBuf<u64> arena_;            // BFS tree: every level's states in visit order
     DBuf<u32> apar_;             // parent rank (in the previous level) of each arena state

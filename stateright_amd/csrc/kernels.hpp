@@ -47,7 +47,9 @@ constexpr int MAX_PARTS = 64;  // visited-set partitions (one per GPU, or virtua
 
 // ERR_EXCHANGE: the direct exchange delivered a receive slot whose sequence tag or checksum does
 // not match what its source stored (kernels_dist.hpp): the check is redone on the collective exchange.
-enum ErrBits { ERR_TABLE_FULL = 1, ERR_FRONTIER_OVERFLOW = 2, ERR_PEER_TIMEOUT = 4, ERR_EXCHANGE = 8 };
+// ERR_DEFERRED: a speculative launch found its frontier too large for the room the host left in the
+// visited set or the arena and expanded nothing (the host grows them and launches the level again).
+enum ErrBits { ERR_TABLE_FULL = 1, ERR_FRONTIER_OVERFLOW = 2, ERR_PEER_TIMEOUT = 4, ERR_EXCHANGE = 8, ERR_DEFERRED = 16 };
 
 // Two slot encodings ("Visited set"):
 //  * fingerprint mode (qbits == 0): a slot holds the 64-bit fingerprint. Exact for one-word states
@@ -390,6 +392,13 @@ struct SlotWork {
     // reference's first insertion, src/checker/bfs.rs:246-263, in a multi-threaded order)
     const u32* peb = nullptr;
     u32* naeb = nullptr;
+    // Speculative launches (prev_n): the visited-set slots the host can still fill below its growth
+    // threshold, and a bound on new states per parent (x 256). A frontier of nn states for which
+    // nn * (1 + g) exceeds that room, or nn * g the arena left after it, is not expanded (ERR_DEFERRED):
+    // the host's plan assumed a smaller frontier, and overfilling a linear-probe table makes every
+    // probe walk long runs (increment_lock's x5 levels: a 4 M-slot table at 0.78 load, then past it).
+    u64 room = 0;
+    u32 gmul = 0;  // 0: no check
 };
 
 // One wave (lane = 0..63): publish sw.pub to sw.hc, then reset sw.zero.
@@ -755,7 +764,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W >
         // that failed (its err word, loaded with its claims) it expands nothing: the host repairs
         // or restarts that level and its frontier is not final.
         const u64 ce = __hip_atomic_load(reinterpret_cast<const u64*>(sw.prev_n), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const u32 nn = (ce >> 32) ? 0u : (u32)ce;
+        u32 nn = (ce >> 32) ? 0u : (u32)ce;
+        if (sw.gmul && nn) {
+            const u64 grow = ((u64)nn * sw.gmul) >> 8;
+            const u64 left = next_cap > nn ? (u64)(next_cap - nn) : 0ull;
+            if ((u64)nn + grow > sw.room || grow > left) {
+                nn = 0;
+                if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(&lc->err, (u32)ERR_DEFERRED);
+            }
+        }
         hi = lo + nn;
         next += (u64)nn * W;
         next_par += nn;

@@ -237,6 +237,19 @@ def test_increment_lock_quotient_table_grows(order):
     assert c.stats()["rehashes"] > 0
 
 
+def test_increment_lock_grows_through_x5_levels():
+    # No hint, increment_lock N=10 (39 M states): every fourth level has five times the states of
+    # the one before, so a speculative launch planned from the last level's growth meets a frontier
+    # five times larger than planned. It must expand nothing (ERR_DEFERRED) and run again on a grown
+    # table, not overfill a small quotient table (kernels.hpp SlotWork.room); counts stay exact.
+    n = 10
+    expect = 1 + 4 * sum(math.factorial(n) // math.factorial(n - k) for k in range(1, n + 1))
+    c = sr.IncrementLock(n).checker().order("fast").spawn_bfs().join()
+    assert c.unique_state_count() == c.state_count() == expect
+    assert c.max_depth() == 4 * n
+    assert c.stats()["rehashes"] > 0
+
+
 def test_2pc_10_fifo_matches_fast():
     # The exact-order pipeline at a BASELINE size: same counts as FAST, same closed forms.
     n = 10
