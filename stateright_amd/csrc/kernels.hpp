@@ -755,9 +755,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W >
     // size (any row below next_cap is inside the arena; rows past the frontier are never used), so
     // the two round trips overlap instead of following each other.
     const u64 r_first = lo + (u64)blockIdx.x * chunk + ((u64)wid << ppw_log2) + lane;
-    u64 first[W];
+    u64 nxt[W];  // the wave's parents of its next chunk (here: its first)
     const bool spec_first = sw.prev_n && lane < (int)ppw && r_first < next_cap;
-    if (spec_first) load_state<W>(frontier, r_first, first);
+    if (spec_first) load_state<W>(frontier, r_first, nxt);
     if (sw.prev_n) {
         // Pipelined launch (enqueued before the host saw the previous level finish): the frontier
         // is the previous level's claims, and the next level starts right after it. Behind a level
@@ -789,13 +789,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W >
     // The wave's parents of the next chunk are loaded one chunk ahead: their latency overlaps this
     // chunk's probes instead of stalling the chunk start.
     const u64 cstride = (u64)nblk * chunk;
-    u64 nxt[W];
-    if (spec_first) {
-#pragma unroll
-        for (int i = 0; i < W; ++i) nxt[i] = first[i];
-    } else if (lane < (int)ppw && r_first < hi) {
-        load_state<W>(frontier, r_first, nxt);
-    }
+    if (!spec_first && lane < (int)ppw && r_first < hi) load_state<W>(frontier, r_first, nxt);
     for (u64 c0 = lo + (u64)blockIdx.x * chunk; c0 < hi; c0 += cstride) {
         const u32 wave0 = (u32)(c0 + ((u64)wid << ppw_log2));  // first parent of the wave
         const u32 r = wave0 + lane;
