@@ -71,10 +71,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--model", default="2pc", choices=["2pc", "paxos", "increment_lock"],
+    ap.add_argument("--model", default="2pc", choices=["2pc", "paxos", "increment_lock", "single_copy"],
                     help="workload (the BASELINE metric is 2pc; the others are side measurements)")
     ap.add_argument("--rm-count", type=int, default=9)
-    ap.add_argument("--clients", type=int, default=3, help="paxos client_count")
+    ap.add_argument("--clients", type=int, default=3, help="paxos / single_copy client_count")
     ap.add_argument("--threads", type=int, default=10, help="increment_lock thread count")
     ap.add_argument("--order", default="fast", choices=["fast", "fifo"])
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU restatement (rank 0, N=1)")
@@ -159,6 +159,8 @@ def cpu_baseline(args, n):
     threads = args.cpu_threads or usable
     if args.model == "paxos":
         cmd, what = ["paxos", str(args.clients)], f"paxos C={args.clients}"
+    elif args.model == "single_copy":
+        cmd, what = ["single_copy", str(args.clients)], f"single-copy register C={args.clients}"
     elif args.model == "increment_lock":
         cmd, what = ["increment_lock", str(min(args.threads, 9))], f"increment_lock N={min(args.threads, 9)}"
     else:
@@ -297,7 +299,7 @@ def main():
 
     import math
 
-    from stateright_amd import IncrementLock, Paxos, TwoPhaseSys
+    from stateright_amd import IncrementLock, Paxos, SingleCopyRegister, TwoPhaseSys
     from stateright_amd import _native as N
     lib = N.load()
     # one GPU per rank: LOCAL_RANK when every rank sees the node's GPUs; a launcher that restricts
@@ -318,6 +320,10 @@ def main():
         make = lambda: Paxos(args.clients)  # noqa: E731
         expect_unique = {1: 265, 2: 16_668, 3: 1_194_428, 4: 2_372_188, 5: 4_711_569, 6: 9_357_525}[args.clients]
         label = f"paxos C={args.clients}"
+    elif args.model == "single_copy":  # the reference's bench.sh: `single-copy-register check 4`
+        make = lambda: SingleCopyRegister(args.clients, 1)  # noqa: E731
+        expect_unique = {1: 5, 2: 93, 3: 4_243, 4: 400_233}[args.clients]
+        label = f"single-copy register C={args.clients}"
     elif args.model == "increment_lock":
         t = args.threads
         make = lambda: IncrementLock(t)  # noqa: E731

@@ -61,7 +61,8 @@ enum sr_model_id {
     SR_MODEL_PINGPONG = 9,        /* (max_nat<=7, lossy, duplicating, maintains_history)
                                      src/actor/actor_test_util.rs:4-96                     */
     SR_MODEL_ACTOR_FIXTURE = 10,  /* (kind: 0 undeliverable envelope, 1 timer) src/actor/model.rs:697-733 */
-    SR_MODEL_ABD = 11             /* (client_count<=3, server_count<=3) examples/linearizable-register.rs */
+    SR_MODEL_ABD = 11,            /* (client_count<=3, server_count<=3) examples/linearizable-register.rs */
+    SR_MODEL_SINGLE_COPY = 12     /* (client_count<=6, server_count; <=8 actors) examples/single-copy-register.rs */
 };
 
 /* Visit order inside a BFS level. */
@@ -280,7 +281,9 @@ int32_t sr_device_synchronize(int32_t device);
 int32_t sr_selftest_tables(void);
 /* Host-only self-check of the compiled-in model encodings: every slot a model's optional
  * `self_loops` reports (counted by the FAST expansion without being generated) is enabled and
- * returns the state itself, over every reachable state of 2pc N=1..7 (and its canonical form).
+ * returns the state itself, over every reachable state of 2pc N=1..7 (and its canonical form);
+ * and the register clients' linearizability test (paxos, single-copy register) agrees with the
+ * tester's serialization search on random histories of 1..6 clients.
  * SR_OK or SR_ERR_ARG (sr_last_error says where). */
 int32_t sr_selftest_models(void);
 /* comm == NULL: `virtual_partitions` partitions in this process on opts->device (same protocol;

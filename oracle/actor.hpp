@@ -698,9 +698,104 @@ struct AbdSys {
     }
 };
 
+// ---------------------------------------------------------------------------------------------
+// Single-copy register (examples/single-copy-register.rs): SingleCopyActor servers (one register
+// value each, no consensus) wrapped by RegisterActor::Server, RegisterActor::Client clients with
+// put_count 1 (src/actor/register.rs:119-217), a non-duplicating lossless network, a
+// LinearizabilityTester<Id, Register<char>> history. Messages are ABD's Put / Get / PutOk / GetOk.
+// ---------------------------------------------------------------------------------------------
+struct SingleCopySys {
+    static constexpr int NET = 8;
+    using AState = AbdActorState;  // server: val; client: awaiting, op_count
+    using Msg = AbdMsg;
+    using Hist = paxos::History;
+    size_t client_count = 2, server_count = 1;
+    bool lossy = false, duplicating = false;  // `.duplicating_network(DuplicatingNetwork::No)`
+
+    size_t actor_count() const { return server_count + client_count; }
+    std::vector<Envelope<Msg>> init_network() const { return {}; }
+    Hist init_history() const { return Hist{}; }
+    AState on_start(Id id, Out<Msg>& o) const {
+        AState s;
+        if (id < server_count) return s;  // SingleCopyActor::on_start: Value::default()
+        // RegisterActor::Client::on_start, put_count 1 (register.rs:130-160)
+        s.server = false;
+        const u64 req = 1 * id;
+        o.send(id % server_count, Msg{A_PUT, req, {}, (char)('A' + (id - server_count))});
+        s.awaiting = req;
+        s.op_count = 1;
+        return s;
+    }
+    bool on_msg(Id id, AState& st, Id src, const Msg& m, Out<Msg>& o) const {
+        if (!st.server) {  // RegisterActor::Client::on_msg (register.rs:170-200)
+            if (!st.awaiting) return false;
+            if (m.kind == A_PUTOK && m.req == *st.awaiting) {
+                const u64 req = (st.op_count + 1) * id;
+                o.send((id + st.op_count) % server_count, Msg{A_GET, req, {}, 0});
+                st.awaiting = req;
+                st.op_count += 1;
+                return true;
+            }
+            if (m.kind == A_GETOK && m.req == *st.awaiting) {
+                st.awaiting.reset();
+                st.op_count += 1;
+                return true;
+            }
+            return false;
+        }
+        // SingleCopyActor::on_msg (examples/single-copy-register.rs:26-37)
+        if (m.kind == A_PUT) {
+            st.val = m.val;  // `*state.to_mut() = value`
+            o.send(src, Msg{A_PUTOK, m.req, {}, 0});
+            return true;
+        }
+        if (m.kind == A_GET) {
+            o.send(src, Msg{A_GETOK, m.req, {}, st.val});
+            return false;
+        }
+        return false;
+    }
+    bool on_timeout(Id, AState&, Out<Msg>&) const { return false; }
+    std::optional<Hist> record_out(const Hist& h, const Envelope<Msg>& e) const { return AbdSys{}.record_out(h, e); }
+    std::optional<Hist> record_in(const Hist& h, const Envelope<Msg>& e) const { return AbdSys{}.record_in(h, e); }
+    template <class State>
+    bool within_boundary(const State&) const { return true; }
+    template <class M>
+    std::vector<Property<M>> properties() const {  // examples/single-copy-register.rs:63-74
+        return AbdSys{}.properties<M>();
+    }
+    void hash_actor(const AState& a, Hasher& h) const {
+        h.write_bool(a.server);
+        if (a.server) {
+            h.write_u64((u8)a.val);
+        } else {
+            h.write_bool(a.awaiting.has_value());
+            h.write_u64(a.awaiting.value_or(0));
+            h.write_u64(a.op_count);
+        }
+    }
+    void hash_history(const Hist& H, Hasher& h) const { AbdSys{}.hash_history(H, h); }
+    void hash_msg(const Msg& m, Hasher& h) const { AbdSys{}.hash_msg(m, h); }
+    i64 msg_code(const Msg& m) const { return AbdSys{}.msg_code(m); }
+    // per actor: server [value code, 0]; client [awaiting (-1 None), op_count]
+    int actor_width() const { return 2; }
+    void describe_actor(Id, const AState& a, std::vector<i64>& d) const {
+        if (a.server) {
+            d.push_back(AbdSys::vcode(a.val));
+            d.push_back(0);
+        } else {
+            d.push_back(a.awaiting ? (i64)*a.awaiting : -1);
+            d.push_back((i64)a.op_count);
+        }
+    }
+    void describe_history(const Hist&, std::vector<i64>&) const {}  // summarised by `linearizable`
+    std::string format_msg(const Msg& m) const { return AbdSys{}.format_msg(m); }
+};
+
 using PingPongModel = ActorModel<PingPongSys>;
 using FixtureModel = ActorModel<FixtureSys>;
 using AbdModel = ActorModel<AbdSys>;
+using SingleCopyModel = ActorModel<SingleCopySys>;
 
 }  // namespace actor
 }  // namespace oracle

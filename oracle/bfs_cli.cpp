@@ -6,6 +6,7 @@
 
 #include "models.hpp"
 #include "paxos.hpp"
+#include "actor.hpp"
 
 using namespace oracle;
 
@@ -27,7 +28,7 @@ int run(M m, size_t threads, u64 target) {
 
 int main(int argc, char** argv) {
     if (argc < 3) {
-        std::cerr << "usage: bfs_cli <2pc|increment|increment_lock|linear_equation> <N> [threads] [target]\n";
+        std::cerr << "usage: bfs_cli <2pc|increment|increment_lock|linear_equation|paxos|single_copy> <N> [threads] [target]\n";
         return 2;
     }
     std::string model = argv[1];
@@ -39,6 +40,12 @@ int main(int argc, char** argv) {
     if (model == "increment_lock") return run(IncrementLock{n}, threads, target);
     if (model == "paxos") return run(paxos::PaxosModel{n, 3}, threads, target);
     if (model == "linear_equation") return run(LinearEquation{2, 4, 7}, threads, target);
+    if (model == "single_copy") {  // examples/single-copy-register.rs `check N`: N clients, 1 server
+        actor::SingleCopyModel m;
+        m.sys.client_count = n;
+        m.sys.server_count = 1;
+        return run(std::move(m), threads, target);
+    }
     std::cerr << "unknown model " << model << "\n";
     return 2;
 }

@@ -14,7 +14,7 @@ thread_local std::string g_last_error;
 
 // Model ids are shared with include/stateright_gpu.h (SR_MODEL_*).
 enum ModelId { LINEAR_EQUATION = 1, BINARY_CLOCK = 2, TWO_PHASE = 3, INCREMENT = 4, INCREMENT_LOCK = 5, DGRAPH = 6, PAXOS = 7, SYM_TOY = 8,
-               PINGPONG = 9, ACTOR_FIXTURE = 10, ABD = 11 };
+               PINGPONG = 9, ACTOR_FIXTURE = 10, ABD = 11, SINGLE_COPY = 12 };
 
 struct HandleBase {
     virtual ~HandleBase() = default;
@@ -168,6 +168,12 @@ auto with_model(int model, const i64* p, int np, F&& f) {
             actor::AbdModel m;
             m.sys.client_count = (size_t)p[0];
             m.sys.server_count = np > 1 ? (size_t)p[1] : 2;
+            return f(m);
+        }
+        case SINGLE_COPY: {  // (client_count, server_count)
+            actor::SingleCopyModel m;
+            m.sys.client_count = (size_t)p[0];
+            m.sys.server_count = np > 1 ? (size_t)p[1] : 1;
             return f(m);
         }
     }

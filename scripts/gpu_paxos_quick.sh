@@ -1,8 +1,14 @@
+#!/bin/bash
+# Quick GPU timing of the register models (paxos C=3 and 6, single-copy register C=4) and the
+# headline 2pc N=9 (no CPU baseline, no side legs): one line each.
 set -o pipefail
 mkdir -p gpurun_out/px
-for c in 3 6; do
-  timeout -k 10 200 python -u bench.py --model paxos --clients $c --steps 10 --warmup 3 --cpu-baseline 0 --config4-steps 0 --no-hint-steps 0 > gpurun_out/px/p$c.json 2> gpurun_out/px/p$c.err || { tail -5 gpurun_out/px/p$c.err; exit 1; }
-  python3 -c "import json; d=json.loads(open('gpurun_out/px/p$c.json').read().strip().splitlines()[-1]); print('paxos $c', round(d['ms_per_step'],3), [round(x,1) for x in d['levels']['kernel_us']])"
-done
-timeout -k 10 200 python -u bench.py --steps 20 --warmup 3 --cpu-baseline 0 --config4-steps 0 --no-hint-steps 0 > gpurun_out/px/b.json 2> gpurun_out/px/b.err || exit 1
-python3 -c "import json; d=json.loads(open('gpurun_out/px/b.json').read().strip().splitlines()[-1]); print('2pc9', round(d['ms_per_step'],3), d['levels']['small_levels_ms'])"
+run() {  # name, bench args
+    local name=$1; shift
+    timeout -k 10 200 python -u bench.py "$@" --cpu-baseline 0 --config4-steps 0 --no-hint-steps 0 > gpurun_out/px/$name.json 2> gpurun_out/px/$name.err || { tail -5 gpurun_out/px/$name.err; exit 1; }
+    python3 -c "import json; d=json.loads(open('gpurun_out/px/$name.json').read().strip().splitlines()[-1]); l=d.get('levels') or {}; print('$name', round(d['ms_per_step'],3), 'small', round(l.get('small_levels_ms', 0), 3), [round(x,1) for x in l.get('kernel_us', [])][:40])"
+}
+run paxos3 --model paxos --clients 3 --steps 10 --warmup 3
+run paxos6 --model paxos --clients 6 --steps 5 --warmup 2
+run single_copy4 --model single_copy --clients 4 --steps 10 --warmup 3
+run 2pc9 --steps 20 --warmup 3

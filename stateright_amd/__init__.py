@@ -10,8 +10,8 @@ include/stateright_gpu.h; this package is the host-side mirror of the reference 
 """
 from .checker import CheckerBuilder, CheckerError, Expectation, GpuBfsChecker, Path, PathRecorder, StateRecorder
 from .models import (AbdRegister, ActorFixture, BinaryClock, DGraph, Increment, IncrementLock, LinearEquation, Paxos,
-                     PingPong, TwoPhaseSys)
+                     PingPong, SingleCopyRegister, TwoPhaseSys)
 
 __all__ = ["CheckerBuilder", "CheckerError", "Expectation", "GpuBfsChecker", "Path", "PathRecorder", "StateRecorder",
            "AbdRegister", "ActorFixture", "BinaryClock", "DGraph", "Increment", "IncrementLock", "LinearEquation", "Paxos",
-           "PingPong", "TwoPhaseSys"]
+           "PingPong", "SingleCopyRegister", "TwoPhaseSys"]

@@ -20,6 +20,7 @@ SR_MODEL_PAXOS = 7
 SR_MODEL_PINGPONG = 9
 SR_MODEL_ACTOR_FIXTURE = 10
 SR_MODEL_ABD = 11
+SR_MODEL_SINGLE_COPY = 12
 
 SR_ORDER_AUTO, SR_ORDER_FIFO, SR_ORDER_FAST = 0, 1, 2
 SR_ALWAYS, SR_EVENTUALLY, SR_SOMETIMES = 0, 1, 2

@@ -5,6 +5,7 @@
 //   PingPongSys   ping-pong (src/actor/actor_test_util.rs:4-96), lossy / duplicating options
 //   FixtureSys    the undeliverable-message and timer fixtures (src/actor/model.rs:697-733)
 //   AbdSys        the ABD linearizable register (examples/linearizable-register.rs)
+//   SingleCopySys the single-copy register (examples/single-copy-register.rs)
 // The CPU restatement the encodings are tested against is oracle/actor.hpp.
 //
 // State: W = AW + K/2 words.
@@ -585,10 +586,130 @@ struct AbdSys {
     }
 };
 
+// ---------------------------------------------------------------------------------------------
+// Single-copy register (examples/single-copy-register.rs): S SingleCopyActor servers (ids 0..S-1,
+// one register value each, no consensus) wrapped by RegisterActor::Server, C RegisterActor clients
+// (ids S..S+C-1, put_count 1), a non-duplicating lossless network, a LinearizabilityTester<Id,
+// Register<char>> history. A client's state follows from its history phase (0: awaiting PutOk(id),
+// 1: awaiting GetOk(2 id), 2: done), so the history holds the clients' whole state:
+//   word 0     server i's value at [3i, 3i + 3) ('\0' 0, 'A'.. 1..)
+//   words 1-2  the history (paxos.hpp PaxosHist: phases, returned values, Get `last` vectors;
+//              the same client protocol as paxos', so its device-side linearizability search)
+// Message (the oracle's key order (kind, req, val)): kind << 12 | req << 4 | val. Each client has
+// at most one message in flight, so K = 6 slots hold up to 6 clients.
+// ---------------------------------------------------------------------------------------------
+struct SingleCopySys {
+    static constexpr int K = 6, AW = 3, NACT = 8, NPROPS = 2, NET = 8;
+    enum Kind : u32 { PUT, GET, PUTOK, GETOK };
+    u32 S = 1, C = 2;
+    bool lossy = false, duplicating = false;
+
+    static SingleCopySys make(int clients, int servers) {
+        if (clients < 1 || clients > 6 || servers < 1 || clients + servers > NACT)
+            throw Error(SR_ERR_UNSUPPORTED, "single-copy register: client_count in 1..=6, client_count + server_count <= 8");
+        SingleCopySys m;
+        m.C = (u32)clients;
+        m.S = (u32)servers;
+        return m;
+    }
+    SR_HD u32 nact() const { return S + C; }
+    SR_HD PaxosHist hs() const {
+        PaxosHist h;
+        h.C = C;
+        return h;
+    }
+    static SR_HD u32 msg(u32 kind, u32 req, u32 val) { return kind << 12 | req << 4 | val; }
+    static SR_HD u32 value(const u64* s, u32 i) { return (u32)(s[0] >> (3 * i)) & 7u; }
+
+    SR_HD void init_network(Out&, u32&) const {}
+    SR_HD void on_start(u64*, u32 id, Out& out) const {
+        // servers: Value::default(); clients: RegisterActor::Client::on_start (register.rs:130-160)
+        if (id >= S && id < S + C) out.send(id % S, msg(PUT, id, id - S + 1));  // Put(1 x id, 'A' + index)
+    }
+    SR_HD bool on_msg(u64* o, u32 id, u32 src, u32 m, Out& out) const {
+        const u32 kind = m >> 12, req = m >> 4 & 255;
+        if (id >= S) {  // RegisterActor::Client::on_msg (register.rs:170-200): the phase is the awaited reply
+            const u32 ph = hs().phase(o[1], o[2], id - S);
+            if (ph == 0 && kind == PUTOK && req == id) {
+                out.send((id + 1) % S, msg(GET, 2 * id, 0));  // Get((op_count + 1) x id) to (id + op_count) % S
+                return true;
+            }
+            return ph == 1 && kind == GETOK && req == 2 * id;
+        }
+        // SingleCopyActor::on_msg (examples/single-copy-register.rs:26-37)
+        if (kind == PUT) {
+            o[0] = (o[0] & ~(7ull << (3 * id))) | (u64)(m & 7) << (3 * id);  // `*state.to_mut() = value`
+            out.send(src, msg(PUTOK, req, 0));
+            return true;
+        }
+        if (kind == GET) {
+            out.send(src, msg(GETOK, req, value(o, id)));
+            return false;
+        }
+        return false;
+    }
+    SR_HD bool on_timeout(u64*, u32, Out&) const { return false; }
+    // RegisterMsg::record_returns / record_invocations (src/actor/register.rs:37-87) on the history
+    // field: PutOk returns WriteOk and the client's Get invocation follows in the same delivery (its
+    // `last` vector: every other client's completed ops); GetOk(v) returns ReadOk(v).
+    SR_HD void record_in(u64* o, u32, u32 dst, u32 m) const {
+        const u32 kind = m >> 12;
+        if (dst < S || (kind != PUTOK && kind != GETOK)) return;
+        const u32 c = dst - S;
+        const PaxosHist h = hs();
+        u64 lo = o[1], hi = o[2];
+        const u32 ph = h.phase(lo, hi, c);
+        if (kind == PUTOK) {
+            for (u32 u = 0; u < C; ++u)
+                if (u != c) PaxosHist::put(lo, hi, h.last_off(c, u), 2, h.phase(lo, hi, u));
+        } else {
+            PaxosHist::put(lo, hi, h.ret_off(c), 3, m & 7);
+        }
+        PaxosHist::put(lo, hi, 2 * c, 2, ph + 1);
+        o[1] = lo;
+        o[2] = hi;
+    }
+    SR_HD void record_out(u64*, u32, u32, u32) const {}  // the Puts at start: phase 0; Gets: in record_in
+    SR_HD bool within_boundary(const u64*) const { return true; }
+    SR_HD bool discovers(int p, const u64* s, const u32* net) const {
+        if (p == 0) return !hs().linearizable(s[1], s[2]);  // always "linearizable"
+        bool any = false;                                   // sometimes "value chosen"
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const u32 e = net[k];
+            any |= e != EMPTY && (e_msg(e) >> 12) == GETOK && (e & 7) != 0;
+        }
+        return any;
+    }
+    int expectation(int p) const { return p == 0 ? ALWAYS : SOMETIMES; }
+    const char* prop_name(int p) const { return p == 0 ? "linearizable" : "value chosen"; }
+    // the oracle's msg code (AbdSys::msg_code with seq (0, Id(0))): ((req * 512 + val) * 8 + kind)
+    i64 msg_code(u32 m) const { return ((i64)(m >> 4 & 255) * 512 + (i64)(m & 7)) * 8 + (i64)(m >> 12); }
+    std::string format_msg(i64 code) const { return AbdSys{}.format_msg(code); }
+    int actors_width() const { return (int)(2 * (S + C)); }
+    static int history_width() { return 0; }
+    // oracle/actor.hpp SingleCopySys::describe_actor: server [value, 0]; client [awaiting, op_count]
+    int describe_fields(const u64* s, i64* d) const {
+        int k = 0;
+        for (u32 id = 0; id < S + C; ++id) {
+            if (id < S) {
+                d[k++] = value(s, id);
+                d[k++] = 0;
+            } else {
+                const u32 ph = hs().phase(s[1], s[2], id - S);
+                d[k++] = ph == 0 ? (i64)id : ph == 1 ? (i64)(2 * id) : -1;
+                d[k++] = (i64)ph + 1;
+            }
+        }
+        return k;
+    }
+};
+
 }  // namespace act
 
 using PingPong = act::ActorGpu<act::PingPongSys>;
 using ActorFixture = act::ActorGpu<act::FixtureSys>;
 using AbdRegister = act::ActorGpu<act::AbdSys>;
+using SingleCopyRegister = act::ActorGpu<act::SingleCopySys>;
 
 }  // namespace sr

@@ -93,6 +93,12 @@ static std::unique_ptr<EngineBase> make_model_engine(int model, const i64* p, in
             static_cast<act::AbdSys&>(m) = act::AbdSys::make((int)p[0], np > 1 ? (int)p[1] : 2, o.device);
             return std::make_unique<E<AbdRegister>>(m, o, args...);
         }
+        case SR_MODEL_SINGLE_COPY: {
+            need(1);
+            SingleCopyRegister m;
+            static_cast<act::SingleCopySys&>(m) = act::SingleCopySys::make((int)p[0], np > 1 ? (int)p[1] : 1);
+            return std::make_unique<E<SingleCopyRegister>>(m, o, args...);
+        }
     }
     throw Error(SR_ERR_ARG, "unknown model id " + std::to_string(model));
 }
@@ -743,8 +749,54 @@ int32_t sr_selftest_tables(void) {
     return SR_OK;
 }
 
+// PaxosHist::linearizable (the cluster-graph test) against PaxosHist::linearizable_search (the
+// tester's serialization search) on random histories of the register clients' protocol (every
+// client: Write invoked at init; on its completion the Read is invoked, recording how many ops every
+// other client had completed; the Read completes with any value): all client counts 1..6.
+static bool check_linearizability(std::string& why) {
+    u64 x = 0x9E3779B97F4A7C15ull;
+    auto rnd = [&]() { return x = fmix64(x + 0x632BE59BD9B4E019ull); };
+    for (u32 C = 1; C <= px::MAX_CLIENTS; ++C) {
+        PaxosHist h;
+        h.C = C;
+        u32 nonlin = 0;
+        for (int it = 0; it < 40000; ++it) {
+            u64 lo = 0, hi = 0;
+            const u32 steps = (u32)(rnd() % (2 * C + 1));
+            for (u32 k = 0; k < steps; ++k) {
+                const u32 t = (u32)(rnd() % C), ph = h.phase(lo, hi, t);
+                if (ph == 0) {
+                    for (u32 u = 0; u < C; ++u)
+                        if (u != t) PaxosHist::put(lo, hi, h.last_off(t, u), 2, h.phase(lo, hi, u));
+                } else if (ph == 1) {
+                    PaxosHist::put(lo, hi, h.ret_off(t), 3, rnd() % (C + 1));
+                } else {
+                    continue;
+                }
+                PaxosHist::put(lo, hi, 2 * t, 2, ph + 1);
+            }
+            const bool a = h.linearizable(lo, hi), b = h.linearizable_search(lo, hi);
+            nonlin += !b;
+            if (a != b) {
+                why = "linearizability: C=" + std::to_string(C) + " history " + std::to_string(lo) + "/" + std::to_string(hi) +
+                      ": cluster test " + std::to_string(a) + ", search " + std::to_string(b);
+                return false;
+            }
+        }
+        if (C >= 2 && nonlin == 0) {
+            why = "linearizability: no non-linearizable history drawn at C=" + std::to_string(C);
+            return false;
+        }
+    }
+    return true;
+}
+
 int32_t sr_selftest_models(void) {
     std::string why;
+    if (!check_linearizability(why)) {
+        set_error(why);
+        return SR_ERR_ARG;
+    }
     for (int n = 1; n <= 7; ++n) {
         TwoPhase m;
         m.n = n;

@@ -403,7 +403,48 @@ struct PaxosHist {
     // client t: 0 = Write(t's letter) (completed from phase 1, with no real-time predecessor),
     // 1 = Read (in flight in phase 1 with predecessors from `last`, completed in phase 2). Threads
     // are tried in id order, completed ops before an in-flight one, as the reference does.
+    // `linearizable` without a search. Every Write has its own value (client t writes t + 1), so a
+    // serialization is a sequence of CLUSTERS: first the Reads of the initial value (cluster 0),
+    // then, per written value v, Write(v) directly followed by the Reads that returned v (no other
+    // Write can come between them, and no Read of another value either), Writes nobody read being
+    // clusters of their own and pending ops left out (a pending Read changes nothing, a pending
+    // Write nobody read only overwrites). Real-time order only runs INTO Reads (every Write is
+    // invoked at init): Write(u) precedes Read(t) when u's Write had completed at t's invocation
+    // (t's own Write always), Read(u) precedes Read(t) when both of u's ops had. A serialization
+    // exists iff no such edge enters cluster 0 from another cluster and the edges between the
+    // value clusters have no cycle (a topological order of the clusters, each cluster in real-time
+    // order inside, is one). O(C^2) bit operations instead of a search whose interleavings grow
+    // factorially (a single-copy register with 4 clients: 4.6 ms for one history on a host core).
+    // Checked against the search (`linearizable_search`) on every history of the paxos and
+    // single-copy state spaces and on random histories (sr_selftest_models).
     SR_HD bool linearizable(u64 lo, u64 hi) const {
+        u64 in = 0;  // byte b: the clusters that must precede cluster b (bit a)
+        for (u32 t = 0; t < C; ++t) {
+            if (phase(lo, hi, t) != 2) continue;  // completed Reads only
+            const u32 r = ret(lo, hi, t);
+            auto edge = [&](u32 a) {
+                if (a != r) in |= 1ull << (8 * r + a);
+            };
+            edge(t + 1);
+            for (u32 u = 0; u < C; ++u) {
+                if (u == t) continue;
+                const u32 l = last(lo, hi, t, u);
+                if (l >= 1) edge(u + 1);
+                if (l >= 2) edge(ret(lo, hi, u));
+            }
+        }
+        if (in & 0xffull) return false;  // an op of a value cluster before a Read of the initial value
+        u32 alive = ((1u << (C + 1)) - 1) & ~1u;
+        while (alive) {
+            u32 rm = 0;
+            for (u32 b = 1; b <= C; ++b)
+                if ((alive >> b & 1) && !((u32)(in >> (8 * b)) & alive & 0xffu)) rm |= 1u << b;
+            if (!rm) return false;  // the clusters left form a cycle
+            alive &= ~rm;
+        }
+        return true;
+    }
+    SR_HD bool linearizable_search(u64 lo, u64 hi) const {
         // No completed Read: the completed ops are Writes invoked together at init, unordered in
         // real time, and any order of them (in-flight ops left out) is a valid serialization.
         // Packed scalars only (2-bit fields per client, 8-bit frames): an array indexed by client
@@ -415,6 +456,13 @@ struct PaxosHist {
             any_read |= p == 2;
         }
         if (!any_read) return true;
+        // In-flight ops worth placing: a pending Read never helps (it changes nothing and may
+        // return anything), and a pending Write only helps if some completed Read returned its
+        // value. Leaving the others out keeps the existence of a serialization (the tester's
+        // `is_some()`) and removes their interleavings from the search.
+        u32 wanted = 0;  // bit t: some completed Read returned client t's value
+        for (u32 t = 0; t < C; ++t)
+            if (phase(lo, hi, t) == 2 && ret(lo, hi, t)) wanted |= 1u << (ret(lo, hi, t) - 1);
         auto f2 = [](u32 v, u32 t) { return v >> (2 * t) & 3u; };
         u32 next = 0, used = 0;  // next op of client t at bits 2t; in-flight op used: bit t
         u64 fl = 0, fh = 0;      // frames (8 bits each): thread | kind << 3 | register before << 4
@@ -438,7 +486,8 @@ struct PaxosHist {
             for (u32 t = t0; t < C && !found; ++t) {
                 const u32 n = f2(next, t), d = f2(done, t);
                 if (n == d) {
-                    if (d == 2 || (used >> t & 1) || violates(t, d)) continue;  // in-flight op: index d
+                    // in-flight op: index d (a Write only when wanted, never a Read)
+                    if (d != 0 || !(wanted >> t & 1) || (used >> t & 1)) continue;
                     push(t, 1);
                     used |= 1u << t;
                     if (d == 0) reg = t + 1;  // a Write takes effect; a Read returns anything

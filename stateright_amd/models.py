@@ -179,6 +179,20 @@ class ActorFixture(_Model):
         return [self.kind]
 
 
+class SingleCopyRegister(_Model):
+    """The single-copy register `SingleCopyModelCfg { client_count, server_count }.into_model()`
+    (examples/single-copy-register.rs:40-78): SingleCopyActor servers (a register value each, no
+    consensus), RegisterActor clients, a non-duplicating network and a linearizability history.
+    Its `check` CLI uses one server (linearizable); two or more are not linearizable."""
+    MODEL_ID = N.SR_MODEL_SINGLE_COPY
+
+    def __init__(self, client_count=2, server_count=1):
+        self.client_count, self.server_count = client_count, server_count
+
+    def params(self):
+        return [self.client_count, self.server_count]
+
+
 class AbdRegister(_Model):
     """The ABD linearizable register `AbdModelCfg { client_count, server_count }.into_model()`
     (examples/linearizable-register.rs:192-229): AbdActor servers, RegisterActor clients, a

@@ -7,9 +7,11 @@ Sources (reference repository):
   resets_timer       src/actor/model.rs:709-733
   Explorer status    src/checker/explorer.rs:370-416
   ABD register       examples/linearizable-register.rs:236-279
-Model ids are shared with include/stateright_gpu.h (SR_MODEL_PINGPONG / _ACTOR_FIXTURE / _ABD).
+  single-copy reg.   examples/single-copy-register.rs:80-118
+Model ids are shared with include/stateright_gpu.h (SR_MODEL_PINGPONG / _ACTOR_FIXTURE / _ABD /
+_SINGLE_COPY).
 """
-PINGPONG, ACTOR_FIXTURE, ABD = 9, 10, 11
+PINGPONG, ACTOR_FIXTURE, ABD, SINGLE_COPY = 9, 10, 11, 12
 
 # ---- envelope codes: (msg code * 128 + dst) * 16 + src ---------------------------------------
 def env_code(msg_code, src, dst):
@@ -109,4 +111,27 @@ ABD_VALUE_CHOSEN_NAMES = [
     "Deliver { src: Id(1), dst: Id(0), msg: Internal(AckQuery(6, (1, Id(1)), 'B')) }",
     "Deliver { src: Id(0), dst: Id(1), msg: Internal(Record(6, (1, Id(1)), 'B')) }",
     "Deliver { src: Id(1), dst: Id(0), msg: Internal(AckRecord(6)) }",
+]
+
+# ---- single-copy register (examples/single-copy-register.rs) ------------------------------------
+# Its messages are ABD's Put / Get / PutOk / GetOk (abd_msg with seq (0, Id(0))).
+# :91-96 (2 clients, 1 server, DFS; unique_state_count 93): "value chosen"
+SINGLE_COPY_VALUE_CHOSEN_1 = [
+    abd_deliver(2, 0, abd_msg(A_PUT, 2, val="B")),
+    abd_deliver(0, 2, abd_msg(A_PUTOK, 2)),
+    abd_deliver(2, 0, abd_msg(A_GET, 4)),
+]
+# :104-109 (2 clients, 2 servers, BFS): "linearizable" is violated
+SINGLE_COPY_NOT_LINEARIZABLE_2 = [
+    abd_deliver(3, 1, abd_msg(A_PUT, 3, val="B")),
+    abd_deliver(1, 3, abd_msg(A_PUTOK, 3)),
+    abd_deliver(3, 0, abd_msg(A_GET, 6)),
+    abd_deliver(0, 3, abd_msg(A_GETOK, 6, val="\0")),
+]
+# :110-115: "value chosen"
+SINGLE_COPY_VALUE_CHOSEN_2 = [
+    abd_deliver(3, 1, abd_msg(A_PUT, 3, val="B")),
+    abd_deliver(1, 3, abd_msg(A_PUTOK, 3)),
+    abd_deliver(2, 0, abd_msg(A_PUT, 2, val="A")),
+    abd_deliver(3, 0, abd_msg(A_GET, 6)),
 ]

@@ -10,7 +10,8 @@ import urllib.request
 import pytest
 
 from actor_golden import (ABD, ABD_VALUE_CHOSEN_NAMES, ABD_VALUE_CHOSEN_PATH, ACTOR_FIXTURE, PINGPONG, PINGPONG_14,
-                          PINGPONG_DROP_FIRST_PING, pingpong_params)
+                          PINGPONG_DROP_FIRST_PING, SINGLE_COPY, SINGLE_COPY_NOT_LINEARIZABLE_2,
+                          SINGLE_COPY_VALUE_CHOSEN_1, SINGLE_COPY_VALUE_CHOSEN_2, pingpong_params)
 from oracle_lib import OracleRun
 
 pytestmark = pytest.mark.gpu
@@ -23,6 +24,8 @@ def model(mid, params):
                            duplicating=bool(params[2]))
     if mid == ACTOR_FIXTURE:
         return sr.ActorFixture(params[0])
+    if mid == SINGLE_COPY:
+        return sr.SingleCopyRegister(*params)
     return sr.AbdRegister(*params)
 
 
@@ -40,11 +43,18 @@ CASES = [
     (ABD, [2, 2]),
     (ABD, [1, 3]),
     (ABD, [3, 2]),
+    (SINGLE_COPY, [1, 1]),
+    (SINGLE_COPY, [2, 1]),
+    (SINGLE_COPY, [3, 1]),
+    (SINGLE_COPY, [1, 2]),
 ]
+# checks that stop early (every property discovered inside a level): FIFO order only
+EARLY_EXIT = [(SINGLE_COPY, [2, 2]), (SINGLE_COPY, [3, 2]), (SINGLE_COPY, [2, 3])]
 
 
 def ids(c):
-    return {PINGPONG: "pingpong", ACTOR_FIXTURE: "fixture", ABD: "abd"}[c[0]] + "-" + "-".join(map(str, c[1]))
+    return {PINGPONG: "pingpong", ACTOR_FIXTURE: "fixture", ABD: "abd", SINGLE_COPY: "single-copy"}[c[0]] + "-" + \
+        "-".join(map(str, c[1]))
 
 
 _oracle = {}
@@ -68,7 +78,7 @@ def test_counts_match_oracle(case, order):
     assert c.is_done() == o.is_done
 
 
-@pytest.mark.parametrize("case", CASES, ids=ids)
+@pytest.mark.parametrize("case", CASES + EARLY_EXIT, ids=ids)
 def test_fifo_visits_and_paths_identical(case):
     mid, params = case
     o = oracle(mid, params, record_visits=True)
@@ -78,6 +88,45 @@ def test_fifo_visits_and_paths_identical(case):
     for name in o.discovery_names():
         assert c.discovery(name).action_ids == o.discovery_actions(name)
         assert c.discovery(name).states == o.discovery_states(name)
+
+
+@pytest.mark.parametrize("order", ["fifo", "auto"])
+@pytest.mark.parametrize("case", EARLY_EXIT, ids=ids)
+def test_early_exit_counts_match_oracle(case, order):
+    mid, params = case
+    o = oracle(mid, params)
+    c = model(mid, params).checker().order(order).spawn_bfs().join()
+    assert (c.unique_state_count(), c.state_count(), c.max_depth()) == (o.unique_state_count, o.state_count, o.max_depth)
+    assert sorted(c.discoveries()) == o.discovery_names()
+
+
+def test_single_copy_register_goldens():
+    # examples/single-copy-register.rs:80-118: one server is linearizable (93 states, the golden
+    # "value chosen" path); two are not (both golden paths are discoveries).
+    for order in ("fifo", "fast", "auto"):
+        c = sr.SingleCopyRegister(2, 1).checker().order(order).spawn_bfs().join()
+        c.assert_properties()
+        c.assert_discovery("value chosen", SINGLE_COPY_VALUE_CHOSEN_1)
+        assert c.unique_state_count() == 93
+    assert [c.action_name(a) for a in SINGLE_COPY_VALUE_CHOSEN_1] == [
+        "Deliver { src: Id(2), dst: Id(0), msg: Put(2, 'B') }",
+        "Deliver { src: Id(0), dst: Id(2), msg: PutOk(2) }",
+        "Deliver { src: Id(2), dst: Id(0), msg: Get(4) }"]
+    c = sr.SingleCopyRegister(2, 2).checker().spawn_bfs().join()
+    c.assert_discovery("linearizable", SINGLE_COPY_NOT_LINEARIZABLE_2)
+    c.assert_discovery("value chosen", SINGLE_COPY_VALUE_CHOSEN_2)
+
+
+@pytest.mark.parametrize("clients", [3, 4])
+def test_single_copy_register_check(clients):
+    # `single-copy-register check 4` is in the reference's bench.sh (one server): full exploration,
+    # the oracle's counts (and 3 clients)
+    o = oracle(SINGLE_COPY, [clients, 1])
+    c = sr.SingleCopyRegister(clients, 1).checker().spawn_bfs().join()
+    assert (c.unique_state_count(), c.state_count(), c.max_depth()) == (o.unique_state_count, o.state_count, o.max_depth)
+    c.assert_properties()
+    c = sr.SingleCopyRegister(clients, 1).checker().partitions(3).spawn_bfs().join()
+    assert (c.unique_state_count(), c.state_count()) == (o.unique_state_count, o.state_count)
 
 
 def test_pingpong_visits_expected_states():

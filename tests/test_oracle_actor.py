@@ -89,3 +89,23 @@ def test_abd_linearizable_register():
     assert r.discovery_names() == ["value chosen"]  # assert_properties: linearizable holds
     states, holds = replay(ABD, params, ABD_VALUE_CHOSEN_PATH, n_props=2)
     assert holds == [1, 1]  # linearizable, and the value is chosen at the end of the golden path
+
+
+def test_single_copy_register():
+    # examples/single-copy-register.rs:80-118. One server: linearizable, 93 states (DFS and, with no
+    # early exit, BFS) and the golden "value chosen" path. Two servers: not linearizable, both
+    # golden paths are discoveries (the reference's BFS count of 20 stops early in its HashSet
+    # order: parity unpinned).
+    from actor_golden import (SINGLE_COPY, SINGLE_COPY_NOT_LINEARIZABLE_2, SINGLE_COPY_VALUE_CHOSEN_1,
+                              SINGLE_COPY_VALUE_CHOSEN_2)
+    r = OracleRun(SINGLE_COPY, [2, 1], dfs=True)
+    assert r.unique_state_count == 93
+    assert r.discovery_names() == ["value chosen"]
+    assert OracleRun(SINGLE_COPY, [2, 1]).unique_state_count == 93
+    _, holds = replay(SINGLE_COPY, [2, 1], SINGLE_COPY_VALUE_CHOSEN_1, n_props=2)
+    assert holds == [1, 1]
+    _, holds = replay(SINGLE_COPY, [2, 2], SINGLE_COPY_NOT_LINEARIZABLE_2, n_props=2)
+    assert holds[0] == 0  # "linearizable" does not hold: an `always` discovery
+    _, holds = replay(SINGLE_COPY, [2, 2], SINGLE_COPY_VALUE_CHOSEN_2, n_props=2)
+    assert holds[1] == 1
+    assert sorted(OracleRun(SINGLE_COPY, [2, 2]).discovery_names()) == ["linearizable", "value chosen"]
