@@ -32,6 +32,7 @@ if want bench; then
     b bench_paxos3 --model paxos --clients 3 --steps 10 --warmup 3 --cpu-baseline 1 --config4-steps 0 || exit 1
     b bench_paxos6 --model paxos --clients 6 --steps 3 --warmup 1 --cpu-baseline 0 --config4-steps 0 || exit 1
     b bench_2pc11 --rm-count 11 --steps 2 --warmup 1 --cpu-baseline 0 --config4-steps 0 --no-hint-steps 0 || exit 1
+    b bench_single_copy4 --model single_copy --clients 4 --steps 10 --warmup 3 --cpu-baseline 1 --config4-steps 0 || exit 1
 fi
 if want prof; then
     export TMPDIR=/tmp
