@@ -16,7 +16,10 @@ def main():
     import stateright_amd as sr
     from stateright_amd.distributed import Communicator
     comm = Communicator.shm(rank, world, name, device=0, slot_bytes=32 << 20, devices_distinct=distinct)
-    make = {"2pc": lambda n: sr.TwoPhaseSys(n), "inclock": lambda n: sr.IncrementLock(n)}
+    make = {"2pc": lambda n: sr.TwoPhaseSys(n), "inclock": lambda n: sr.IncrementLock(n),
+            # ping-pong on a lossy duplicating network: three `eventually` properties, so the
+            # records carry their EventuallyBits word (models.hpp EvBits)
+            "pingpong": lambda n: sr.PingPong(n, lossy=True)}
     try:
         for spec in sys.argv[5:]:
             model, n = spec.split(":")

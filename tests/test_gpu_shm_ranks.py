@@ -39,15 +39,20 @@ def run_ranks(checks, world=2, distinct=False, env=None, timeout=240):
 
 def expect(spec):
     model, n = spec.split(":")
-    o = OracleRun(TWO_PHASE if model == "2pc" else INCREMENT_LOCK, [int(n)])
+    if model == "pingpong":
+        from actor_golden import PINGPONG, pingpong_params
+        o = OracleRun(PINGPONG, pingpong_params(int(n), lossy=True))
+    else:
+        o = OracleRun(TWO_PHASE if model == "2pc" else INCREMENT_LOCK, [int(n)])
     return o.unique_state_count, o.state_count, o.max_depth, o.discovery_names()
 
 
 @pytest.mark.parametrize("direct", ["1", "0"], ids=["direct", "collective"])
 def test_processes_match_oracle(direct):
     # consecutive checks on the same ranks: the direct exchange's set-up is reused (2pc 5 twice),
-    # grows with a larger check (2pc 7, increment_lock 7) and is reused again
-    checks = ["2pc:5", "2pc:5", "2pc:7", "inclock:7", "2pc:5"]
+    # grows with a larger check (2pc 7, increment_lock 7) and is reused again; ping-pong's
+    # `eventually` properties across processes (one more word per record)
+    checks = ["2pc:5", "2pc:5", "2pc:7", "inclock:7", "2pc:5", "pingpong:5"]
     outs = run_ranks(checks, env={"SR_DIRECT": direct, "SR_HEAD_MAX": "0"})
     for rank_out in outs:
         assert [r["check"] for r in rank_out] == checks
