@@ -929,6 +929,13 @@ class DistEngine final : public EngineBase {
         if (model_emask(m))
             throw Error(SR_ERR_UNSUPPORTED, "partitioned search: `eventually` properties need a one-GPU check (FIFO or FAST order)");
         T_ = comm_ ? (u32)comm_->world : (u32)std::max(1, virtual_parts);
+        // `target_state_count` (bfs.rs:113-135): the reference stops at a 1500-pop block boundary of
+        // its worker order; the partitioned levels have no single pop order, so the check stops at
+        // the first LEVEL boundary where state_count >= target (the levels synchronous, no head).
+        if (o_.target_state_count) {
+            lag_ = false;
+            head_max_ = 0;
+        }
         if (T_ > (u32)MAX_PARTS) throw Error(SR_ERR_ARG, "at most 64 partitions");
         const u32 L = comm_ ? 1 : T_;
         parts_.resize(L);
@@ -1430,6 +1437,7 @@ class DistEngine final : public EngineBase {
             // the replicated head explored everything (or discovered every property)
         } else if (lag_) lag_loop(unique_total, undiscovered);
         else for (u32 level = lvl0_;; ++level) {
+            const bool target_hit = o_.target_state_count && level > lvl0_ && state_count >= o_.target_state_count;
             // ---- 1. expand + route (grid sized from an upper bound of the frontier) ----
             const u64 d_eff = pessimistic_ ? D_ : std::min<u64>(D_, (u64)std::ceil(1.5 * ratio + 1.0));
             for (auto& p : parts_) {
@@ -1500,6 +1508,17 @@ class DistEngine final : public EngineBase {
                 p.lstart.push_back(p.lstart.back() + p.n);  // where the next frontier starts
             }
             if (level == 0) unique_total = glob_roots;  // (a replicated head sets it instead)
+            if (target_hit && glob_n) {
+                // the last level took state_count to the target: its successors are all inserted
+                // (this frontier, generated but never popped: no discovery among them counts),
+                // this expansion is not counted, and the check is not done
+                unique_total += glob_n;
+                max_depth = level;
+                unique = unique_total;
+                reference_done = false;
+                early_exit_ = true;
+                break;
+            }
             // discoveries among this level's states: the lowest (partition, rank) per property
             u32 newly = 0;
             for (int pr = 0; pr < M::NPROPS; ++pr) {

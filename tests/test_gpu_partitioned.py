@@ -64,6 +64,23 @@ def test_batched_insert_counts_match_oracle(case, parts, monkeypatch):
     assert sorted(c.discoveries()) == o.discovery_names()
 
 
+def test_partitioned_target_state_count():
+    # `target_state_count` (src/checker/bfs.rs:113-135): the partitioned search stops at the first
+    # LEVEL boundary at which state_count >= target (the reference's single order has 1500-pop
+    # blocks; the partitions have no single pop order). Level-synchronous, so the counts do not
+    # depend on the partition count; the stop is past the target and short of the full check.
+    n, target = 7, 20_000
+    full = oracle(TWO_PHASE, [n])
+    seen = set()
+    for parts in (2, 3, 5):
+        c = sr.TwoPhaseSys(n).checker().partitions(parts).target_state_count(target).spawn_bfs().join()
+        assert c.state_count() >= target
+        assert c.unique_state_count() < full.unique_state_count
+        assert not c.is_done()
+        seen.add((c.unique_state_count(), c.state_count(), c.max_depth()))
+    assert len(seen) == 1, seen
+
+
 @pytest.mark.parametrize("parts", [2, 5])
 def test_partitioned_paths_replay(parts):
     c = sr.TwoPhaseSys(5).checker().partitions(parts).spawn_bfs().join()
