@@ -308,7 +308,6 @@ class Engine final : public EngineBase {
         // the visited-set load factor the capacity hint is sized for.
         if (const char* e = std::getenv("SR_PROBE_BATCH")) probe_batch_ = std::atoi(e);
         if (const char* e = std::getenv("SR_TABLE_LOAD")) table_load_ = std::atof(e), load_env_ = true;
-        if (const char* e = std::getenv("SR_PROBE_LOAD")) probe_load_ = std::atoi(e);
         if (const char* e = std::getenv("SR_PPW_LOG2")) ppw_env_ = std::atoi(e);
         if (const char* e = std::getenv("SR_FILTER_LOG2")) filt_log2_ = (u32)std::atoi(e);
         // The LDS duplicate filter compares fingerprints: exact only in fingerprint mode (one-word
@@ -1133,7 +1132,8 @@ class Engine final : public EngineBase {
         if (grid_max_) return grid_max_;
         int per_cu = 0, cus = 0;
         const size_t dyn = filt_log2_ ? (8u << filt_log2_) : 0u;
-        const void* k = probe_batch_ == 2 ? (const void*)expand_fast<M, 2, 0> : (const void*)expand_fast<M, 1, 0>;
+        const void* k = probe_batch_ == 2 ? (const void*)expand_fast<M, 2, 0>
+                      : probe_batch_ == 3 ? (const void*)expand_fast<M, 3, 0> : (const void*)expand_fast<M, 1, 0>;
         SR_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 256, dyn));
         SR_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, o_.device));
         grid_max_ = per_cu > 0 && cus > 0 ? (u32)(2 * per_cu * cus) : ~0u;
@@ -1168,8 +1168,9 @@ class Engine final : public EngineBase {
                     undiscovered, nullptr, sq, 0u, ppw_log2, filt_log2_, sw);
             };
             if (o_.counters) launch(expand_fast<M, 1, 0, true>);
-            else switch (probe_batch_ * 10 + probe_load_) {
-                case 20: launch(expand_fast<M, 2, 0>); break;
+            else switch (probe_batch_) {
+                case 2: launch(expand_fast<M, 2, 0>); break;
+                case 3: launch(expand_fast<M, 3, 0>); break;
                 default: launch(expand_fast<M, 1, 0>); break;
             }
         }, n);
@@ -1249,12 +1250,9 @@ class Engine final : public EngineBase {
                                 last ? 1u : 0u, ppw_log2, filt_log2_, sw);
                         };
                         if (o_.counters) launch(expand_fast<M, 1, 0, true>);
-                        else switch (probe_batch_ * 10 + probe_load_) {
-                            case 11: launch(expand_fast<M, 1, 1>); break;
-                            case 12: launch(expand_fast<M, 1, 2>); break;
-                            case 13: launch(expand_fast<M, 1, 3>); break;
-                            case 20: launch(expand_fast<M, 2, 0>); break;
-                            case 21: launch(expand_fast<M, 2, 1>); break;
+                        else switch (probe_batch_) {
+                            case 2: launch(expand_fast<M, 2, 0>); break;
+                            case 3: launch(expand_fast<M, 3, 0>); break;
                             default: launch(expand_fast<M, 1, 0>); break;
                         }
                     });
@@ -1345,7 +1343,6 @@ class Engine final : public EngineBase {
     u32 emask_;  // the model's `eventually` properties
     bool fifo_ = false;
     int probe_batch_ = 1;
-    int probe_load_ = 0;
     int ppw_env_ = -1;
     bool table_recycle_ = true;  // the visited set is returned zeroed (~Engine)
     u32 grid_max_ = 0;      // cap on expand_fast's grid, 0 = two device residencies (SR_GRID_MAX)
