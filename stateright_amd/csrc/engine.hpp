@@ -1132,8 +1132,7 @@ class Engine final : public EngineBase {
         if (grid_max_) return grid_max_;
         int per_cu = 0, cus = 0;
         const size_t dyn = filt_log2_ ? (8u << filt_log2_) : 0u;
-        const void* k = probe_batch_ == 2 ? (const void*)expand_fast<M, 2, 0>
-                      : probe_batch_ == 3 ? (const void*)expand_fast<M, 3, 0> : (const void*)expand_fast<M, 1, 0>;
+        const void* k = probe_batch_ == 2 ? (const void*)expand_fast<M, 2, 0> : (const void*)expand_fast<M, 1, 0>;
         SR_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 256, dyn));
         SR_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, o_.device));
         grid_max_ = per_cu > 0 && cus > 0 ? (u32)(2 * per_cu * cus) : ~0u;
@@ -1170,7 +1169,6 @@ class Engine final : public EngineBase {
             if (o_.counters) launch(expand_fast<M, 1, 0, true>);
             else switch (probe_batch_) {
                 case 2: launch(expand_fast<M, 2, 0>); break;
-                case 3: launch(expand_fast<M, 3, 0>); break;
                 default: launch(expand_fast<M, 1, 0>); break;
             }
         }, n);
@@ -1252,7 +1250,6 @@ class Engine final : public EngineBase {
                         if (o_.counters) launch(expand_fast<M, 1, 0, true>);
                         else switch (probe_batch_) {
                             case 2: launch(expand_fast<M, 2, 0>); break;
-                            case 3: launch(expand_fast<M, 3, 0>); break;
                             default: launch(expand_fast<M, 1, 0>); break;
                         }
                     });

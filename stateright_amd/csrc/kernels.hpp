@@ -884,103 +884,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W >
         tl_first_chunk = false;
 #endif
 
-        if constexpr (PB == 3) {
-            // One successor per lane and round, software-pipelined one round ahead (SR_PROBE_BATCH=3):
-            // round r+1's successor is expanded, filtered and its home-slot load issued BEFORE round
-            // r's probe is resolved, so each wave keeps two probe loads in flight and its expansion
-            // work runs under the previous probe's latency instead of between rounds.
-            auto prep = [&](u32 i, u64 (&ns)[W], ProbeKey& pk, u32& par, bool& ok) {
-                ok = i < wend;
-                par = 0;
-                if (ok) {
-                    const u32 e = smap[wid][i - w0];
-                    const u32 p = e & 63, a = e >> 6;
-                    u64 ps[W];
-#pragma unroll
-                    for (int x = 0; x < W; ++x) ps[x] = pst[wid][p * W + x];
-                    ok = m.apply(ps, (int)a, ns);
-                    par = p;
-                    if (ok && same_state<W>(ns, ps)) {  // self-loop: counted, never probed
-                        ++succ;
-                        ok = false;
-                    }
-                }
-                pk = ok ? probe_key(m, t, ns) : ProbeKey{0, 0};
-                if (fmask && ok) {  // the block-local duplicate filter (see below)
-                    const u64 old = atomicExch(reinterpret_cast<unsigned long long*>(&filt[(u32)(pk.tag >> 40) & fmask]),
-                                               (unsigned long long)pk.tag);
-                    if (old == pk.tag) {
-                        ++succ;
-                        ok = false;
-                    }
-                }
-            };
-            u64 nsA[W], curA = 0;
-            ProbeKey pkA;
-            u32 parA;
-            bool okA;
-            prep(w0 + (u32)lane, nsA, pkA, parA, okA);
-            if (okA) curA = probe_load<POL>(&t.keys[pkA.home]);
-            if constexpr (STATS) probes += okA;
-            for (u32 it = w0; it < wend; it += 64) {
-                u64 nsB[W], curB = 0;
-                ProbeKey pkB{0, 0};
-                u32 parB = 0;
-                bool okB = false;
-#pragma unroll
-                for (int x = 0; x < W; ++x) nsB[x] = 0;
-                if (it + 64 < wend) {  // wave-uniform: the next round's successor and its probe load
-                    prep(it + 64 + (u32)lane, nsB, pkB, parB, okB);
-                    if (okB) curB = probe_load<POL>(&t.keys[pkB.home]);
-                    if constexpr (STATS) probes += okB;
-                }
-                bool nwA = false;
-                if (okA) {
-                    ++succ;
-                    if (curA != pkA.tag)
-                        find_or_claim_from<POL>(t, pkA, curA, &nwA, &lc->err, STATS ? &probes : nullptr, STATS ? &cas : nullptr);
-                }
-                // append round r's new state (as below: one LDS atomic per wave, overflow direct)
-                const u64 mask = __ballot(nwA);
-                if (mask) {
-                    const u32 cnt = __popcll(mask);
-                    const u32 below = __popcll(mask & ((1ull << lane) - 1));
-                    const int leader = __builtin_ctzll(mask);
-                    u32 sb = 0;
-                    if (lane == leader) sb = atomicAdd(&stage_n, cnt);
-                    sb = __shfl(sb, leader, 64);
-                    const u32 in_stage = sb >= (u32)STAGE ? 0u : min(cnt, (u32)STAGE - sb);
-                    u32 gb = 0;
-                    if (cnt > in_stage && lane == leader) gb = atomicAdd(&lc->claims, cnt - in_stage);
-                    gb = __shfl(gb, leader, 64);
-                    if (nwA) {
-                        const u32 pr = wave0 + parA;
-                        if (below < in_stage) {
-                            const u32 kk = sb + below;
-#pragma unroll
-                            for (int x = 0; x < W; ++x) stage[kk * W + x] = nsA[x];
-                            stage_par[kk] = pr;
-                        } else {
-                            const u32 pos = gb + (below - in_stage);
-                            if (pos < next_cap) {
-                                store_state<W>(next, pos, nsA);
-                                next_par[pos] = pr;
-                                if (sw.naeb) sw.naeb[pos] = sw.peb[pr];
-                            } else {
-                                atomicOr(&lc->err, (u32)ERR_FRONTIER_OVERFLOW);
-                            }
-                            eval_props(m, nsA, pos, undiscovered, lc);
-                        }
-                    }
-                }
-#pragma unroll
-                for (int x = 0; x < W; ++x) nsA[x] = nsB[x];
-                curA = curB;
-                pkA = pkB;
-                parA = parB;
-                okA = okB;
-            }
-        } else
         for (u32 it = w0; it < wend; it += 64 * PB) {
             u64 ns[PB][W], cur[PB];
             ProbeKey pk[PB];
