@@ -804,6 +804,35 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W >
         u64 mk[MW];
 #pragma unroll
         for (int i = 0; i < MW; ++i) mk[i] = 0;
+        if constexpr (has_enabled_slot<M>::value) {
+            // One lane per (parent, slot): PPP parents per pass, their masks assembled from the
+            // pass's ballot (has_enabled_slot). The parents are read from the wave's LDS copy.
+            static_assert(MW == 1 && M::ESLOTS <= 64 && 64 % M::ESLOTS == 0, "enabled_slot: ESLOTS must divide 64");
+            static_assert(!has_self_loops<M>::value, "enabled_slot: no self_loops hook");
+            constexpr u32 ES = M::ESLOTS, PPP = 64 / ES;
+            if (lane < (int)ppw && r < hi) {
+#pragma unroll
+                for (int i = 0; i < W; ++i) pst[wid][lane * W + i] = s[i];
+            }
+            wave_lds_sync();
+            const u32 np = hi > wave0 ? min(ppw, hi - wave0) : 0u;  // this wave's parents (uniform)
+            u64 mine = 0;
+            for (u32 p0 = 0; p0 < np; p0 += PPP) {
+                const u32 p = p0 + (u32)lane / ES, k = (u32)lane % ES;
+                const bool en = p < np && m.enabled_slot(&pst[wid][p * W], (int)k);
+                const u64 b = __ballot(en);
+                const u32 i = (u32)lane - p0;
+                if ((u32)lane >= p0 && i < PPP) mine = ES == 64 ? b : (b >> (i * ES)) & ((1ull << (ES % 64)) - 1);
+            }
+            if (lane < (int)ppw && r < hi) {
+                mk[0] = mine;
+                cnt = (u32)__popcll(mine);
+            }
+#if SR_TIMELINE
+            if (tl_first_chunk) SR_TL(2);
+            if (tl_first_chunk) SR_TL(10);
+#endif
+        } else
         if (lane < ppw && r < hi) {
             m.enabled(s, mk);
 #if SR_TIMELINE

@@ -73,6 +73,17 @@ template <class M>
 struct has_self_loops<M, std::void_t<decltype(std::declval<const M&>().self_loops((const u64*)nullptr, (const u64*)nullptr,
                                                                                   (u64*)nullptr))>> : std::true_type {};
 
+// Wide models whose enabled mask is a per-slot test (`enabled_slot(s, k)` = bit k of `enabled(s)`,
+// `ESLOTS` = max_actions, a power of two <= 64, MW = 1). Small levels of such a model are chains of
+// dependent instructions on a few lanes; the FAST expansion then evaluates the mask with one lane
+// per (parent, slot) instead of one lane per parent walking all the slots (paxos: 16 slots, each a
+// switch over the destination server's word), reading the parent from the wave's LDS copy.
+template <class M, class = void>
+struct has_enabled_slot : std::false_type {};
+template <class M>
+struct has_enabled_slot<M, std::void_t<decltype(std::declval<const M&>().enabled_slot((const u64*)nullptr, 0)),
+                                       decltype(M::ESLOTS)>> : std::true_type {};
+
 // Models with an OWNER KEY (`owner_key(s, &key)`: a projection of the state that most actions
 // leave unchanged; returns false when this instance has none). The partitioned search then owns a
 // state by its key instead of its fingerprint, so most successors stay in their parent's

@@ -606,6 +606,12 @@ struct PaxosT {
         }
         m[0] = mk;
     }
+    // Bit k of enabled(s) alone (has_enabled_slot: one lane per parent and slot on the device).
+    static constexpr int ESLOTS = px::SLOTS;
+    SR_HD bool enabled_slot(const u64* s, int k) const {
+        const u32 e = slot(s, k);
+        return e != px::EMPTY && delivers(s, e, (u32)(s[0] >> px::SBITS));
+    }
 
     // Deliver the a-th envelope (src/actor/model.rs:259-327); false = no-op (None).
     SR_HD bool apply(const u64* s, int a, u64* o) const {
