@@ -28,11 +28,6 @@
  *                                             (2pc reports all of them: 37% of successors)
  *             SR_HD canonical(s, out)         a canonical representative under the model's symmetry
  *                                             (the opt-in symmetry_canonical reduction)
- *             SR_HD enabled_slot(s, k) + static constexpr int ESLOTS
- *                                             bit k of enabled(s) alone (MW = 1, ESLOTS = max_actions
- *                                             dividing 64, no self_loops): FAST expansion evaluates
- *                                             the mask one lane per (parent, slot), with s in LDS
- *                                             (paxos: each slot's test is a switch; C = 3 -9.5%)
  *
  * Equal states must have equal words (the words ARE the state), and slots are enumerated in the
  * reference's `actions()` order, so FIFO runs reproduce the reference's visit order and paths.
