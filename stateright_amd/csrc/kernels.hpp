@@ -34,7 +34,7 @@ constexpr int MAX_PROPS = 32;
 constexpr int MAX_PARTS = 64;  // visited-set partitions (one per GPU, or virtual ones on one GPU)
 // expand_fast's largest parents per wave (log2) for wide states (W >= 4).
 #ifndef SR_WIDE_PPW_LOG2_MAX
-#define SR_WIDE_PPW_LOG2_MAX 5
+#define SR_WIDE_PPW_LOG2_MAX 4
 #endif
 // expand_fast's LDS stage of new states, in 64-bit words (its size sets the blocks per CU).
 #ifndef SR_STAGE_WORDS
