@@ -571,7 +571,8 @@ def main():
         } if prof else None,
         "engine": {k: st[k] for k in ("levels", "table_capacity", "rehashes", "level_loop_sec", "total_sec",
                                       "restarts", "pipelined", "records_routed", "head_levels")},
-        "runtime": {"hip": versions["hip"], "rccl": versions["rccl"], "libs": N.loaded_runtime_paths()},
+        "runtime": {"hip": versions["hip"], "rccl": versions["rccl"], "libs": N.loaded_runtime_paths(),
+                    "lib_digest": N.build_digest(), "source_digest": __import__("stateright_amd.build").build.source_digest()},
     }
     if no_hint is not None:
         no_hint["vs_value"] = no_hint["value"] / res["value"]

@@ -276,6 +276,10 @@ void sr_dist_free(sr_dist* comm);
 int32_t sr_rccl_version(int32_t* runtime, int32_t* compiled);
 int32_t sr_hip_runtime_version(int32_t* runtime, int32_t* compiled);
 int32_t sr_device_synchronize(int32_t device);
+/* The source digest this library was compiled from (16 hex digits: sha256 over the engine's sources
+ * and headers, stateright_amd/build.py `source_digest`). The Python loader refuses a library whose
+ * digest differs from the sources beside it, so a stale binary never tests or benches old code. */
+const char* sr_build_digest(void);
 /* Host-only self-test of the visited set's quotient encoding (kernels.hpp): the key permutation is
  * a bijection and slot values decode to their keys. SR_OK or SR_ERR_ARG (sr_last_error). */
 int32_t sr_selftest_tables(void);

@@ -8,6 +8,7 @@ K=""
 if [ "$1" = "--parity" ]; then K=$2; shift 2; fi
 [ "$1" = "--" ] && shift
 cd "$GRAFT_REPO_ROOT" || exit 1
+export SR_LIB_DIGEST_CHECK=0  # lib_base.so is a build of older sources (see _native.check_digest)
 O=gpurun_out/$TAG
 mkdir -p "$O"
 LIB=stateright_amd/libstateright_gpu.so

@@ -127,6 +127,7 @@ SIGNATURES = [
     ("sr_rccl_version", ctypes.c_int32, [ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32)]),
     ("sr_hip_runtime_version", ctypes.c_int32, [ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32)]),
     ("sr_device_synchronize", ctypes.c_int32, [ctypes.c_int32]),
+    ("sr_build_digest", ctypes.c_char_p, []),
     ("sr_selftest_tables", ctypes.c_int32, []),
     ("sr_selftest_models", ctypes.c_int32, []),
     ("sr_gpu_bfs_spawn_plugin", _P, [_P, _I64P, ctypes.c_int32, ctypes.POINTER(sr_opts)]),
@@ -156,8 +157,34 @@ def load():
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
+        check_digest(lib)
         _lib = lib
     return _lib
+
+
+class StaleLibraryError(ImportError):
+    pass
+
+
+def check_digest(lib, sources_root=None):
+    """Refuses a library compiled from other sources than the ones beside it: sr_build_digest()
+    must equal build.source_digest() (stateright_amd/build.py). SR_LIB_DIGEST_CHECK=0 turns the
+    check off; only scripts/gpu_lib_ab.sh does that, to time a saved build of older sources against
+    the current one (bench.py still records both digests in its line)."""
+    if os.environ.get("SR_LIB_DIGEST_CHECK", "1") == "0":
+        return
+    from . import build
+    want = build.source_digest() if sources_root is None else build.source_digest_at(sources_root)
+    got = lib.sr_build_digest().decode()
+    if got != want:
+        raise StaleLibraryError(
+            f"{LIB_PATH} was built from sources with digest {got}, but the sources here have digest {want}; "
+            "rebuild it (`python -c 'import __graft_entry__ as g; g.build()'`)")
+
+
+def build_digest():
+    """The source digest compiled into the loaded library."""
+    return load().sr_build_digest().decode()
 
 
 def last_error():

@@ -48,7 +48,7 @@
 namespace sr {
 
 // Element-wise reduction of `rows` vectors of n words (rows x n, row-major) into out.
-__global__ void reduce_rows(const u64* in, u32 rows, u64 n, u32 op, u64* out) {
+template <int = 0> __global__ void reduce_rows(const u64* in, u32 rows, u64 n, u32 op, u64* out) {
     const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     u64 v = in[i];
@@ -158,7 +158,7 @@ inline u64 peer_timeout_ticks() {
 
 // Flag words of the direct exchange cleared with system-scope stores and a system-scope release: no
 // dirty line of them stays in this device's L2 to be written back over a peer's later flag store.
-__global__ void flags_clear(u32* f, u32 n) {
+template <int = 0> __global__ void flags_clear(u32* f, u32 n) {
     for (u32 i = threadIdx.x; i < n; i += blockDim.x) __hip_atomic_store(&f[i], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
@@ -172,7 +172,7 @@ __device__ __host__ __forceinline__ u64 probe_word(u32 src, u32 dst, u64 i, u32 
 // those of a receive buffer it read two levels earlier); `sink` keeps the reads.
 // The stores are written back (system-scope release) before the reads: a dirty line of the owner
 // could otherwise be evicted over a peer's later store.
-__global__ void probe_warm(u64* buf, u64 n, u64 v, u64* sink) {
+template <int = 0> __global__ void probe_warm(u64* buf, u64 n, u64 v, u64* sink) {
     u64 acc = 0;
     for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) buf[i] = v;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -183,7 +183,7 @@ __global__ void probe_warm(u64* buf, u64 n, u64 v, u64* sink) {
 }
 // One workgroup of rank `me` stores its pattern into slot `me` of every rank's buffer (btab[q]),
 // then releases at system scope and raises its flag in every rank's flags (expand_route's order).
-__global__ void probe_store(u64* const* btab, u32* const* ftab, u32 world, u64 K, u32 me, u32 seq) {
+template <int = 0> __global__ void probe_store(u64* const* btab, u32* const* ftab, u32 world, u64 K, u32 me, u32 seq) {
     for (u32 q = 0; q < world; ++q)
         for (u64 i = threadIdx.x; i < K; i += blockDim.x) btab[q][i] = probe_word(me, q, i, seq);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -195,7 +195,7 @@ __global__ void probe_store(u64* const* btab, u32* const* ftab, u32 world, u64 K
 }
 // The owner waits for every flag inside the kernel that reads (insert_recv_lag's fused wait: poll,
 // system-scope acquire, then plain loads), bounded, and counts the words that differ.
-__global__ void probe_verify(const u64* buf, const u32* flags, u32 world, u64 K, u32 me, u32 seq, u64 timeout,
+template <int = 0> __global__ void probe_verify(const u64* buf, const u32* flags, u32 world, u64 K, u32 me, u32 seq, u64 timeout,
                              unsigned long long* bad, LevelCounters* lc) {
     __shared__ u32 ok;
     if (threadIdx.x == 0) {

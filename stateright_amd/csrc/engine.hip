@@ -1,7 +1,7 @@
 // MI355X breadth-first model-checking engine library: the compiled-in GpuModel registry and the
 // C ABI (include/stateright_gpu.h). The engine itself is engine.hpp.
 #include <unordered_set>
-#include "engine.hpp"
+#include "registry.hpp"
 #include "dgraph.hpp"
 #include "paxos.hpp"
 #include "actor.hpp"
@@ -15,96 +15,33 @@ static void set_error(const std::string& e) { g_last_error = e; }
 
 namespace sr {
 
-// 2pc's owner key for the partitioned search (TwoPhase::okey_rms): the tuples of this many RMs.
-// More RMs balance the partitions better, fewer keep more successors local (DESIGN.md §6 measures
-// the trade-off). SR_OWNER_RMS overrides it; 0 owns states by fingerprint.
-static int two_phase_owner_rms(int n) {
-    if (const char* e = std::getenv("SR_OWNER_RMS")) return std::max(0, std::min(n, std::atoi(e)));
-    return n <= 7 ? (n + 1) / 2 : 4;  // N=11 at T=8: 0.33 of successors cross, per-level balance 1.14
-}
-
-// The registry below instantiates `E<Model>` for every model; the single-GPU engine and the
-// partitioned engine share it.
-// A model with `eventually` properties runs partitioned as EvBits<Model> (models.hpp).
-template <template <class> class E, class M, class... Args>
-static std::unique_ptr<EngineBase> engine_for(const M& m, const sr_opts& o, Args... args) {
-    if constexpr (std::is_same<E<M>, DistEngine<M>>::value && has_emask<M>::value) {
-        if (model_emask(m)) return std::make_unique<DistEngine<EvBits<M>>>(EvBits<M>(m), o, args...);
-    }
-    return std::make_unique<E<M>>(m, o, args...);
-}
-
-template <template <class> class E, class... Args>
-static std::unique_ptr<EngineBase> make_model_engine(int model, const i64* p, int np, const sr_opts& o, Args... args) {
-    auto need = [&](int k) {
-        if (np < k) throw Error(SR_ERR_ARG, "model " + std::to_string(model) + " needs " + std::to_string(k) + " params");
-    };
-    if (o.symmetry && model != SR_MODEL_2PC)
-        throw Error(SR_ERR_UNSUPPORTED, "symmetry reduction: model " + std::to_string(model) + " has no canonical form");
-    switch (model) {
+// The registry (registry.hpp): each family of models compiles in its own translation unit.
+static std::unique_ptr<EngineBase> make_model_engine(const EngineArgs& a) {
+    if (a.o->symmetry && a.model != SR_MODEL_2PC)
+        throw Error(SR_ERR_UNSUPPORTED, "symmetry reduction: model " + std::to_string(a.model) + " has no canonical form");
+    switch (a.model) {
         case SR_MODEL_LINEAR_EQUATION:
-            need(3);
-            return std::make_unique<E<LinearEquation>>(LinearEquation{(u32)(p[0] & 0xff), (u32)(p[1] & 0xff), (u32)(p[2] & 0xff)}, o, args...);
         case SR_MODEL_BINARY_CLOCK:
-            return std::make_unique<E<BinaryClock>>(BinaryClock{}, o, args...);
-        case SR_MODEL_2PC:
-            need(1);
-            if (p[0] < 1 || p[0] > 14) throw Error(SR_ERR_UNSUPPORTED, "2pc: rm_count must be in 1..=14 (4n+4 <= 63 bits)");
-            if (o.symmetry)
-                return std::make_unique<E<Canon<TwoPhase>>>(Canon<TwoPhase>(TwoPhase{(int)p[0], two_phase_owner_rms((int)p[0])}), o, args...);
-            return std::make_unique<E<TwoPhase>>(TwoPhase{(int)p[0], two_phase_owner_rms((int)p[0])}, o, args...);
-        case SR_MODEL_INCREMENT:
-            need(1);
-            if (p[0] < 1 || p[0] > 15) throw Error(SR_ERR_UNSUPPORTED, "increment: threads must be in 1..=15");
-            if (p[0] <= 9) return std::make_unique<E<Increment<1>>>(Increment<1>{(int)p[0]}, o, args...);
-            return std::make_unique<E<Increment<2>>>(Increment<2>{(int)p[0]}, o, args...);
-        case SR_MODEL_INCREMENT_LOCK:
-            need(1);
-            if (p[0] < 1 || p[0] > 12) throw Error(SR_ERR_UNSUPPORTED, "increment_lock: threads must be in 1..=12");
-            if (p[0] <= 8) return std::make_unique<E<IncrementLock<1>>>(IncrementLock<1>{(int)p[0]}, o, args...);
-            return std::make_unique<E<IncrementLock<2>>>(IncrementLock<2>{(int)p[0]}, o, args...);
-        case SR_MODEL_PAXOS:
-            need(1);
-            if (p[0] < 1 || p[0] > px::MAX_CLIENTS) throw Error(SR_ERR_UNSUPPORTED, "paxos: client_count must be in 1..=6");
-            if (p[0] <= Paxos::max_clients()) return std::make_unique<E<Paxos>>(Paxos::make((int)p[0]), o, args...);
-            return std::make_unique<E<PaxosWide>>(PaxosWide::make((int)p[0]), o, args...);
         case SR_MODEL_DGRAPH:
-            return engine_for<E>(DGraph::make(p, np, o.device), o, args...);
-        case SR_MODEL_PINGPONG: {
-            need(1);
-            if (p[0] < 0 || p[0] > 7) throw Error(SR_ERR_UNSUPPORTED, "ping-pong: max_nat must be in 0..=7 (16 network slots)");
-            PingPong m;
-            m.max_nat = (u32)p[0];
-            m.lossy = np > 1 && p[1] != 0;
-            m.duplicating = np > 2 ? p[2] != 0 : true;
-            m.maintains_history = np > 3 && p[3] != 0;
-            return engine_for<E>(m, o, args...);
-        }
-        case SR_MODEL_ACTOR_FIXTURE: {
-            need(1);
-            if (p[0] < 0 || p[0] > 1) throw Error(SR_ERR_ARG, "actor fixture: kind 0 (undeliverable) or 1 (timer)");
-            ActorFixture m;
-            m.kind = (int)p[0];
-            return std::make_unique<E<ActorFixture>>(m, o, args...);
-        }
-        case SR_MODEL_ABD: {
-            need(1);
-            AbdRegister m;
-            static_cast<act::AbdSys&>(m) = act::AbdSys::make((int)p[0], np > 1 ? (int)p[1] : 2, o.device);
-            return std::make_unique<E<AbdRegister>>(m, o, args...);
-        }
-        case SR_MODEL_SINGLE_COPY: {
-            need(1);
-            SingleCopyRegister m;
-            static_cast<act::SingleCopySys&>(m) = act::SingleCopySys::make((int)p[0], np > 1 ? (int)p[1] : 1);
-            return std::make_unique<E<SingleCopyRegister>>(m, o, args...);
-        }
+        case SR_MODEL_ACTOR_FIXTURE:
+            return reg_basic(a);
+        case SR_MODEL_2PC: return reg_two_phase(a);
+        case SR_MODEL_INCREMENT: return reg_increment(a);
+        case SR_MODEL_INCREMENT_LOCK: return reg_increment_lock(a);
+        case SR_MODEL_PAXOS:
+            a.need(1);
+            if (a.p[0] < 1 || a.p[0] > px::MAX_CLIENTS) throw Error(SR_ERR_UNSUPPORTED, "paxos: client_count must be in 1..=6");
+            return a.p[0] <= Paxos::max_clients() ? reg_paxos(a) : reg_paxos_wide(a);
+        case SR_MODEL_PINGPONG: return reg_ping_pong(a);
+        case SR_MODEL_ABD:
+        case SR_MODEL_SINGLE_COPY:
+            return reg_registers(a);
     }
-    throw Error(SR_ERR_ARG, "unknown model id " + std::to_string(model));
+    throw Error(SR_ERR_ARG, "unknown model id " + std::to_string(a.model));
 }
 
 static std::unique_ptr<EngineBase> make_engine(int model, const i64* p, int np, const sr_opts& o) {
-    return make_model_engine<Engine>(model, p, np, o);
+    return make_model_engine(EngineArgs{model, p, np, &o, false, nullptr, 0});
 }
 
 }  // namespace sr
@@ -706,6 +643,11 @@ int32_t sr_rccl_version(int32_t* runtime, int32_t* compiled) {
     return SR_OK;
 }
 
+#ifndef SR_BUILD_DIGEST
+#define SR_BUILD_DIGEST "unstamped"
+#endif
+const char* sr_build_digest(void) { return SR_BUILD_DIGEST; }
+
 int32_t sr_hip_runtime_version(int32_t* runtime, int32_t* compiled) {
     int v = 0;
     if (hipRuntimeGetVersion(&v) != hipSuccess) return SR_ERR_HIP;
@@ -826,7 +768,7 @@ sr_bfs* sr_gpu_bfs_spawn_partitioned(sr_dist* comm, int32_t virtual_parts, int32
         sr_opts o = normalized_opts(opts);
         if (comm) o.device = comm->c->device;
         if (sr_device_count() <= 0) throw Error(SR_ERR_NO_DEVICE, "no HIP device visible");
-        return start(make_model_engine<DistEngine>(model_id, params, nparams, o, comm ? comm->c.get() : nullptr, (int)virtual_parts));
+        return start(make_model_engine(EngineArgs{model_id, params, nparams, &o, true, comm ? comm->c.get() : nullptr, (int)virtual_parts}));
     } catch (const std::exception& x) {
         set_error(x.what());
         return nullptr;
@@ -861,4 +803,16 @@ extern "C" int64_t sr_timeline_fetch(int32_t device, uint64_t* out, int64_t cap)
         return SR_ERR_HIP;
     return (int64_t)words;
 }
+#endif
+
+#ifdef SR_ONE_TU
+// One translation unit (diagnostic builds, scripts/build_timeline.sh): the registry families too.
+#include "reg_basic.hip"
+#include "reg_two_phase.hip"
+#include "reg_increment.hip"
+#include "reg_increment_lock.hip"
+#include "reg_paxos.hip"
+#include "reg_paxos_wide.hip"
+#include "reg_ping_pong.hip"
+#include "reg_registers.hip"
 #endif

@@ -358,7 +358,7 @@ __device__ __forceinline__ void publish(LevelCounters* lc, HostCounters* h, u32 
 }
 
 // Standalone publish (after kernels that do not publish themselves).
-__global__ void publish_kernel(LevelCounters* lc, HostCounters* h, u32 seq, u32 reset, const u32* aux) {
+template <int = 0> __global__ void publish_kernel(LevelCounters* lc, HostCounters* h, u32 seq, u32 reset, const u32* aux) {
     publish<MAX_PROPS>(lc, h, seq, reset != 0, aux);
 }
 
@@ -1206,7 +1206,7 @@ __global__ void __launch_bounds__(256) ev_scan(M m, const u64* __restrict__ fron
 
 // Pass 2 over the expanded ranks [0, limit): the bits each state passes to its children, and per
 // property the LAST terminal state (rank + 1) whose bits still hold it.
-__global__ void __launch_bounds__(256) ev_resolve(const u32* __restrict__ tsat, const u32* __restrict__ eb_in, u32 limit,
+template <int = 0> __global__ void __launch_bounds__(256) ev_resolve(const u32* __restrict__ tsat, const u32* __restrict__ eb_in, u32 limit,
                                                   u32 eund, const u32* __restrict__ evf, u32* __restrict__ peb,
                                                   u32* evl) {
     const u32 r = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1223,7 +1223,7 @@ __global__ void __launch_bounds__(256) ev_resolve(const u32* __restrict__ tsat, 
         for (u32 c = eff; c; c &= c - 1) atomicMax(&evl[__builtin_ctz(c)], r + 1);
 }
 
-__global__ void fill_u32(u32* p, u32 n, u32 v) {
+template <int = 0> __global__ void fill_u32(u32* p, u32 n, u32 v) {
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) p[i] = v;
 }
@@ -1291,7 +1291,7 @@ __device__ __forceinline__ void init_counter_words(LevelCounters* lc, LevelCount
         *w = o >= D0 && o < D0 + MAX_PROPS ? ~0u : 0u;
     }
 }
-__global__ void init_level_counters(LevelCounters* lc, LevelCounters* slots, u32 nslots) {
+template <int = 0> __global__ void init_level_counters(LevelCounters* lc, LevelCounters* slots, u32 nslots) {
     init_counter_words(lc, slots, nslots);
 }
 
@@ -1336,7 +1336,7 @@ __global__ void __launch_bounds__(256) roots_start(M m, TableView t, InlineState
 
 // Rehash into a larger table (keys and meta move together); an entry that does not fit the new
 // table's probe limit sets ERR_TABLE_FULL in *err (the host then rehashes into a larger one).
-__global__ void rehash(TableView from, u64 from_cap, TableView to, u32* err) {
+template <int = 0> __global__ void rehash(TableView from, u64 from_cap, TableView to, u32* err) {
     u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= from_cap) return;
     u64 k = from.keys[i];
@@ -1349,7 +1349,7 @@ __global__ void rehash(TableView from, u64 from_cap, TableView to, u32* err) {
 
 // Longest linear-probe displacement over the occupied slots (sr_stats.max_displacement): quotient
 // mode stores 1 + the displacement in the low dbits; a fingerprint's home is fp & mask.
-__global__ void __launch_bounds__(256) table_max_disp(TableView t, u64 cap, u32* out) {
+template <int = 0> __global__ void __launch_bounds__(256) table_max_disp(TableView t, u64 cap, u32* out) {
     u32 best = 0;
     const u64 dmask = t.qbits ? (1ull << t.dbits) - 1 : 0;
     for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < cap; i += (u64)gridDim.x * blockDim.x) {
@@ -1364,7 +1364,7 @@ __global__ void __launch_bounds__(256) table_max_disp(TableView t, u64 cap, u32*
 }
 
 // After a rehash: candidate slot indices of the old table -> slots of the new one.
-__global__ void remap_slots(u32* cand, u64 n, TableView from, TableView to) {
+template <int = 0> __global__ void remap_slots(u32* cand, u64 n, TableView from, TableView to) {
     u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     u32 s = cand[i];
@@ -1399,7 +1399,7 @@ __device__ __forceinline__ u32 block_exclusive_scan(u32 v, u32* total) {
     return base + x - v;
 }
 
-__global__ void __launch_bounds__(SCAN_BLOCK) scan_tile_sums(const u32* in, u32 n, u32* sums) {
+template <int = 0> __global__ void __launch_bounds__(SCAN_BLOCK) scan_tile_sums(const u32* in, u32 n, u32* sums) {
     u64 base = (u64)blockIdx.x * SCAN_TILE + threadIdx.x * SCAN_ITEMS;
     u32 acc = 0;
 #pragma unroll
@@ -1410,7 +1410,7 @@ __global__ void __launch_bounds__(SCAN_BLOCK) scan_tile_sums(const u32* in, u32 
     if (threadIdx.x == 0) sums[blockIdx.x] = tot;
 }
 
-__global__ void __launch_bounds__(SCAN_BLOCK) scan_sums(u32* sums, u32 nt, u32* grand_total) {
+template <int = 0> __global__ void __launch_bounds__(SCAN_BLOCK) scan_sums(u32* sums, u32 nt, u32* grand_total) {
     // one block; sequential over chunks of SCAN_BLOCK tiles
     u32 carry = 0;
     for (u32 base = 0; base < nt; base += SCAN_BLOCK) {
@@ -1425,7 +1425,7 @@ __global__ void __launch_bounds__(SCAN_BLOCK) scan_sums(u32* sums, u32 nt, u32* 
     if (threadIdx.x == 0) *grand_total = carry;
 }
 
-__global__ void __launch_bounds__(SCAN_BLOCK) scan_tiles(const u32* in, u32 n, const u32* sums, u32* out) {
+template <int = 0> __global__ void __launch_bounds__(SCAN_BLOCK) scan_tiles(const u32* in, u32 n, const u32* sums, u32* out) {
     u64 base = (u64)blockIdx.x * SCAN_TILE + threadIdx.x * SCAN_ITEMS;
     u32 v[SCAN_ITEMS];
     u32 acc = 0;

@@ -118,7 +118,7 @@ __device__ __forceinline__ bool last_block(LevelCounters* lc, bool sysrel = fals
 // satisfies the wait (its next level writes the other buffer parity). Bounded: after `timeout`
 // ticks of the 100 MHz real-time counter the wait gives up and sets ERR_PEER_TIMEOUT, which
 // reaches every rank through the next level's rows.
-__global__ void peer_wait(const u32* flags, u32 nparts, u32 seq, LevelCounters* lc, u64 timeout) {
+template <int = 0> __global__ void peer_wait(const u32* flags, u32 nparts, u32 seq, LevelCounters* lc, u64 timeout) {
     const u32 q = threadIdx.x;
     bool ok = q >= nparts;
     const u64 t0 = __builtin_amdgcn_s_memrealtime();
@@ -133,14 +133,6 @@ __global__ void peer_wait(const u32* flags, u32 nparts, u32 seq, LevelCounters* 
     }
     if (!ok) atomicOr(&lc->err, (u32)ERR_PEER_TIMEOUT);
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-}
-
-// Direct exchange, one-off check of a transport (sr_dist probe): rank `me` stores `seq` into flag
-// word `me` of every rank's flag array (ftab[q]) after a system-scope release.
-__global__ void peer_signal(u32* const* ftab, u32 nparts, u32 seq) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-    for (u32 q = threadIdx.x; q < nparts; q += blockDim.x)
-        __hip_atomic_store(ftab[q], seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Local new states expand_route stages per chunk (states of W words): a partition keeps ~1/T of its
@@ -864,7 +856,7 @@ __global__ void __launch_bounds__(256) insert_recv_lag(M m, const u64* __restric
 }
 
 // Copies the all-gathered rows to pinned host memory and then stores `seq` (the host spins on it).
-__global__ void rows_publish(const u64* rows, u64* host_rows, u32 words, u32* host_seq, u32 seq) {
+template <int = 0> __global__ void rows_publish(const u64* rows, u64* host_rows, u32 words, u32* host_seq, u32 seq) {
     for (u32 i = threadIdx.x; i < words; i += blockDim.x) host_rows[i] = rows[i];
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: host memory
     __syncthreads();
@@ -874,7 +866,7 @@ __global__ void rows_publish(const u64* rows, u64* host_rows, u32 words, u32* ho
 // Test hook of the exchange check (SR_DX_CORRUPT_LEVEL): flips one bit of the first record some
 // source stored into this owner's receive slots, or of a header row word when no source sent any,
 // AFTER the sources computed their checksums. The owner's insert must report ERR_EXCHANGE.
-__global__ void dx_corrupt(u64* recv, u64 S, u32 C, u32 me, u32 nparts) {
+template <int = 0> __global__ void dx_corrupt(u64* recv, u64 S, u32 C, u32 me, u32 nparts) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     for (u32 q = 0; q < nparts; ++q) {
         const u64 c = recv[(u64)q * S + me];

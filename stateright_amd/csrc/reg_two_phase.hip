@@ -1,0 +1,21 @@
+// Registry family: 2pc and its canonical (symmetry) reduction (registry.hpp).
+#include "registry.hpp"
+
+namespace sr {
+// 2pc's owner key for the partitioned search (TwoPhase::okey_rms): the tuples of this many RMs.
+// More RMs balance the partitions better, fewer keep more successors local (DESIGN.md §6 measures
+// the trade-off). SR_OWNER_RMS overrides it; 0 owns states by fingerprint.
+static int two_phase_owner_rms(int n) {
+    if (const char* e = std::getenv("SR_OWNER_RMS")) return std::max(0, std::min(n, std::atoi(e)));
+    return n <= 7 ? (n + 1) / 2 : 4;  // N=11 at T=8: 0.33 of successors cross, per-level balance 1.14
+}
+
+std::unique_ptr<EngineBase> reg_two_phase(const EngineArgs& a) {
+    a.need(1);
+    const i64 n = a.p[0];
+    if (n < 1 || n > 14) throw Error(SR_ERR_UNSUPPORTED, "2pc: rm_count must be in 1..=14 (4n+4 <= 63 bits)");
+    const TwoPhase m{(int)n, two_phase_owner_rms((int)n)};
+    if (a.o->symmetry) return make_for(Canon<TwoPhase>(m), a);
+    return make_for(m, a);
+}
+}  // namespace sr
