@@ -1687,7 +1687,7 @@ class DistEngine final : public EngineBase {
             const u32 ppw_log2 = std::max<u32>(2, std::min<u32>(6, ppw_for(n)));
             const u32 grid = std::max<u32>(1, blocks_for((n + (1u << ppw_log2) - 1) >> ppw_log2, 4));
             p0.seq++;
-            expand_fast<M, 1, 0><<<grid, 256, filt_log2_ ? (8u << filt_log2_) : 0u, stream_>>>(
+            expand_fast<M, 0, 0><<<grid, 256, filt_log2_ ? (8u << filt_log2_) : 0u, stream_>>>(
                 m_, harena_.p + fb * W, 0u, (u32)n, hv, harena_.p + nb * W, hpar_.p + nb, ncap, p0.lc, und, p0.hc_dev, p0.seq,
                 1u, ppw_log2, filt_log2_, SlotWork{});
             SR_HIP(hipGetLastError());
@@ -2053,15 +2053,28 @@ class DistEngine final : public EngineBase {
                     recs += row[d];
                 }
             }
-            // A bucket over its capacity, an arena or a visited set too small: the sender's (or,
-            // one level later, the receiver's) error bit is in these rows on every rank.
+            // A failed exchange check, a bucket over its capacity, an arena or a visited set too
+            // small: the sender's (or, one level later, the receiver's) error bit is in these rows on
+            // every rank, so every rank throws at the SAME level. The owner of a corrupt slot knows
+            // one level earlier (its insert's own err word) but does not act on it then: its peers
+            // have enqueued waits for its flags of the next level, and leaving them unanswered would
+            // stall the vote until SR_PEER_TIMEOUT_MS. An exchange error wins over a
+            // capacity error (a corrupt record can overflow a bucket; a capacity restart would keep
+            // the direct exchange).
+            auto exchange_error = [&](u32 lv) {
+                return Error(ERR_CODE_EXCHANGE, "direct exchange: a receive slot failed its sequence tag or checksum (level " +
+                                                    std::to_string(lv) + ")");
+            };
+            if (glob_err & ERR_EXCHANGE) throw exchange_error(level);
             if (glob_err & ERR_TABLE_FULL) throw Error(SR_ERR_CAPACITY, "visited set probe limit exceeded");
             if (glob_err & ERR_FRONTIER_OVERFLOW) throw Error(SR_ERR_CAPACITY, "frontier or send bucket overflow");
-            u32 own_err = 0;  // this rank's inserts of `level` (their exchange check)
-            for (size_t i = 0; i < parts_.size(); ++i) own_err |= ctx_->parts[parts_[i].res].pub[(seq0[i] + (level - lvl0_)) & 1]->err;
-            if ((glob_err | own_err) & ERR_EXCHANGE)
-                throw Error(ERR_CODE_EXCHANGE, "direct exchange: a receive slot failed its sequence tag or checksum (level " +
-                                                   std::to_string(level) + ")");
+            // The last level's insert has no later rows: its own check is read where the search
+            // ends (the vote then makes every rank redo the check).
+            auto own_exchange_check = [&] {
+                u32 own_err = 0;
+                for (size_t i = 0; i < parts_.size(); ++i) own_err |= ctx_->parts[parts_[i].res].pub[(seq0[i] + (level - lvl0_)) & 1]->err;
+                if (own_err & ERR_EXCHANGE) throw exchange_error(level);
+            };
             if (glob_err & ERR_PEER_TIMEOUT) {
                 auto& d = ctx_->dx;
                 d.valid = false;
@@ -2125,6 +2138,7 @@ class DistEngine final : public EngineBase {
             }
             glob_prev_ = glob_n;
             if (glob_n == 0) {  // frontier exhausted everywhere: `is_done` (bfs.rs:307-311)
+                own_exchange_check();
                 reference_done = true;
                 break;
             }
@@ -2132,6 +2146,7 @@ class DistEngine final : public EngineBase {
             max_depth = level;
             unique = unique_total;
             if (M::NPROPS == 0 || (newly && undiscovered == 0)) {
+                own_exchange_check();
                 reference_done = true;
                 early_exit_ = true;
                 break;

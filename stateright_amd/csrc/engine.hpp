@@ -1132,7 +1132,7 @@ class Engine final : public EngineBase {
         if (grid_max_) return grid_max_;
         int per_cu = 0, cus = 0;
         const size_t dyn = filt_log2_ ? (8u << filt_log2_) : 0u;
-        const void* k = probe_batch_ == 2 ? (const void*)expand_fast<M, 2, 0> : (const void*)expand_fast<M, 1, 0>;
+        const void* k = probe_batch_ == 1 ? (const void*)expand_fast<M, 1, 0> : (const void*)expand_fast<M, 0, 0>;
         SR_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 256, dyn));
         SR_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, o_.device));
         grid_max_ = per_cu > 0 && cus > 0 ? (u32)(2 * per_cu * cus) : ~0u;
@@ -1166,11 +1166,9 @@ class Engine final : public EngineBase {
                     m_, arena_.p + fbase * W, 0u, n, view(), arena_.p + nbase * W, apar_.p + nbase, ncap, lc,
                     undiscovered, nullptr, sq, 0u, ppw_log2, filt_log2_, sw);
             };
-            if (o_.counters) launch(expand_fast<M, 1, 0, true>);
-            else switch (probe_batch_) {
-                case 2: launch(expand_fast<M, 2, 0>); break;
-                default: launch(expand_fast<M, 1, 0>); break;
-            }
+            if (o_.counters) launch(expand_fast<M, 0, 0, true>);
+            else if (probe_batch_ == 1) launch(expand_fast<M, 1, 0>);
+            else launch(expand_fast<M, 0, 0>);
         }, n);
         slot_seq_ = sq;
         slot_published_ = false;
@@ -1247,11 +1245,9 @@ class Engine final : public EngineBase {
                                 m_, cur(), ulo, uhi, view(), next, npar, ncap, lc_d_, undiscovered, hcd(sq), sq,
                                 last ? 1u : 0u, ppw_log2, filt_log2_, sw);
                         };
-                        if (o_.counters) launch(expand_fast<M, 1, 0, true>);
-                        else switch (probe_batch_) {
-                            case 2: launch(expand_fast<M, 2, 0>); break;
-                            default: launch(expand_fast<M, 1, 0>); break;
-                        }
+                        if (o_.counters) launch(expand_fast<M, 0, 0, true>);
+                        else if (probe_batch_ == 1) launch(expand_fast<M, 1, 0>);
+                        else launch(expand_fast<M, 0, 0>);
                     });
                 }
                 return sq;
@@ -1339,7 +1335,7 @@ class Engine final : public EngineBase {
     u32 D_;  // max successors of one state (bounds the new states a chunk can create)
     u32 emask_;  // the model's `eventually` properties
     bool fifo_ = false;
-    int probe_batch_ = 1;
+    int probe_batch_ = 0;  // expand_fast's probe loop: 0 the lane queue, 1 rounds of one successor per lane (SR_PROBE_BATCH)
     int ppw_env_ = -1;
     bool table_recycle_ = true;  // the visited set is returned zeroed (~Engine)
     u32 grid_max_ = 0;      // cap on expand_fast's grid, 0 = two device residencies (SR_GRID_MAX)

@@ -870,6 +870,41 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W >
         if (tl_first_chunk) SR_TL(11);
 #endif
 
+        // Appends the wave's new states of one round: one LDS atomic reserves the wave's span of the
+        // stage; what does not fit goes straight to the next frontier with ONE global atomic for the
+        // wave (never one per state).
+        auto append_new = [&](bool nw, const u64* ns, u32 par) {
+            const u64 mask = __ballot(nw);
+            if (!mask) return;
+            const u32 cnt = __popcll(mask);
+            const u32 below = __popcll(mask & ((1ull << lane) - 1));
+            const int leader = __builtin_ctzll(mask);
+            u32 sb = 0;
+            if (lane == leader) sb = atomicAdd(&stage_n, cnt);
+            sb = __shfl(sb, leader, 64);
+            const u32 in_stage = sb >= (u32)STAGE ? 0u : min(cnt, (u32)STAGE - sb);
+            u32 gb = 0;
+            if (cnt > in_stage && lane == leader) gb = atomicAdd(&lc->claims, cnt - in_stage);
+            gb = __shfl(gb, leader, 64);
+            if (!nw) return;
+            const u32 pr = wave0 + par;  // parent rank
+            if (below < in_stage) {
+                const u32 kk = sb + below;
+#pragma unroll
+                for (int x = 0; x < W; ++x) stage[kk * W + x] = ns[x];
+                stage_par[kk] = pr;
+            } else {
+                const u32 pos = gb + (below - in_stage);
+                if (pos < next_cap) {
+                    store_state<W>(next, pos, ns);
+                    next_par[pos] = pr;
+                    if (sw.naeb) sw.naeb[pos] = sw.peb[pr];
+                } else {
+                    atomicOr(&lc->err, (u32)ERR_FRONTIER_OVERFLOW);
+                }
+                eval_props(m, ns, pos, undiscovered, lc);
+            }
+        };
         for (u32 w0 = 0; w0 < total; w0 += MAPCAP) {
         const u32 wend = min(total, w0 + MAPCAP);
         if (MW <= 2 && ppw <= 8) {
@@ -913,6 +948,92 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W >
         tl_first_chunk = false;
 #endif
 
+        if constexpr (PB == 0) {
+            // Lane work queue (the default, DESIGN.md §3 "Probe rounds as a lane queue"). A lane owns
+            // one successor at a time and issues exactly one visited-set access per iteration for it:
+            // the home-slot load, a linear-probe step's load, or the claim CAS. A lane whose successor
+            // is resolved takes the window's next entry at once (a wave-uniform cursor, ranked by
+            // ballot), so the wave's memory round trips stay full: in the round-based loop below, a
+            // round lasted as long as its slowest lane's dependent chain (load, step, CAS) while the
+            // other lanes idled, and lanes whose successor the LDS filter had removed idled a whole
+            // round.
+            u32 cursor = w0;                   // next window entry to hand out (wave-uniform)
+            u32 st = 0;                        // 0: needs an entry, 1: load pending, 2: claim pending
+            u64 q[W];                          // the lane's successor
+            u64 si = 0, tag = 0;               // its current slot and the value that slot would hold
+            u32 qpar = 0, disp = 0;            // parent (in the wave) and linear-probe displacement
+            const u64 step = probe_step(t);
+            const u64 lanes_below = (1ull << lane) - 1;
+            for (;;) {
+                // idle lanes take entries until each holds a successor to probe or the window is spent
+                for (;;) {
+                    const u64 need = __ballot(st == 0);
+                    if (!need || cursor >= wend) break;
+                    const u32 i = cursor + (u32)__popcll(need & lanes_below);
+                    cursor += (u32)__popcll(need);
+                    if (st == 0 && i < wend) {
+                        const u32 e = smap[wid][i - w0];
+                        const u32 p = e & 63, a = e >> 6;
+                        u64 ps[W];
+#pragma unroll
+                        for (int x = 0; x < W; ++x) ps[x] = pst[wid][p * W + x];
+                        bool ok = m.apply(ps, (int)a, q);
+                        if (ok) {
+                            ++succ;  // within boundary: counted once, whatever follows
+                            ok = !same_state<W>(q, ps);  // self-loop: never probed
+                        }
+                        if (ok) {
+                            const ProbeKey k = probe_key(m, t, q);
+                            // block-local duplicate filter (see the round loop below)
+                            if (fmask) {
+                                const u64 old = atomicExch(reinterpret_cast<unsigned long long*>(&filt[(u32)(k.tag >> 40) & fmask]),
+                                                           (unsigned long long)k.tag);
+                                ok = old != k.tag;
+                            }
+                            si = k.home;
+                            tag = k.tag;
+                        }
+                        if (ok) {
+                            st = 1;
+                            qpar = p;
+                            disp = 0;
+                        }
+                    }
+                }
+                if (!__ballot(st != 0)) break;
+#if SR_TIMELINE
+                if (tl_first_round) SR_TL(4);
+#endif
+                u64 v = 0;
+                if (st == 1) v = probe_load<POL>(&t.keys[si]);
+                if (st == 2) v = atomicCAS(reinterpret_cast<unsigned long long*>(&t.keys[si]), 0ull, (unsigned long long)tag);
+                if constexpr (STATS) {
+                    probes += st == 1;
+                    cas += st == 2;
+                }
+                bool nw = false;
+                if (st != 0) {
+                    if (v == tag) {
+                        st = 0;  // visited already (or claimed by a concurrent duplicate)
+                    } else if (v == 0) {
+                        nw = st == 2;  // our claim won
+                        st = st == 1 ? 2u : 0u;
+                    } else if (++disp >= t.plimit) {
+                        atomicOr(&lc->err, (u32)ERR_TABLE_FULL);
+                        st = 0;
+                    } else {  // another key: the next slot
+                        si = (si + 1) & t.mask;
+                        tag += step;
+                        st = 1;
+                    }
+                }
+#if SR_TIMELINE
+                if (tl_first_round) SR_TL(5);
+                tl_first_round = false;
+#endif
+                append_new(nw, q, qpar);
+            }
+        } else
         for (u32 it = w0; it < wend; it += 64 * PB) {
             u64 ns[PB][W], cur[PB];
             ProbeKey pk[PB];
@@ -974,42 +1095,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W >
             if (tl_first_round) SR_TL(5);
             tl_first_round = false;
 #endif
-            // Append the new states of this round, aggregated per wave: one LDS atomic reserves the
-            // wave's span of the stage; what does not fit goes straight to the next frontier with
-            // ONE global atomic for the wave (never one per state).
+            // Append the new states of this round, aggregated per wave (append_new).
 #pragma unroll
-            for (int j = 0; j < PB; ++j) {
-                const u64 mask = __ballot(nw[j]);
-                if (!mask) continue;
-                const u32 cnt = __popcll(mask);
-                const u32 below = __popcll(mask & ((1ull << lane) - 1));
-                const int leader = __builtin_ctzll(mask);
-                u32 sb = 0;
-                if (lane == leader) sb = atomicAdd(&stage_n, cnt);
-                sb = __shfl(sb, leader, 64);
-                const u32 in_stage = sb >= (u32)STAGE ? 0u : min(cnt, (u32)STAGE - sb);
-                u32 gb = 0;
-                if (cnt > in_stage && lane == leader) gb = atomicAdd(&lc->claims, cnt - in_stage);
-                gb = __shfl(gb, leader, 64);
-                if (!nw[j]) continue;
-                const u32 pr = wave0 + par[j];  // parent rank
-                if (below < in_stage) {
-                    const u32 kk = sb + below;
-#pragma unroll
-                    for (int x = 0; x < W; ++x) stage[kk * W + x] = ns[j][x];
-                    stage_par[kk] = pr;
-                } else {
-                    const u32 pos = gb + (below - in_stage);
-                    if (pos < next_cap) {
-                        store_state<W>(next, pos, ns[j]);
-                        next_par[pos] = pr;
-                        if (sw.naeb) sw.naeb[pos] = sw.peb[pr];
-                    } else {
-                        atomicOr(&lc->err, (u32)ERR_FRONTIER_OVERFLOW);
-                    }
-                    eval_props(m, ns[j], pos, undiscovered, lc);
-                }
-            }
+            for (int j = 0; j < PB; ++j) append_new(nw[j], ns[j], par[j]);
         }
         wave_lds_sync();  // the window's map is read before the next window overwrites it
         }

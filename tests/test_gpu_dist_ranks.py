@@ -9,6 +9,7 @@ the CPU oracle model. Plus the BASELINE configuration 4 at its full size: 2pc N=
 ways (virtual partitions) against the closed forms of BASELINE.md §3."""
 import json
 import os
+import time
 import subprocess
 import sys
 
@@ -241,15 +242,20 @@ def test_corrupt_slot_falls_back_to_collective(level, monkeypatch):
     # sent records to rank 0) flipped after its source checksummed the slot makes the owner's insert
     # report ERR_EXCHANGE; the ranks vote, and the check is redone on the collective exchange with
     # exact counts. The communicator then keeps the collective exchange.
+    # Every rank throws at the same level: with SR_PEER_TIMEOUT_MS at its default (20 s)
+    # the fallback must not wait for an unanswered peer flag.
     monkeypatch.setenv("SR_HEAD_MAX", "0")
     monkeypatch.setenv("SR_DX_CORRUPT_LEVEL", str(level))
+    monkeypatch.delenv("SR_PEER_TIMEOUT_MS", raising=False)
     o = oracle(TWO_PHASE, [6])
     comms = Communicator.local_group(2)
     try:
         for k in range(2):
+            t0 = time.monotonic()
             cs = [sr.TwoPhaseSys(6).checker().comm(c).spawn_bfs() for c in comms]
             for ch in cs:
                 ch.join()
+            assert time.monotonic() - t0 < 5.0, "the fallback stalled (a peer waited for its timeout)"
             for ch in cs:
                 assert (ch.unique_state_count(), ch.state_count(), ch.max_depth()) == \
                     (o.unique_state_count, o.state_count, o.max_depth)
