@@ -321,10 +321,16 @@ sr_bfs* sr_gpu_bfs_spawn_plugin_partitioned(const sr_plugin* plugin, sr_dist* co
 /* The engine's fingerprint of a state of a registered model, given by its canonical description
  * (the integers sr_gpu_bfs_discovery_path / sr_gpu_bfs_visits return, describe_width of them):
  * what a host-side `Path::from_fingerprints` (src/checker/path.rs:20-86) compares with the chain of
- * sr_gpu_bfs_discovery. Host-only (no device needed). SR_ERR_UNSUPPORTED for models whose
- * description does not determine the state (paxos: its history index is not described). */
+ * sr_gpu_bfs_discovery. Host-only (no device needed). Every registered model but DGraph: the
+ * register models (paxos, ABD, single-copy) describe their LinearizabilityTester history
+ * canonically (per client the Get's returned value and its real-time predecessors), so their
+ * description determines the state. SR_ERR_UNSUPPORTED for DGraph. */
 int32_t sr_model_fingerprint(int32_t model_id, const int64_t* params, int32_t nparams, const int64_t* described,
                              int32_t width, uint64_t* fp_out);
+/* Host-only self-test of sr_model_fingerprint: a host BFS over up to max_states reachable states of
+ * the model; every state's description must give the state back and the engine's fingerprint of
+ * it. Returns the states checked, or SR_ERR_* (sr_last_error says which state failed). */
+int64_t sr_selftest_describe(int32_t model_id, const int64_t* params, int32_t nparams, int64_t max_states);
 
 #ifdef __cplusplus
 }

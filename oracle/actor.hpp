@@ -677,7 +677,9 @@ struct AbdSys {
         }
         d.resize(o + (size_t)actor_width(), 0);
     }
-    void describe_history(const Hist&, std::vector<i64>&) const {}  // summarised by `linearizable`
+    void describe_history(const Hist& h, std::vector<i64>& d) const {
+        paxos::describe_register_history(h, server_count, client_count, d);
+    }
     std::string format_msg(const Msg& m) const {
         auto ch = [](char c) {
             if (!c) return std::string("'\\u{0}'");
@@ -788,7 +790,9 @@ struct SingleCopySys {
             d.push_back((i64)a.op_count);
         }
     }
-    void describe_history(const Hist&, std::vector<i64>&) const {}  // summarised by `linearizable`
+    void describe_history(const Hist& h, std::vector<i64>& d) const {
+        paxos::describe_register_history(h, server_count, client_count, d);
+    }
     std::string format_msg(const Msg& m) const { return AbdSys{}.format_msg(m); }
 };
 

@@ -197,6 +197,35 @@ struct History {
     }
 };
 
+// The register history in canonical form (shared with the GPU encodings' `describe`, so that a
+// description determines the state and the engine can fingerprint it: sr_model_fingerprint). Per
+// client c (actor id first_id + c), c = 0..C-1: its Get's returned value (value code: '\0' 0,
+// the k-th client's letter k + 1; -1 while the Get has not returned), then for every other client
+// u in ascending order how many of u's ops had completed when c invoked its Get (-1 before it).
+// Every client runs put_count 1 (a Put invoked at init, then one Get).
+inline void describe_register_history(const History& H, size_t first_id, size_t C, std::vector<i64>& d) {
+    for (size_t c = 0; c < C; ++c) {
+        const Id id = first_id + c;
+        auto bt = H.by_thread.find(id);
+        const size_t ndone = bt == H.by_thread.end() ? 0 : bt->second.size();
+        const LastCompleted* last = nullptr;  // the Get's real-time predecessors
+        if (ndone >= 2) last = &bt->second[1].last;
+        else if (ndone == 1 && H.in_flight.count(id)) last = &H.in_flight.at(id).last;
+        const char v = ndone >= 2 ? bt->second[1].ret.value : 0;
+        d.push_back(ndone >= 2 ? (v ? (i64)(v - 'A' + 1) : 0) : -1);
+        for (size_t u = 0; u < C; ++u) {
+            if (u == c) continue;
+            if (!last) {
+                d.push_back(-1);
+                continue;
+            }
+            auto it = last->find(first_id + u);
+            d.push_back(it == last->end() ? 0 : (i64)it->second + 1);
+        }
+    }
+}
+inline int register_history_width(size_t C) { return (int)(C * C); }
+
 struct State {
     std::vector<ActorState> actors;
     History history;
@@ -499,7 +528,7 @@ struct PaxosModel {
     // Canonical description (shared with the GPU encoding): per server [round, ballot id,
     // proposal client (-1 none), prepares per server (-1 absent, else acc code), accepts mask,
     // accepted acc code, decided], per client [op_count], then the network as 16 sorted
-    // envelope codes padded with -1. (The history is summarised by linearizability only.)
+    // envelope codes padded with -1, then the register history (describe_register_history).
     std::vector<i64> describe(const State& s) const {
         std::vector<i64> d;
         for (Id i = 0; i < server_count; ++i) {
@@ -523,6 +552,7 @@ struct PaxosModel {
         std::sort(net.begin(), net.end());
         net.resize(16, -1);
         d.insert(d.end(), net.begin(), net.end());
+        describe_register_history(s.history, server_count, client_count, d);
         return d;
     }
 };

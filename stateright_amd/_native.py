@@ -135,6 +135,7 @@ SIGNATURES = [
                                                  ctypes.POINTER(sr_opts)]),
     ("sr_model_fingerprint", ctypes.c_int32, [ctypes.c_int32, _I64P, ctypes.c_int32, _I64P, ctypes.c_int32,
                                               ctypes.POINTER(ctypes.c_uint64)]),
+    ("sr_selftest_describe", ctypes.c_int64, [ctypes.c_int32, _I64P, ctypes.c_int32, ctypes.c_int64]),
     ("sr_gpu_bfs_spawn_partitioned", _P, [_P, ctypes.c_int32, ctypes.c_int32, _I64P, ctypes.c_int32,
                                           ctypes.POINTER(sr_opts)]),
 ]

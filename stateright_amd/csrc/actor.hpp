@@ -194,7 +194,7 @@ struct ActorGpu : Sys {
     // Canonical description (oracle/actor.hpp describe): the actors' and the history's fields, the
     // timer vector (length, bits), then the network as NET descriptive envelope codes (msg code *
     // 128 + dst) * 16 + src, ascending, padded with -1.
-    int describe_width() const { return Sys::actors_width() + Sys::history_width() + 2 + Sys::NET; }
+    int describe_width() const { return this->actors_width() + this->history_width() + 2 + Sys::NET; }
     static i64 desc_env(const Sys& sy, u32 e) { return (sy.msg_code(e_msg(e)) * 128 + (i64)e_dst(e)) * 16 + (i64)e_src(e); }
     static_assert(Sys::NET >= K, "the description holds every envelope");
     void describe(const u64* s, i64* d) const {
@@ -208,6 +208,24 @@ struct ActorGpu : Sys {
         std::sort(net.begin(), net.end());
         net.resize(Sys::NET, -1);
         for (i64 v : net) d[k++] = v;
+    }
+    // The state of a description (sr_model_fingerprint): the inverse of describe.
+    void undescribe(const i64* d, u64* s) const {
+        for (int w = 0; w < W; ++w) s[w] = 0;
+        int k = this->undescribe_fields(d, s);
+        s[0] |= (u64)(d[k] & 15) << 52 | (u64)(d[k + 1] & 255) << 56;
+        k += 2;
+        u32 net[K];
+        int n = 0;
+        for (int j = 0; j < Sys::NET; ++j, ++k) {
+            if (d[k] < 0) continue;
+            if (n >= K) throw Error(SR_ERR_ARG, "actor model: the described network exceeds the encoding's capacity");
+            const i64 c = d[k];
+            net[n++] = env((u32)(c % 16), (u32)(c / 16 % 128), this->msg_decode(c / 2048));
+        }
+        std::sort(net, net + n);
+        for (int j = n; j < K; ++j) net[j] = EMPTY;
+        pack(s, net);
     }
     // Action ids (oracle/actor.hpp action_id): Deliver = code * 4 + 1, Drop = code * 4 + 2,
     // Timeout(i) = i * 4 + 3.
@@ -276,6 +294,7 @@ struct PingPongSys {
         return n[p];
     }
     i64 msg_code(u32 msg) const { return (i64)(msg & 255) * 2 + (msg >> 8); }
+    u32 msg_decode(i64 code) const { return (u32)(code & 1) << 8 | (u32)(code / 2); }
     std::string format_msg(i64 code) const { return std::string(code & 1 ? "Pong(" : "Ping(") + std::to_string(code / 2) + ")"; }
     static int actors_width() { return 2; }
     static int history_width() { return 2; }
@@ -284,6 +303,10 @@ struct PingPongSys {
         d[1] = count(s, 1);
         d[2] = (i64)(s[0] >> 8 & 255);
         d[3] = (i64)(s[0] >> 16 & 255);
+        return 4;
+    }
+    int undescribe_fields(const i64* d, u64* s) const {
+        s[0] = (u64)(d[0] & 15) | (u64)(d[1] & 15) << 4 | (u64)(d[2] & 255) << 8 | (u64)(d[3] & 255) << 16;
         return 4;
     }
 };
@@ -313,6 +336,7 @@ struct FixtureSys {
     int expectation(int) const { return ALWAYS; }
     const char* prop_name(int) const { return "unused"; }
     i64 msg_code(u32) const { return 0; }
+    u32 msg_decode(i64) const { return 0; }
     std::string format_msg(i64) const { return "()"; }
     static int actors_width() { return 1; }
     static int history_width() { return 0; }
@@ -320,6 +344,7 @@ struct FixtureSys {
         d[0] = 0;
         return 1;
     }
+    int undescribe_fields(const i64*, u64*) const { return 1; }
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -537,6 +562,9 @@ struct AbdSys {
         const i64 kind = m >> 12, req = m >> 8 & 15, clock = m >> 5 & 7, id = m >> 2 & 7, val = m & 3;
         return (((req * 8 + clock) * 8 + id) * 8 + val) * 8 + kind;
     }
+    u32 msg_decode(i64 code) const {
+        return msg((u32)(code % 8), (u32)(code / 4096), (u32)(code / 512 % 8), (u32)(code / 64 % 8), (u32)(code / 8 % 8));
+    }
     std::string format_msg(i64 code) const {
         const i64 kind = code % 8, val = code / 8 % 8, id = code / 64 % 8, clock = code / 512 % 8, req = code / 4096;
         auto ch = [](i64 v) { return v ? std::string("'") + (char)('A' + v - 1) + "'" : std::string("'\\u{0}'"); };
@@ -553,8 +581,9 @@ struct AbdSys {
         }
     }
     int actors_width() const { return (int)((S + C) * (8 + S)); }
-    static int history_width() { return 0; }
-    // oracle/actor.hpp AbdSys::describe_actor, per actor (8 + S values)
+    int history_width() const { return (int)(C * C); }
+    // oracle/actor.hpp AbdSys::describe_actor, per actor (8 + S values), then the history
+    // (oracle/paxos.hpp describe_register_history) of the interned index's history
     int describe_fields(const u64* s, i64* d) const {
         int k = 0;
         const int width = 8 + (int)S;
@@ -582,7 +611,44 @@ struct AbdSys {
             }
             while (k < base + width) d[k++] = 0;
         }
-        return k;
+        px::Tables& t = px::tables((int)C, -1);
+        const u32 h = (u32)(s[0] & 0xffff);
+        if (h >= t.hists.size()) throw Error(SR_ERR_ARG, "abd: history index out of range");
+        px::describe_hist(t.hists[h], (int)C, d + k);
+        return k + history_width();
+    }
+    int undescribe_fields(const i64* d, u64* s) const {
+        int k = 0;
+        const int width = 8 + (int)S;
+        for (u32 id = 0; id < S + C; ++id) {
+            const int base = k;
+            if (id < S) {
+                u64 w = 0;
+                const u32 phase = (u32)d[k + 3];
+                w = setf(w, 0, 3, (u32)d[k]);
+                w = setf(w, 3, 2, (u32)d[k + 1]);
+                w = setf(w, 5, 2, (u32)d[k + 2]);
+                w = setf(w, 7, 2, phase);
+                if (phase) {
+                    w = setf(w, 9, 4, (u32)d[k + 4]);
+                    w = setf(w, 13, 3, (u32)d[k + 5]);
+                    if (d[k + 6] >= 0) w = setf(w, 16, 3, (u32)d[k + 6] + 1);
+                }
+                for (u32 j = 0; j < S; ++j) {
+                    const i64 r = d[k + 7 + (int)j];
+                    if (r >= 0) w = setf(w, 19 + 8 * (int)j, 8, 1u | (u32)(r / 64) << 1 | (u32)(r / 8 % 8) << 4 | (u32)(r % 8) << 6);
+                }
+                if (phase == 2) w = setf(w, 19 + 8 * (int)S, (int)S, (u32)d[k + 7 + (int)S]);
+                s[1 + id] = w;
+            } else {
+                const i64 aw = d[k], ops = d[k + 1];
+                s[0] = setf(s[0], 16 + 7 * (int)(id - S), 7, (aw >= 0 ? 1u | (u32)aw << 1 : 0u) | (u32)ops << 5);
+            }
+            k = base + width;
+        }
+        px::Tables& t = px::tables((int)C, -1);
+        s[0] |= t.hist_index(d + k);
+        return k + history_width();
     }
 };
 
@@ -685,9 +751,10 @@ struct SingleCopySys {
     const char* prop_name(int p) const { return p == 0 ? "linearizable" : "value chosen"; }
     // the oracle's msg code (AbdSys::msg_code with seq (0, Id(0))): ((req * 512 + val) * 8 + kind)
     i64 msg_code(u32 m) const { return ((i64)(m >> 4 & 255) * 512 + (i64)(m & 7)) * 8 + (i64)(m >> 12); }
+    u32 msg_decode(i64 code) const { return msg((u32)(code % 8), (u32)(code / 4096), (u32)(code / 8 % 512)); }
     std::string format_msg(i64 code) const { return AbdSys{}.format_msg(code); }
     int actors_width() const { return (int)(2 * (S + C)); }
-    static int history_width() { return 0; }
+    int history_width() const { return hs().width(); }
     // oracle/actor.hpp SingleCopySys::describe_actor: server [value, 0]; client [awaiting, op_count]
     int describe_fields(const u64* s, i64* d) const {
         int k = 0;
@@ -701,7 +768,18 @@ struct SingleCopySys {
                 d[k++] = (i64)ph + 1;
             }
         }
-        return k;
+        hs().describe(s[1], s[2], d + k);
+        return k + history_width();
+    }
+    int undescribe_fields(const i64* d, u64* s) const {
+        int k = 0;
+        u32 phases[px::MAX_CLIENTS];
+        for (u32 id = 0; id < S + C; ++id, k += 2) {
+            if (id < S) s[0] |= (u64)(d[k] & 7) << (3 * id);
+            else phases[id - S] = (u32)(d[k + 1] - 1);
+        }
+        hs().undescribe(d + k, phases, s[1], s[2]);
+        return k + history_width();
     }
 };
 

@@ -277,39 +277,141 @@ sr_bfs* sr_gpu_bfs_spawn_plugin_partitioned(const sr_plugin* pl, sr_dist* comm, 
     return spawn_plugin(pl, comm, comm ? 0 : std::max(vparts, 2), params, nparams, opts);
 }
 
+}  // extern "C"
+
+namespace sr {
+// A registered model built for host use only (no device tables), handed to f: the models whose
+// description determines the state (`undescribe`), for sr_model_fingerprint and the self-test.
+template <class F>
+static int with_host_model(int model, const i64* p, int np, F&& f) {
+    auto need = [&](int k) {
+        if (np < k) throw Error(SR_ERR_ARG, "model " + std::to_string(model) + " needs " + std::to_string(k) + " params");
+    };
+    switch (model) {
+        case SR_MODEL_LINEAR_EQUATION:
+            need(3);
+            return f(LinearEquation{(u32)(p[0] & 0xff), (u32)(p[1] & 0xff), (u32)(p[2] & 0xff)});
+        case SR_MODEL_BINARY_CLOCK: return f(BinaryClock{});
+        case SR_MODEL_2PC:
+            need(1);
+            if (p[0] < 1 || p[0] > 14) throw Error(SR_ERR_UNSUPPORTED, "2pc: rm_count must be in 1..=14");
+            return f(TwoPhase{(int)p[0]});
+        case SR_MODEL_INCREMENT:
+            need(1);
+            if (p[0] < 1 || p[0] > 15) throw Error(SR_ERR_UNSUPPORTED, "increment: threads must be in 1..=15");
+            return p[0] <= 9 ? f(Increment<1>{(int)p[0]}) : f(Increment<2>{(int)p[0]});
+        case SR_MODEL_INCREMENT_LOCK:
+            need(1);
+            if (p[0] < 1 || p[0] > 12) throw Error(SR_ERR_UNSUPPORTED, "increment_lock: threads must be in 1..=12");
+            return p[0] <= 8 ? f(IncrementLock<1>{(int)p[0]}) : f(IncrementLock<2>{(int)p[0]});
+        case SR_MODEL_PAXOS:
+            need(1);
+            if (p[0] < 1 || p[0] > px::MAX_CLIENTS) throw Error(SR_ERR_UNSUPPORTED, "paxos: client_count must be in 1..=6");
+            return p[0] <= Paxos::max_clients() ? f(Paxos::make((int)p[0])) : f(PaxosWide::make((int)p[0]));
+        case SR_MODEL_PINGPONG: {
+            need(1);
+            if (p[0] < 0 || p[0] > 7) throw Error(SR_ERR_UNSUPPORTED, "ping-pong: max_nat must be in 0..=7");
+            PingPong m;
+            m.max_nat = (u32)p[0];
+            m.lossy = np > 1 && p[1] != 0;
+            m.duplicating = np > 2 ? p[2] != 0 : true;
+            m.maintains_history = np > 3 && p[3] != 0;
+            return f(m);
+        }
+        case SR_MODEL_ACTOR_FIXTURE: {
+            need(1);
+            ActorFixture m;
+            m.kind = (int)p[0];
+            return f(m);
+        }
+        case SR_MODEL_ABD: {
+            need(1);
+            AbdRegister m;
+            static_cast<act::AbdSys&>(m) = act::AbdSys::make((int)p[0], np > 1 ? (int)p[1] : 2, -1);
+            return f(m);
+        }
+        case SR_MODEL_SINGLE_COPY: {
+            need(1);
+            SingleCopyRegister m;
+            static_cast<act::SingleCopySys&>(m) = act::SingleCopySys::make((int)p[0], np > 1 ? (int)p[1] : 1);
+            return f(m);
+        }
+        default:
+            return SR_ERR_UNSUPPORTED;
+    }
+}
+
+// Host BFS over up to max_states reachable states of m: every state's description must give the
+// state back (undescribe) and so the engine's fingerprint of it. Returns the states checked.
+template <class M>
+static i64 describe_roundtrip(const M& m, i64 max_states, std::string& why) {
+    if constexpr (!has_undescribe<M>::value) {
+        why = "model has no state description inverse";
+        return SR_ERR_UNSUPPORTED;
+    } else {
+        constexpr int W = M::W, MW = M::MW;
+        struct H {
+            size_t operator()(const std::vector<u64>& v) const {
+                u64 h = 0;
+                for (u64 x : v) h = fmix64(h ^ x) + 0x9E3779B97F4A7C15ull;
+                return (size_t)h;
+            }
+        };
+        std::unordered_set<std::vector<u64>, H> seen;
+        std::vector<std::vector<u64>> queue;
+        const std::vector<u64> inits = init_states_of(m);
+        for (size_t i = 0; i + W <= inits.size(); i += W) {
+            std::vector<u64> st(inits.begin() + (i64)i, inits.begin() + (i64)(i + W));
+            if (seen.insert(st).second) queue.push_back(st);
+        }
+        std::vector<i64> d((size_t)m.describe_width());
+        for (size_t q = 0; q < queue.size() && (i64)q < max_states; ++q) {
+            const std::vector<u64> st = queue[q];
+            m.describe(st.data(), d.data());
+            u64 back[W];
+            m.undescribe(d.data(), back);
+            if (!std::equal(back, back + W, st.data())) {
+                why = "state " + std::to_string(q) + " does not survive describe -> undescribe";
+                return SR_ERR_ARG;
+            }
+            u64 fp = 0;
+            if (described_fingerprint(m, d.data(), (int)d.size(), &fp) != SR_OK || fp != state_fp<M>(st.data())) {
+                why = "state " + std::to_string(q) + ": sr_model_fingerprint differs from the engine's fingerprint";
+                return SR_ERR_ARG;
+            }
+            u64 mk[MW], o[W];
+            m.enabled(st.data(), mk);
+            for (int w = 0; w < MW; ++w)
+                for (u64 bits = mk[w]; bits; bits &= bits - 1) {
+                    const int a = w * 64 + __builtin_ctzll(bits);
+                    if (!m.apply(st.data(), a, o)) continue;
+                    std::vector<u64> nx(o, o + W);
+                    if (seen.insert(nx).second) queue.push_back(std::move(nx));
+                }
+        }
+        return (i64)std::min<size_t>(queue.size(), (size_t)max_states);
+    }
+}
+}  // namespace sr
+
+extern "C" {
+
 int32_t sr_model_fingerprint(int32_t model, const int64_t* p, int32_t np, const int64_t* d, int32_t width, uint64_t* fp) {
     try {
-        auto need = [&](int k) {
-            if (np < k) throw Error(SR_ERR_ARG, "model " + std::to_string(model) + " needs " + std::to_string(k) + " params");
-        };
-        int r = SR_ERR_UNSUPPORTED;
-        switch (model) {
-            case SR_MODEL_LINEAR_EQUATION:
-                need(3);
-                r = described_fingerprint(LinearEquation{(u32)(p[0] & 0xff), (u32)(p[1] & 0xff), (u32)(p[2] & 0xff)}, d, width, fp);
-                break;
-            case SR_MODEL_BINARY_CLOCK: r = described_fingerprint(BinaryClock{}, d, width, fp); break;
-            case SR_MODEL_2PC:
-                need(1);
-                if (p[0] < 1 || p[0] > 14) throw Error(SR_ERR_UNSUPPORTED, "2pc: rm_count must be in 1..=14");
-                r = described_fingerprint(TwoPhase{(int)p[0]}, d, width, fp);
-                break;
-            case SR_MODEL_INCREMENT:
-                need(1);
-                if (p[0] < 1 || p[0] > 15) throw Error(SR_ERR_UNSUPPORTED, "increment: threads must be in 1..=15");
-                r = p[0] <= 9 ? described_fingerprint(Increment<1>{(int)p[0]}, d, width, fp)
-                              : described_fingerprint(Increment<2>{(int)p[0]}, d, width, fp);
-                break;
-            case SR_MODEL_INCREMENT_LOCK:
-                need(1);
-                if (p[0] < 1 || p[0] > 12) throw Error(SR_ERR_UNSUPPORTED, "increment_lock: threads must be in 1..=12");
-                r = p[0] <= 8 ? described_fingerprint(IncrementLock<1>{(int)p[0]}, d, width, fp)
-                              : described_fingerprint(IncrementLock<2>{(int)p[0]}, d, width, fp);
-                break;
-            default:
-                break;
-        }
+        const int r = with_host_model(model, p, np, [&](const auto& m) { return described_fingerprint(m, d, width, fp); });
         if (r != SR_OK) set_error(r == SR_ERR_UNSUPPORTED ? "model has no state description inverse" : "bad description width");
+        return r;
+    } catch (const Error& x) {
+        set_error(x.what());
+        return x.code;
+    }
+}
+
+int64_t sr_selftest_describe(int32_t model, const int64_t* p, int32_t np, int64_t max_states) {
+    try {
+        std::string why;
+        const i64 r = with_host_model(model, p, np, [&](const auto& m) { return (int)describe_roundtrip(m, max_states, why); });
+        if (r < 0) set_error(why);
         return r;
     } catch (const Error& x) {
         set_error(x.what());

@@ -1167,8 +1167,12 @@ class Engine final : public EngineBase {
                     undiscovered, nullptr, sq, 0u, ppw_log2, filt_log2_, sw);
             };
             if (o_.counters) launch(expand_fast<M, 0, 0, true>);
-            else if (probe_batch_ == 1) launch(expand_fast<M, 1, 0>);
-            else launch(expand_fast<M, 0, 0>);
+            else switch (probe_batch_) {
+                case 1: launch(expand_fast<M, 1, 0>); break;
+                case -4: launch(expand_fast<M, -4, 0>); break;
+                case -8: launch(expand_fast<M, -8, 0>); break;
+                default: launch(expand_fast<M, 0, 0>); break;
+            }
         }, n);
         slot_seq_ = sq;
         slot_published_ = false;
@@ -1246,8 +1250,12 @@ class Engine final : public EngineBase {
                                 last ? 1u : 0u, ppw_log2, filt_log2_, sw);
                         };
                         if (o_.counters) launch(expand_fast<M, 0, 0, true>);
-                        else if (probe_batch_ == 1) launch(expand_fast<M, 1, 0>);
-                        else launch(expand_fast<M, 0, 0>);
+                        else switch (probe_batch_) {
+                            case 1: launch(expand_fast<M, 1, 0>); break;
+                            case -4: launch(expand_fast<M, -4, 0>); break;
+                            case -8: launch(expand_fast<M, -8, 0>); break;
+                            default: launch(expand_fast<M, 0, 0>); break;
+                        }
                     });
                 }
                 return sq;
@@ -1335,7 +1343,7 @@ class Engine final : public EngineBase {
     u32 D_;  // max successors of one state (bounds the new states a chunk can create)
     u32 emask_;  // the model's `eventually` properties
     bool fifo_ = false;
-    int probe_batch_ = 0;  // expand_fast's probe loop: 0 the lane queue, 1 rounds of one successor per lane (SR_PROBE_BATCH)
+    int probe_batch_ = 1;  // expand_fast's probe loop (SR_PROBE_BATCH): 1 rounds of one successor per lane, 0 the lane queue, -R per-lane register queues over R rounds
     int ppw_env_ = -1;
     bool table_recycle_ = true;  // the visited set is returned zeroed (~Engine)
     u32 grid_max_ = 0;      // cap on expand_fast's grid, 0 = two device residencies (SR_GRID_MAX)

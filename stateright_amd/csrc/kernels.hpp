@@ -686,7 +686,7 @@ __device__ u64* g_timeline;
 // Wide states (W >= 4: paxos, the actor models) run three waves per SIMD (<= 168 VGPRs): their
 // levels are latency-bound, and paxos' device-side history search had pushed them to two.
 template <class M, int PB, int POL, bool STATS = false>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W >= 4 ? 3 : 1))) expand_fast(M m, const u64* __restrict__ frontier, u32 lo, u32 hi,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W >= 4 ? 3 : PB < 0 ? 6 : 1))) expand_fast(M m, const u64* __restrict__ frontier, u32 lo, u32 hi,
                                                    TableView t, u64* __restrict__ next, u32* __restrict__ next_par,
                                                    u32 next_cap, LevelCounters* lc, u32 undiscovered,
                                                    HostCounters* hc, u32 seq, u32 reset, u32 ppw_log2,
@@ -948,6 +948,121 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W >
         tl_first_chunk = false;
 #endif
 
+        if constexpr (PB < 0) {
+            // Per-lane probe queue over R = -PB rounds of the window (DESIGN.md §3 "probe loops").
+            // Phase A expands R rounds of successors with every lane busy (apply, fingerprint, the
+            // LDS filter) and keeps each lane's probe keys in registers; phase B walks each lane's
+            // keys one visited-set access per iteration (home load, linear-probe step or claim CAS),
+            // a lane moving to its next key as soon as one resolves, so the wave's round trips are
+            // not each as long as its slowest lane's chain. New states are appended after phase B
+            // (their states recomputed from the map: only ~1 successor in 8 is new).
+            constexpr int R = -PB;
+            // without a packed key the table is always in fingerprint mode: home = tag & mask
+            constexpr bool FP_ONLY = !(has_qkey<M>::value && M::W >= 2);
+            for (u32 s0 = w0; s0 < wend; s0 += 64u * R) {
+                u64 kh[FP_ONLY ? 1 : R], kt[R];  // home slot and slot value of round r's successor
+                u32 vmask = 0;     // bit r: round r's successor is probed
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    if (!FP_ONLY) kh[FP_ONLY ? 0 : r] = 0;
+                    kt[r] = 0;
+                    const u32 i = s0 + (u32)r * 64u + (u32)lane;
+                    if (i < wend) {
+                        const u32 e = smap[wid][i - w0];
+                        const u32 p = e & 63, a = e >> 6;
+                        u64 ps[W], q[W];
+#pragma unroll
+                        for (int x = 0; x < W; ++x) ps[x] = pst[wid][p * W + x];
+                        bool ok = m.apply(ps, (int)a, q);
+                        if (ok) {
+                            ++succ;  // within boundary: counted once, whatever follows
+                            ok = !same_state<W>(q, ps);  // self-loop: never probed
+                        }
+                        if (ok) {
+                            const ProbeKey k = probe_key(m, t, q);
+                            if (fmask) {  // block-local duplicate filter (see the round loop below)
+                                const u64 old = atomicExch(reinterpret_cast<unsigned long long*>(&filt[(u32)(k.tag >> 40) & fmask]),
+                                                           (unsigned long long)k.tag);
+                                ok = old != k.tag;
+                            }
+                            if (!FP_ONLY) kh[FP_ONLY ? 0 : r] = k.home;
+                            kt[r] = k.tag;
+                        }
+                        if (ok) vmask |= 1u << r;
+                    }
+                }
+#if SR_TIMELINE
+                if (tl_first_round) SR_TL(4);
+#endif
+                u32 nmask = 0;  // bit r: round r's successor claimed a vacant slot (a new state)
+                u32 st = 0, cr = 0, disp = 0;  // 0 idle, 1 load pending, 2 claim pending; its round
+                u64 si = 0, tag = 0;
+                const u64 step = probe_step(t);
+                for (;;) {
+                    if (st == 0 && vmask) {
+                        cr = (u32)__builtin_ctz(vmask);
+                        vmask &= vmask - 1;
+                        tag = kt[0];
+#pragma unroll
+                        for (int r = 1; r < R; ++r)
+                            if (cr == (u32)r) tag = kt[r];
+                        if constexpr (FP_ONLY) {
+                            si = tag & t.mask;
+                        } else {
+                            si = kh[0];
+#pragma unroll
+                            for (int r = 1; r < R; ++r)
+                                if (cr == (u32)r) si = kh[FP_ONLY ? 0 : r];
+                        }
+                        st = 1;
+                        disp = 0;
+                    }
+                    if (!__ballot(st != 0)) break;
+                    u64 v = 0;
+                    if (st == 1) v = probe_load<POL>(&t.keys[si]);
+                    if (st == 2) v = atomicCAS(reinterpret_cast<unsigned long long*>(&t.keys[si]), 0ull, (unsigned long long)tag);
+                    if constexpr (STATS) {
+                        probes += st == 1;
+                        cas += st == 2;
+                    }
+                    if (st != 0) {
+                        if (v == tag) {
+                            st = 0;  // visited already (or claimed by a concurrent duplicate)
+                        } else if (v == 0) {
+                            if (st == 2) nmask |= 1u << cr;  // our claim won
+                            st = st == 1 ? 2u : 0u;
+                        } else if (++disp >= t.plimit) {
+                            atomicOr(&lc->err, (u32)ERR_TABLE_FULL);
+                            st = 0;
+                        } else {  // another key: the next slot
+                            si = (si + 1) & t.mask;
+                            tag += step;
+                            st = 1;
+                        }
+                    }
+                }
+#if SR_TIMELINE
+                if (tl_first_round) SR_TL(5);
+                tl_first_round = false;
+#endif
+                // the new states, round by round (their states recomputed from the map)
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const bool nw = nmask >> r & 1;
+                    u64 q[W];
+                    u32 p = 0;
+                    if (nw) {
+                        const u32 e = smap[wid][s0 + (u32)r * 64u + (u32)lane - w0];
+                        p = e & 63;
+                        u64 ps[W];
+#pragma unroll
+                        for (int x = 0; x < W; ++x) ps[x] = pst[wid][p * W + x];
+                        m.apply(ps, (int)(e >> 6), q);
+                    }
+                    append_new(nw, q, p);
+                }
+            }
+        } else
         if constexpr (PB == 0) {
             // Lane work queue (the default, DESIGN.md §3 "Probe rounds as a lane queue"). A lane owns
             // one successor at a time and issues exactly one visited-set access per iteration for it:

@@ -174,6 +174,27 @@ inline i64 acc_code(u32 acc) {
     if (!(acc & 128)) return 0;
     return 1 + (i64)(acc >> 5 & 3) * 64 + (i64)(acc >> 3 & 3) * 8 + (i64)(acc & 7) + 3;
 }
+// Inverses (sr_model_fingerprint: a described state back to its words).
+inline u32 acc_decode(i64 code) {
+    if (code <= 0) return 0;
+    const i64 c = code - 1, round = c / 64, id = c / 8 % 8, req = c % 8;
+    return 128u | (u32)((round << 2 | id) << 3) | (u32)(req - 3);
+}
+inline u32 env_decode(i64 code) {
+    const u32 src = (u32)(code % 16), dst = (u32)(code / 16 % 16), kind = (u32)(code / 256 % 16);
+    const i64 f = code / 4096;
+    auto bal = [](i64 b) { return (u32)((b / 8) << 2 | (b % 8)); };
+    switch (kind) {
+        case PREPARE: case ACCEPTED: return env(src, dst, kind, bal(f), 0);
+        case PREPARED: return env(src, dst, kind, bal(f / 4096), acc_decode(f % 4096));
+        case ACCEPT: case DECIDED: return env(src, dst, kind, bal(f / 16), (u32)(f % 16));
+        case GETOK: {
+            const i64 v = f % 256;
+            return env(src, dst, kind, 0, v ? (u32)(v - 'A' + 1) : 0u);
+        }
+        default: return env(src, dst, kind, 0, 0);
+    }
+}
 inline i64 env_code(u32 e) {
     const u32 kind = e_kind(e);
     const i64 bal = (i64)(e_bal(e) >> 2) * 8 + (e_bal(e) & 3);
@@ -276,13 +297,45 @@ struct Hist {
     }
 };
 
+// The canonical description of a history (oracle/paxos.hpp describe_register_history): per
+// client c its Get's returned value (-1 before it returned), then per other client u the number of
+// u's ops completed when c invoked its Get (-1 before the Get). C * C values.
+inline void describe_hist(const Hist& h, int C, i64* d) {
+    int k = 0;
+    for (int c = 0; c < C; ++c) {
+        const size_t nd = h.done[c].size();
+        const std::vector<int>* last = nd >= 2 ? &h.done[c][1].last : nd == 1 && h.inflight[c].some ? &h.inflight[c].last : nullptr;
+        const int v = nd >= 2 ? h.done[c][1].ret_value : 0;
+        d[k++] = nd >= 2 ? (v ? (i64)(v - 'A' + 1) : 0) : -1;
+        for (int u = 0; u < C; ++u)
+            if (u != c) d[k++] = last ? (i64)(*last)[u] + 1 : -1;
+    }
+}
+
 // Host-compiled history tables, one copy per (process, C) plus one device copy per GPU.
 struct Tables {
     int C = 0, nh = 0, nev = 0;
     u32 init_hist = 0;
     std::vector<u16> h_next;  // [h * nev + event], 0xffff = never occurs
     std::vector<u8> h_lin;    // linearizable per history
+    std::vector<Hist> hists;  // the interned histories (describe)
     std::map<int, std::pair<u16*, u8*>> dev;  // device copies (process lifetime)
+    // The index of a described history (undescribe); throws if no reachable history has it.
+    u32 hist_index(const i64* d) {
+        static std::mutex mu;
+        std::lock_guard<std::mutex> g(mu);
+        if (by_desc_.empty()) {
+            std::vector<i64> k((size_t)(C * C));
+            for (size_t h = 0; h < hists.size(); ++h) {
+                describe_hist(hists[h], C, k.data());
+                by_desc_.emplace(k, (u32)h);
+            }
+        }
+        auto it = by_desc_.find(std::vector<i64>(d, d + C * C));
+        if (it == by_desc_.end()) throw Error(SR_ERR_ARG, "register history: no reachable history has this description");
+        return it->second;
+    }
+    std::map<std::vector<i64>, u32> by_desc_;
 };
 
 inline Tables compile(int C) {
@@ -332,6 +385,7 @@ inline Tables compile(int C) {
             if (rows[k][ev] >= 0) T.h_next[(size_t)k * T.nev + ev] = (u16)rows[k][ev];
         T.h_lin[k] = H[k].linearizable() ? 1 : 0;
     }
+    T.hists = std::move(H);
     return T;
 }
 
@@ -521,6 +575,35 @@ struct PaxosHist {
         return false;
     }
     static constexpr u32 MAXC = px::MAX_CLIENTS;
+
+    // Canonical description of the history (oracle/paxos.hpp describe_register_history): per
+    // client c its Get's returned value (-1 before the Get returned), then per other client u how
+    // many of u's ops had completed when c invoked its Get (-1 before the Get). C * C values.
+    int width() const { return (int)(C * C); }
+    void describe(u64 lo, u64 hi, i64* d) const {
+        int k = 0;
+        for (u32 c = 0; c < C; ++c) {
+            const u32 ph = phase(lo, hi, c);
+            d[k++] = ph == 2 ? (i64)ret(lo, hi, c) : -1;
+            for (u32 u = 0; u < C; ++u)
+                if (u != c) d[k++] = ph >= 1 ? (i64)last(lo, hi, c, u) : -1;
+        }
+    }
+    // Inverse, given every client's phase (op_count - 1, described with the actors).
+    void undescribe(const i64* d, const u32* phases, u64& lo, u64& hi) const {
+        lo = hi = 0;
+        int k = 0;
+        for (u32 c = 0; c < C; ++c) {
+            put(lo, hi, 2 * c, 2, phases[c]);
+            const i64 r = d[k++];
+            if (r >= 0) put(lo, hi, ret_off(c), 3, (u64)r);
+            for (u32 u = 0; u < C; ++u) {
+                if (u == c) continue;
+                const i64 l = d[k++];
+                if (l >= 0) put(lo, hi, last_off(c, u), 2, (u64)l);
+            }
+        }
+    }
 };
 
 // W = 11 holds the history of up to 4 clients in the 3 x 17 bits the servers leave free; W = 12
@@ -708,7 +791,7 @@ struct PaxosT {
     int expectation(int p) const { return p == 0 ? ALWAYS : SOMETIMES; }
     const char* prop_name(int p) const { return p == 0 ? "linearizable" : "value chosen"; }
     // The oracle's canonical description (oracle/paxos.hpp describe).
-    int describe_width() const { return 3 * 9 + C + 16; }
+    int describe_width() const { return 3 * 9 + C + 16 + hs().width(); }
     void describe(const u64* s, i64* d) const {
         int k = 0;
         for (int i = 0; i < 3; ++i) {
@@ -728,6 +811,39 @@ struct PaxosT {
         std::sort(net.begin(), net.end());
         net.resize(16, -1);
         for (i64 v : net) d[k++] = v;
+        u64 lo, hi;
+        hist_get(s, lo, hi);
+        hs().describe(lo, hi, d + k);
+    }
+    // The state of a description (sr_model_fingerprint): the inverse of describe.
+    void undescribe(const i64* d, u64* s) const {
+        u64 w[4] = {0, 0, 0, 0};
+        int k = 0;
+        for (int i = 0; i < 3; ++i) {
+            px::Srv v{};
+            v.bal = (u32)(d[k] << 2 | d[k + 1]);
+            k += 2;
+            v.prop = d[k] < 0 ? 0u : (u32)d[k];
+            ++k;
+            for (int j = 0; j < 3; ++j, ++k) v.prep[j] = d[k] < 0 ? 0u : 256u | px::acc_decode(d[k]);
+            v.accepts = (u32)d[k++];
+            v.accepted = px::acc_decode(d[k++]);
+            v.decided = (u32)d[k++];
+            w[i] = v.store();
+        }
+        u32 phases[px::MAX_CLIENTS];
+        for (int c = 0; c < C; ++c) phases[c] = (u32)(d[k++] - 1);
+        u32 net[px::SLOTS];
+        int n = 0;
+        for (int j = 0; j < 16; ++j, ++k)
+            if (d[k] >= 0) net[n++] = px::env_decode(d[k]);
+        std::sort(net, net + n);
+        for (int j = n; j < px::SLOTS; ++j) net[j] = px::EMPTY;
+        u64 lo, hi;
+        hs().undescribe(d + k, phases, lo, hi);
+        hist_set(w, lo, hi);
+        for (int i = 0; i < NET0; ++i) s[i] = w[i];
+        for (int j = 0; j < px::SLOTS / 2; ++j) s[NET0 + j] = (u64)net[2 * j] | (u64)net[2 * j + 1] << 32;
     }
     i64 action_id(const u64* s, int a) const { return px::env_code(slot(s, a)); }
     i64 action_id_bound() const { return 0; }  // ids are sparse envelope codes

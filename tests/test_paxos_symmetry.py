@@ -91,7 +91,7 @@ def apply_g(v, c, ps, pc, data):
         nb[:, 8] = blk[:, 8]
     for k in range(c):
         out[:, 27 + int(pc[k])] = v[:, 27 + k]
-    net = v[:, 27 + c:]
+    net = v[:, 27 + c:27 + c + 16]
     code = np.where(net >= 0, net, 0)
     src, dst, kind, f = code % 16, (code // 16) % 16, (code // 256) % 16, code // 4096
     nsrc, ndst = actor[src], actor[dst]
@@ -114,7 +114,19 @@ def apply_g(v, c, ps, pc, data):
     ncode = (((nf * 16) + kind) * 16 + ndst) * 16 + nsrc
     ncode = np.where(net >= 0, ncode, np.iinfo(np.int64).max)
     ncode.sort(axis=1)
-    out[:, 27 + c:] = np.where(ncode == np.iinfo(np.int64).max, -1, ncode)
+    out[:, 27 + c:27 + c + 16] = np.where(ncode == np.iinfo(np.int64).max, -1, ncode)
+    # the register history (oracle/paxos.hpp describe_register_history): per client k its Get's
+    # returned value, then its `last` entries for the other clients in ascending order
+    h0 = 27 + c + 16
+    for k in range(c):
+        nk = int(pc[k])
+        ret = v[:, h0 + k * c]
+        if data:  # a value is a client's letter: it follows the client
+            ret = np.where(ret > 0, 1 + pc[np.clip(ret - 1, 0, c - 1)], ret)
+        out[:, h0 + nk * c] = ret
+        others, nothers = [u for u in range(c) if u != k], [u for u in range(c) if u != nk]
+        for i, u in enumerate(others):
+            out[:, h0 + nk * c + 1 + nothers.index(int(pc[u]))] = v[:, h0 + k * c + 1 + i]
     return out
 
 

@@ -62,4 +62,4 @@ def test_model_fingerprint_registered_models():
     assert model_fingerprint(LinearEquation(2, 4, 7), [3, 5]) == fp1(3 | 5 << 8)
     from stateright_amd import Paxos
     with pytest.raises(ValueError):
-        model_fingerprint(Paxos(2), [0] * 45)  # paxos descriptions omit the history: no inverse
+        model_fingerprint(Paxos(2), [0] * 45)  # a description of the wrong width (paxos C=2: 49)
