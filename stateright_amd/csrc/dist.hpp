@@ -1687,7 +1687,7 @@ class DistEngine final : public EngineBase {
             const u32 ppw_log2 = std::max<u32>(2, std::min<u32>(6, ppw_for(n)));
             const u32 grid = std::max<u32>(1, blocks_for((n + (1u << ppw_log2) - 1) >> ppw_log2, 4));
             p0.seq++;
-            expand_fast<M, 0, 0><<<grid, 256, filt_log2_ ? (8u << filt_log2_) : 0u, stream_>>>(
+            expand_fast<M, 1, 0><<<grid, 256, filt_log2_ ? (8u << filt_log2_) : 0u, stream_>>>(
                 m_, harena_.p + fb * W, 0u, (u32)n, hv, harena_.p + nb * W, hpar_.p + nb, ncap, p0.lc, und, p0.hc_dev, p0.seq,
                 1u, ppw_log2, filt_log2_, SlotWork{});
             SR_HIP(hipGetLastError());

@@ -1133,7 +1133,7 @@ class Engine final : public EngineBase {
         if (grid_max_) return grid_max_;
         int per_cu = 0, cus = 0;
         const size_t dyn = filt_log2_ ? (8u << filt_log2_) : 0u;
-        const void* k = probe_batch_ == 1 ? (const void*)expand_fast<M, 1, 0> : (const void*)expand_fast<M, 0, 0>;
+        const void* k = probe_loop() < 0 ? (const void*)expand_fast<M, -4, 0> : (const void*)expand_fast<M, 1, 0>;
         SR_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 256, dyn));
         SR_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, o_.device));
         grid_max_ = per_cu > 0 && cus > 0 ? (u32)(2 * per_cu * cus) : ~0u;
@@ -1167,13 +1167,9 @@ class Engine final : public EngineBase {
                     m_, arena_.p + fbase * W, 0u, n, view(), arena_.p + nbase * W, apar_.p + nbase, ncap, lc,
                     undiscovered, nullptr, sq, 0u, ppw_log2, filt_log2_, sw);
             };
-            if (o_.counters) launch(expand_fast<M, 0, 0, true>);
-            else switch (probe_batch_) {
-                case 1: launch(expand_fast<M, 1, 0>); break;
-                case -4: launch(expand_fast<M, -4, 0>); break;
-                case -8: launch(expand_fast<M, -8, 0>); break;
-                default: launch(expand_fast<M, 0, 0>); break;
-            }
+            if (o_.counters) launch(expand_fast<M, 1, 0, true>);
+            else if (probe_loop() < 0) launch(expand_fast<M, -4, 0>);
+            else launch(expand_fast<M, 1, 0>);
         }, n);
         slot_seq_ = sq;
         slot_published_ = false;
@@ -1250,13 +1246,9 @@ class Engine final : public EngineBase {
                                 m_, cur(), ulo, uhi, view(), next, npar, ncap, lc_d_, undiscovered, hcd(sq), sq,
                                 last ? 1u : 0u, ppw_log2, filt_log2_, sw);
                         };
-                        if (o_.counters) launch(expand_fast<M, 0, 0, true>);
-                        else switch (probe_batch_) {
-                            case 1: launch(expand_fast<M, 1, 0>); break;
-                            case -4: launch(expand_fast<M, -4, 0>); break;
-                            case -8: launch(expand_fast<M, -8, 0>); break;
-                            default: launch(expand_fast<M, 0, 0>); break;
-                        }
+                        if (o_.counters) launch(expand_fast<M, 1, 0, true>);
+                        else if (probe_loop() < 0) launch(expand_fast<M, -4, 0>);
+                        else launch(expand_fast<M, 1, 0>);
                     });
                 }
                 return sq;
@@ -1345,7 +1337,16 @@ class Engine final : public EngineBase {
     u32 emask_;  // the model's `eventually` properties
     bool fifo_ = false;
     bool xcd_map_ = false;  // XCD-aware chunk order in expand_fast (SR_XCD_MAP)
-    int probe_batch_ = 1;  // expand_fast's probe loop (SR_PROBE_BATCH): 1 rounds of one successor per lane, 0 the lane queue, -R per-lane register queues over R rounds
+    int probe_batch_ = 0;  // SR_PROBE_BATCH: 1 forces the probe rounds, -4 the per-lane probe queues (0: probe_loop)
+    // expand_fast's probe loop (DESIGN.md §3 "Probe loops"): rounds of one successor per lane, or
+    // per-lane queues over 4 rounds (-4) once the visited set is far beyond the 256 MB Infinity
+    // Cache (>= 2^27 slots), where each probe is a longer round trip: 2pc N=10 -7 %, N=11 -6 %,
+    // N=9 (2^25 slots) +6 % (profiles/r05_probe_loops.txt). Fingerprint-mode narrow states only.
+    int probe_loop() const {
+        if (probe_batch_) return probe_batch_ < 0 ? -4 : 1;
+        constexpr bool fp_only = !(has_qkey<M>::value && M::W >= 2);
+        return fp_only && W < 4 && cap_ >= (1ull << 27) ? -4 : 1;
+    }
     int ppw_env_ = -1;
     bool table_recycle_ = true;  // the visited set is returned zeroed (~Engine)
     u32 grid_max_ = 0;      // cap on expand_fast's grid, 0 = two device residencies (SR_GRID_MAX)

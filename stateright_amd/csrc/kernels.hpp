@@ -34,7 +34,7 @@ constexpr int MAX_PROPS = 32;
 constexpr int MAX_PARTS = 64;  // visited-set partitions (one per GPU, or virtual ones on one GPU)
 // expand_fast's largest parents per wave (log2) for wide states (W >= 4).
 #ifndef SR_WIDE_PPW_LOG2_MAX
-#define SR_WIDE_PPW_LOG2_MAX 4
+#define SR_WIDE_PPW_LOG2_MAX 5
 #endif
 // expand_fast's LDS stage of new states, in 64-bit words (its size sets the blocks per CU).
 #ifndef SR_STAGE_WORDS
@@ -1074,92 +1074,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W >
                     }
                     append_new(nw, q, p);
                 }
-            }
-        } else
-        if constexpr (PB == 0) {
-            // Lane work queue (the default, DESIGN.md §3 "Probe rounds as a lane queue"). A lane owns
-            // one successor at a time and issues exactly one visited-set access per iteration for it:
-            // the home-slot load, a linear-probe step's load, or the claim CAS. A lane whose successor
-            // is resolved takes the window's next entry at once (a wave-uniform cursor, ranked by
-            // ballot), so the wave's memory round trips stay full: in the round-based loop below, a
-            // round lasted as long as its slowest lane's dependent chain (load, step, CAS) while the
-            // other lanes idled, and lanes whose successor the LDS filter had removed idled a whole
-            // round.
-            u32 cursor = w0;                   // next window entry to hand out (wave-uniform)
-            u32 st = 0;                        // 0: needs an entry, 1: load pending, 2: claim pending
-            u64 q[W];                          // the lane's successor
-            u64 si = 0, tag = 0;               // its current slot and the value that slot would hold
-            u32 qpar = 0, disp = 0;            // parent (in the wave) and linear-probe displacement
-            const u64 step = probe_step(t);
-            const u64 lanes_below = (1ull << lane) - 1;
-            for (;;) {
-                // idle lanes take entries until each holds a successor to probe or the window is spent
-                for (;;) {
-                    const u64 need = __ballot(st == 0);
-                    if (!need || cursor >= wend) break;
-                    const u32 i = cursor + (u32)__popcll(need & lanes_below);
-                    cursor += (u32)__popcll(need);
-                    if (st == 0 && i < wend) {
-                        const u32 e = smap[wid][i - w0];
-                        const u32 p = e & 63, a = e >> 6;
-                        u64 ps[W];
-#pragma unroll
-                        for (int x = 0; x < W; ++x) ps[x] = pst[wid][p * W + x];
-                        bool ok = m.apply(ps, (int)a, q);
-                        if (ok) {
-                            ++succ;  // within boundary: counted once, whatever follows
-                            ok = !same_state<W>(q, ps);  // self-loop: never probed
-                        }
-                        if (ok) {
-                            const ProbeKey k = probe_key(m, t, q);
-                            // block-local duplicate filter (see the round loop below)
-                            if (fmask) {
-                                const u64 old = atomicExch(reinterpret_cast<unsigned long long*>(&filt[(u32)(k.tag >> 40) & fmask]),
-                                                           (unsigned long long)k.tag);
-                                ok = old != k.tag;
-                            }
-                            si = k.home;
-                            tag = k.tag;
-                        }
-                        if (ok) {
-                            st = 1;
-                            qpar = p;
-                            disp = 0;
-                        }
-                    }
-                }
-                if (!__ballot(st != 0)) break;
-#if SR_TIMELINE
-                if (tl_first_round) SR_TL(4);
-#endif
-                u64 v = 0;
-                if (st == 1) v = probe_load<POL>(&t.keys[si]);
-                if (st == 2) v = atomicCAS(reinterpret_cast<unsigned long long*>(&t.keys[si]), 0ull, (unsigned long long)tag);
-                if constexpr (STATS) {
-                    probes += st == 1;
-                    cas += st == 2;
-                }
-                bool nw = false;
-                if (st != 0) {
-                    if (v == tag) {
-                        st = 0;  // visited already (or claimed by a concurrent duplicate)
-                    } else if (v == 0) {
-                        nw = st == 2;  // our claim won
-                        st = st == 1 ? 2u : 0u;
-                    } else if (++disp >= t.plimit) {
-                        atomicOr(&lc->err, (u32)ERR_TABLE_FULL);
-                        st = 0;
-                    } else {  // another key: the next slot
-                        si = (si + 1) & t.mask;
-                        tag += step;
-                        st = 1;
-                    }
-                }
-#if SR_TIMELINE
-                if (tl_first_round) SR_TL(5);
-                tl_first_round = false;
-#endif
-                append_new(nw, q, qpar);
             }
         } else
         for (u32 it = w0; it < wend; it += 64 * PB) {
