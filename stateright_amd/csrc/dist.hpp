@@ -1044,7 +1044,7 @@ class DistEngine final : public EngineBase {
             // stale or partial slot is seen by its owner only (ERR_EXCHANGE, ERR_PEER_TIMEOUT), and
             // its rows may not reach the others. Same decision on every rank: `vote` depends only
             // on collectively agreed state.
-            const bool vote = comm_ && lag_ && direct_env_on() && comm_->direct_ok != 0;
+            const bool vote = comm_ && lag_ && direct_env_on() && comm_->direct_ok != 0 && vote_;
             int code = 0;  // 0 ok, 1 capacity restart, 2 exchange failure, 3 other error
             std::string what;
             int ecode = 0;
@@ -2328,6 +2328,8 @@ class DistEngine final : public EngineBase {
     i64 corrupt_level_ = std::getenv("SR_DX_CORRUPT_LEVEL") ? std::atoll(std::getenv("SR_DX_CORRUPT_LEVEL")) : -1;
     // the exchange check (SR_DX_CHECK=0 turns it off: measurements only)
     bool xcheck_ = !(std::getenv("SR_DX_CHECK") && std::atoi(std::getenv("SR_DX_CHECK")) == 0);
+    // the outcome vote of the direct exchange (SR_DX_VOTE=0 skips it: measurements only)
+    bool vote_ = !(std::getenv("SR_DX_VOTE") && std::atoi(std::getenv("SR_DX_VOTE")) == 0);
     u32 send_cache_max_parts_ = std::getenv("SR_SEND_CACHE") ? (u32)std::atoi(std::getenv("SR_SEND_CACHE")) : 4;
     u64 glob_prev_ = 0;        // pipelined mode: global frontier of the last level read
     // replicated head (SR_HEAD_MAX: largest head frontier; 0 disables)
