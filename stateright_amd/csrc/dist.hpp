@@ -618,13 +618,21 @@ struct LocalComm final : Comm {
 // GPU, where RCCL refuses two ranks on the same device; `devices_distinct` is set when every rank
 // has its own GPU.
 struct ShmComm final : Comm {
+    static constexpr int MAX_RANKS = 240;
     struct Header {
         std::atomic<u64> arrived;
         std::atomic<u64> generation;
         std::atomic<u32> failed;
         std::atomic<u32> ready;  // READY once rank 0 has initialised this segment
+        // attach handshake: rank r > 0 writes a nonce of its own, rank 0 echoes it (ack), rank r
+        // confirms (attach |= CONFIRMED). Only a live rank 0 echoes, so a rank that opened a
+        // segment a crashed run left (already READY) gets no echo and opens the name again.
+        std::atomic<u64> attach[MAX_RANKS];
+        std::atomic<u64> ack[MAX_RANKS];
     };
+    static_assert(sizeof(Header) <= 4096, "the header fits its page");
     static constexpr u32 READY = 0x53524844u;
+    static constexpr u64 CONFIRMED = 1ull << 63;
     static constexpr size_t HDR = 4096;
     std::string name;
     size_t slot_bytes = 0;
@@ -642,21 +650,45 @@ struct ShmComm final : Comm {
         slot_bytes = slot;
         devices_distinct = distinct;
         bytes = HDR + slot_bytes * (size_t)w;
+        if (w > MAX_RANKS) throw Error(SR_ERR_ARG, "shm transport: at most 240 ranks");
         // Rank 0 removes a segment a crashed run may have left under this name and creates a fresh
         // one exclusively, with a zeroed header, marked READY last; the other ranks open it (no
-        // create) once it exists at full size, and wait for READY. A stale segment's barrier state
-        // therefore never reaches a new run through rank 0; callers still name segments per run.
-        int fd = -1;
+        // create) once it exists at full size, wait for READY and then attach (the handshake in
+        // Header): a rank that raced rank 0's unlink and opened the stale segment gets no echo
+        // there and opens the name again.
         const auto t0 = Clock::now();
         if (rank == 0) {
             (void)shm_unlink(name.c_str());
-            fd = shm_open(name.c_str(), O_CREAT | O_EXCL | O_RDWR, 0600);
+            int fd = shm_open(name.c_str(), O_CREAT | O_EXCL | O_RDWR, 0600);
             if (fd < 0) throw Error(SR_ERR_ARG, "shm_open(" + name + ", O_EXCL) failed");
             if (ftruncate(fd, (off_t)bytes) != 0) {
                 ::close(fd);
                 throw Error(SR_ERR_ARG, "ftruncate of the shared segment failed");
             }
-        } else {
+            map_fd(fd);
+            Header* h = hdr();
+            h->arrived.store(0);
+            h->generation.store(0);
+            h->failed.store(0);
+            for (int q = 0; q < MAX_RANKS; ++q) h->attach[q].store(0), h->ack[q].store(0);
+            h->ready.store(READY, std::memory_order_release);
+            // echo every rank's nonce until each has confirmed it
+            for (int pending = w - 1; pending > 0;) {
+                pending = 0;
+                for (int q = 1; q < w; ++q) {
+                    const u64 a = h->attach[q].load(std::memory_order_acquire);
+                    if (a & CONFIRMED) continue;
+                    ++pending;
+                    if (a && h->ack[q].load(std::memory_order_relaxed) != a) h->ack[q].store(a, std::memory_order_release);
+                }
+                if (pending && secs(t0, Clock::now()) > timeout_s) throw Error(SR_ERR_ARG, "shm transport: ranks never attached to " + name);
+                if (pending) usleep(100);
+            }
+            return;
+        }
+        const u64 nonce = (((u64)::getpid() << 20 ^ (u64)Clock::now().time_since_epoch().count() ^ (u64)r << 8) & ~CONFIRMED) | 1;
+        for (;;) {
+            int fd = -1;
             for (;;) {
                 fd = shm_open(name.c_str(), O_RDWR, 0600);
                 if (fd >= 0) {
@@ -668,23 +700,34 @@ struct ShmComm final : Comm {
                 if (secs(t0, Clock::now()) > timeout_s) throw Error(SR_ERR_ARG, "shm transport: rank 0 never created " + name);
                 usleep(1000);
             }
+            map_fd(fd);
+            Header* h = hdr();
+            const auto t1 = Clock::now();
+            bool ok = false;
+            while (secs(t1, Clock::now()) < 2.0) {  // READY, then the echo of our nonce
+                if (h->ready.load(std::memory_order_acquire) == READY) {
+                    h->attach[r].store(nonce, std::memory_order_release);
+                    if (h->ack[r].load(std::memory_order_acquire) == nonce) {
+                        ok = true;
+                        break;
+                    }
+                }
+                usleep(100);
+            }
+            if (ok) {
+                h->attach[r].store(nonce | CONFIRMED, std::memory_order_release);
+                return;
+            }
+            munmap(base, bytes);  // no live rank 0 behind this segment (yet): open the name again
+            base = nullptr;
+            if (secs(t0, Clock::now()) > timeout_s) throw Error(SR_ERR_ARG, "shm transport: " + name + " never became ready");
         }
+    }
+    void map_fd(int fd) {
         void* m = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
         ::close(fd);
         if (m == MAP_FAILED) throw Error(SR_ERR_ARG, "mmap of the shared segment failed");
         base = static_cast<char*>(m);
-        Header* h = hdr();
-        if (rank == 0) {
-            h->arrived.store(0);
-            h->generation.store(0);
-            h->failed.store(0);
-            h->ready.store(READY, std::memory_order_release);
-        } else {
-            while (h->ready.load(std::memory_order_acquire) != READY) {
-                if (secs(t0, Clock::now()) > timeout_s) throw Error(SR_ERR_ARG, "shm transport: " + name + " never became ready");
-                usleep(100);
-            }
-        }
     }
     ~ShmComm() override {
         ipc.close();
@@ -1077,7 +1120,7 @@ class DistEngine final : public EngineBase {
                     if (code == 3) throw Error(ecode, what);
                     throw Error(SR_ERR_HIP, "partitioned search: another rank failed");
                 }
-                if (hi == 2 || hi != lo) {  // a corrupt exchange somewhere, or ranks that disagree
+                if (hi == 2) {  // a corrupt exchange somewhere (only this falls back)
                     if (attempt >= 3) throw Error(SR_ERR_HIP, "partitioned search: the exchange failed repeatedly: " + what);
                     exchange_fallback(code == 2 ? what : std::string("another rank's exchange failed"));
                     continue;
@@ -1087,7 +1130,14 @@ class DistEngine final : public EngineBase {
                     gather_visits();
                     return;
                 }
-                if (attempt >= 3) throw Error(ecode, what);
+                // hi == 1: a capacity restart on every rank. Capacity errors travel in the rows and
+                // reach every rank at the same level, so a rank that finished cleanly (lo == 0)
+                // means they did not: said, and restarted like the others (the direct exchange kept).
+                if (lo != hi)
+                    std::fprintf(stderr, "[sr] rank %d: the ranks disagree on a capacity restart (this rank: %s); restarting on every rank\n",
+                                 comm_->rank, code ? what.c_str() : "finished");
+                if (attempt >= 3) throw Error(code ? ecode : SR_ERR_CAPACITY, code ? what : std::string("another rank ran out of capacity"));
+                if (!code) what = "another rank ran out of capacity";
             } else if (code == 0) {
                 gather_paths();
                 gather_visits();
@@ -1166,7 +1216,9 @@ class DistEngine final : public EngineBase {
         vst_.clear();
         vlev_.clear();
         if (!o_.record_visits) return;
-        const u32 last = max_depth;  // levels 0..max_depth hold states
+        // levels 0..max_depth hold states; after a target_state_count stop the last of them was
+        // generated but never popped, and the reference visits a state at its pop (bfs.rs:188)
+        const u32 md = max_depth.load(), last = target_stop_ && md > 0 ? md - 1 : md;
         auto fetch = [&](const u64* dev, u64 words, int root) {
             std::vector<u64> h(words);
             if (!words) return h;
@@ -1334,6 +1386,7 @@ class DistEngine final : public EngineBase {
         auto t_start = Clock::now();
         state_count = 0;
         unique = 0;
+        target_stop_ = false;
         max_depth = 0;
         reference_done = false;
         early_exit_ = false;
@@ -1517,6 +1570,7 @@ class DistEngine final : public EngineBase {
                 unique = unique_total;
                 reference_done = false;
                 early_exit_ = true;
+                target_stop_ = true;
                 break;
             }
             // discoveries among this level's states: the lowest (partition, rank) per property
@@ -1829,7 +1883,11 @@ class DistEngine final : public EngineBase {
             SR_HIP(hipGetLastError());
         }
     }
-    bool dcheck() const { return direct_ && xcheck_; }
+    // The exchange check guards what crosses from one partition's kernels to another's inside
+    // running kernels. With ONE partition in all (a one-rank communicator) every
+    // record is its own, written and read by consecutive launches of one stream: ordered by the
+    // kernel boundary, nothing to check (-0.07 ms per 2pc N=9 check, profiles/r05_rccl1_attribution.txt).
+    bool dcheck() const { return direct_ && xcheck_ && T_ > 1; }
     // memory of the direct exchange's flags and receive buffers (SR_DX_FINE=0: ordinary device
     // memory, measurements only)
     static int dx_kind() {
@@ -2344,6 +2402,7 @@ class DistEngine final : public EngineBase {
     std::vector<u64> hlstart_;          // head arena offset of each head level
     u64 grow_factor_ = 1;
     bool early_exit_ = false;
+    bool target_stop_ = false;  // the search stopped at a target_state_count level boundary
     std::vector<DiscAt> disc_at_;
     std::vector<std::vector<u64>> gl_lstart_;  // per partition: arena offset of each level
     std::vector<u64> gl_off_;

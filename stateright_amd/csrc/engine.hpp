@@ -307,7 +307,6 @@ class Engine final : public EngineBase {
         // Internal tuning knobs (not part of the ABI): successors per lane per probe round and
         // the visited-set load factor the capacity hint is sized for.
         if (const char* e = std::getenv("SR_PROBE_BATCH")) probe_batch_ = std::atoi(e);
-        if (const char* e = std::getenv("SR_XCD_MAP")) xcd_map_ = std::atoi(e) != 0;
         if (const char* e = std::getenv("SR_TABLE_LOAD")) table_load_ = std::atof(e), load_env_ = true;
         if (const char* e = std::getenv("SR_PPW_LOG2")) ppw_env_ = std::atoi(e);
         if (const char* e = std::getenv("SR_FILTER_LOG2")) filt_log2_ = (u32)std::atoi(e);
@@ -1153,7 +1152,7 @@ class Engine final : public EngineBase {
         seq_launch_[sq] = launch_frontier.size();
         // a slotted launch: it counts into its own slot and is published by its successor
         SlotWork sw = slot_work(dev_n);
-        sw.flags = flags | (xcd_map_ ? (u32)SLOT_XCD : 0u);
+        sw.flags = flags;
         if (dev_n) {  // speculative: the device checks its frontier against the room left (ERR_DEFERRED)
             const double room = lmax_ * (double)cap_ - (double)unique.load();
             sw.room = room > 0 ? (u64)room : 0ull;
@@ -1235,7 +1234,7 @@ class Engine final : public EngineBase {
                     const u32 ppw_log2 = ppw_env_ >= 0 ? (u32)ppw_env_ : ppw_for(c);
                     const u32 grid = std::min(expand_grid_cap(), blocks_for((c + (1u << ppw_log2) - 1) >> ppw_log2, 4));
                     SlotWork sw{};
-                    sw.flags = (repair ? (u32)SLOT_REPAIR : 0u) | (xcd_map_ ? (u32)SLOT_XCD : 0u);
+                    sw.flags = repair ? SLOT_REPAIR : 0u;
                     if (emask_ && peb) {
                         sw.peb = peb;
                         sw.naeb = aeb_.p + nbase;
@@ -1336,7 +1335,6 @@ class Engine final : public EngineBase {
     u32 D_;  // max successors of one state (bounds the new states a chunk can create)
     u32 emask_;  // the model's `eventually` properties
     bool fifo_ = false;
-    bool xcd_map_ = false;  // XCD-aware chunk order in expand_fast (SR_XCD_MAP)
     int probe_batch_ = 0;  // SR_PROBE_BATCH: 1 forces the probe rounds, -4 the per-lane probe queues (0: probe_loop)
     // expand_fast's probe loop (DESIGN.md §3 "Probe loops"): rounds of one successor per lane, or
     // per-lane queues over 4 rounds (-4) once the visited set is far beyond the 256 MB Infinity

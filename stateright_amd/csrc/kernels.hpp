@@ -377,19 +377,7 @@ enum SlotFlags : u32 {
     // claimed and appended after the ones the first pass appended; successors are not counted
     // again (the first pass counted every one of them).
     SLOT_REPAIR = 1,
-    // XCD-aware chunk assignment (xcd_block): the workgroups that share an XCD take consecutive
-    // chunks of the frontier.
-    SLOT_XCD = 2,
 };
-
-// T1 of the CDNA4 guide: workgroups are dealt round-robin over the 8 XCDs (b and b + 8 share one;
-// speed only, never correctness). The bijection below gives the workgroups of one XCD consecutive
-// logical indices, so that they expand neighbouring parents: siblings share successors (commuting
-// actions), and their duplicate probes then hit the same XCD's L2.
-__device__ __forceinline__ u32 xcd_block(u32 b, u32 n) {
-    const u32 x = b % 8, q = n / 8, r = n % 8;
-    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
-}
 struct SlotWork {
     const u32* prev_n;          // frontier size = the previous level's claims (nullptr: `hi` is exact);
                                 // prev_n[1] is that level's err word: a launch behind a failed level
@@ -757,7 +745,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W >
         return;
     }
     const u32 nblk = gridDim.x - (svc ? 1u : 0u);  // workgroups that expand parents
-    const u32 lblk = (sw.flags & SLOT_XCD) ? xcd_block(blockIdx.x, nblk) : blockIdx.x;  // chunk order
     // Each wave takes ppw = 2^ppw_log2 <= 64 parents (small levels use fewer parents per wave so
     // that their successors spread over more waves: shorter per-lane probe chains). The grid
     // strides over chunks of 4 waves (a pipelined launch is sized from an estimate of the frontier).
@@ -767,7 +754,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W >
     // The wave's first parents. A pipelined launch issues their load before it knows the frontier
     // size (any row below next_cap is inside the arena; rows past the frontier are never used), so
     // the two round trips overlap instead of following each other.
-    const u64 r_first = lo + (u64)lblk * chunk + ((u64)wid << ppw_log2) + lane;
+    const u64 r_first = lo + (u64)blockIdx.x * chunk + ((u64)wid << ppw_log2) + lane;
     u64 nxt[W];  // the wave's parents of its next chunk (here: its first)
     const bool spec_first = sw.prev_n && lane < (int)ppw && r_first < next_cap;
     if (spec_first) load_state<W>(frontier, r_first, nxt);
@@ -793,7 +780,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W >
     }
     SR_TL(1);
     const u32 fmask = filt_log2 ? (1u << filt_log2) - 1 : 0;
-    if (lo + (u64)lblk * chunk < hi)  // blocks past the frontier only take their ticket
+    if (lo + (u64)blockIdx.x * chunk < hi)  // blocks past the frontier only take their ticket
         for (u32 i = threadIdx.x; i < (fmask ? fmask + 1 : 0u); i += blockDim.x) filt[i] = 0;
     // One level: parents [lo, hi) of `frontier` into `next`.
     auto level = [&](const u64* __restrict__ frontier, u32 lo, u32 hi, u64* __restrict__ next,
@@ -803,7 +790,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W >
     // chunk's probes instead of stalling the chunk start.
     const u64 cstride = (u64)nblk * chunk;
     if (!spec_first && lane < (int)ppw && r_first < hi) load_state<W>(frontier, r_first, nxt);
-    for (u64 c0 = lo + (u64)lblk * chunk; c0 < hi; c0 += cstride) {
+    for (u64 c0 = lo + (u64)blockIdx.x * chunk; c0 < hi; c0 += cstride) {
         const u32 wave0 = (u32)(c0 + ((u64)wid << ppw_log2));  // first parent of the wave
         const u32 r = wave0 + lane;
         u32 cnt = 0;
@@ -1137,9 +1124,42 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W >
             if (tl_first_round) SR_TL(5);
             tl_first_round = false;
 #endif
-            // Append the new states of this round, aggregated per wave (append_new).
+            // Append the new states of this round, aggregated per wave: one LDS atomic reserves the
+            // wave's span of the stage; what does not fit goes straight to the next frontier with
+            // ONE global atomic for the wave (never one per state).
 #pragma unroll
-            for (int j = 0; j < PB; ++j) append_new(nw[j], ns[j], par[j]);
+            for (int j = 0; j < PB; ++j) {
+                const u64 mask = __ballot(nw[j]);
+                if (!mask) continue;
+                const u32 cnt = __popcll(mask);
+                const u32 below = __popcll(mask & ((1ull << lane) - 1));
+                const int leader = __builtin_ctzll(mask);
+                u32 sb = 0;
+                if (lane == leader) sb = atomicAdd(&stage_n, cnt);
+                sb = __shfl(sb, leader, 64);
+                const u32 in_stage = sb >= (u32)STAGE ? 0u : min(cnt, (u32)STAGE - sb);
+                u32 gb = 0;
+                if (cnt > in_stage && lane == leader) gb = atomicAdd(&lc->claims, cnt - in_stage);
+                gb = __shfl(gb, leader, 64);
+                if (!nw[j]) continue;
+                const u32 pr = wave0 + par[j];  // parent rank
+                if (below < in_stage) {
+                    const u32 kk = sb + below;
+#pragma unroll
+                    for (int x = 0; x < W; ++x) stage[kk * W + x] = ns[j][x];
+                    stage_par[kk] = pr;
+                } else {
+                    const u32 pos = gb + (below - in_stage);
+                    if (pos < next_cap) {
+                        store_state<W>(next, pos, ns[j]);
+                        next_par[pos] = pr;
+                        if (sw.naeb) sw.naeb[pos] = sw.peb[pr];
+                    } else {
+                        atomicOr(&lc->err, (u32)ERR_FRONTIER_OVERFLOW);
+                    }
+                    eval_props(m, ns[j], pos, undiscovered, lc);
+                }
+            }
         }
         wave_lds_sync();  // the window's map is read before the next window overwrites it
         }

@@ -18,12 +18,19 @@ pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
-def run_ranks(checks, world=2, distinct=False, env=None, timeout=240):
-    name = f"/sr_test_{os.getpid()}_{uuid.uuid4().hex[:8]}"
+def run_ranks(checks, world=2, distinct=False, env=None, timeout=240, name=None, stagger=None):
+    name = name or f"/sr_test_{os.getpid()}_{uuid.uuid4().hex[:8]}"
     e = dict(os.environ, **(env or {}))
-    procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "shm_rank_worker.py"), str(r), str(world), name,
-                               "1" if distinct else "0", *checks], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
-                              text=True, env=e) for r in range(world)]
+    procs = []
+    for r in (range(world) if stagger is None else reversed(range(world))):  # stagger: rank 0 last
+        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "shm_rank_worker.py"), str(r), str(world), name,
+                                       "1" if distinct else "0", *checks], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                                      text=True, env=e))
+        if stagger is not None:
+            import time
+            time.sleep(stagger)
+    if stagger is not None:
+        procs.reverse()
     outs = []
     for p in procs:
         try:
@@ -45,6 +52,27 @@ def expect(spec):
     else:
         o = OracleRun(TWO_PHASE if model == "2pc" else INCREMENT_LOCK, [int(n)])
     return o.unique_state_count, o.state_count, o.max_depth, o.discovery_names()
+
+
+def test_stale_segment_of_a_crashed_run():
+    # A crashed run left its segment under this name, full size and marked READY. Rank 1
+    # starts first and opens it; rank 0 starts later, replaces it with a fresh one, and the attach
+    # handshake brings rank 1 over to the live segment: the ranks meet and count right.
+    import struct
+    name = f"/sr_test_{os.getpid()}_{uuid.uuid4().hex[:8]}"
+    slot_bytes, world = 32 << 20, 2
+    path = "/dev/shm" + name
+    with open(path, "wb") as f:
+        f.truncate(4096 + slot_bytes * world)
+        f.seek(20)
+        f.write(struct.pack("<I", 0x53524844))  # READY
+    try:
+        outs = run_ranks(["2pc:5"], env={"SR_HEAD_MAX": "0"}, name=name, stagger=3.0)
+    finally:
+        if os.path.exists(path):
+            os.unlink(path)
+    for rank_out in outs:
+        assert [(r["unique"], r["states"], r["depth"], r["discoveries"]) for r in rank_out] == [expect("2pc:5")]
 
 
 @pytest.mark.parametrize("direct", ["1", "0"], ids=["direct", "collective"])

@@ -106,3 +106,22 @@ def test_partitioned_visitors_ranks():
     finally:
         for cm in comms:
             cm.close()
+
+
+@pytest.mark.parametrize("parts", [2, 3])
+def test_partitioned_target_stop_visits_popped_states_only(parts, monkeypatch):
+    # A target_state_count stop ends the partitioned search at a level boundary: the
+    # last level's states were generated, never popped, and the reference calls the visitor at a
+    # pop (src/checker/bfs.rs:188). So the StateRecorder sees every state of the levels before the
+    # last one, and none of the last level.
+    monkeypatch.setenv("SR_HEAD_MAX", "0")
+    n, target = 7, 20_000
+    o = OracleRun(TWO_PHASE, [n], record_visits=True)
+    depth = {s: len(a) for s, a in zip(o.visits(), o.visit_paths())}
+    rec = sr.StateRecorder()
+    c = sr.TwoPhaseSys(n).checker().partitions(parts).target_state_count(target).visitor(rec).spawn_bfs().join()
+    assert not c.is_done()
+    last = c.max_depth()
+    want = {s for s, d in depth.items() if d < last}
+    assert set(rec.states) == want
+    assert len(rec.states) == len(want)
