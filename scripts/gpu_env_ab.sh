@@ -15,7 +15,7 @@ for r in $(seq 1 "$REPS"); do
     for i in "${!ENVS[@]}"; do
         label="e${i}_r${r}"
         env ${ENVS[$i]} timeout -k 10 200 python -u bench.py --cpu-baseline 0 --config4-steps 0 --no-hint-steps 0 "$@" > "$O/$label.json" 2> "$O/$label.err" || { tail -5 "$O/$label.err"; exit 1; }
-        python3 -c "import json; d=json.loads(open('$O/$label.json').read().strip().splitlines()[-1]); l=d.get('levels',{}); e=d.get('engine',{}); print('[${ENVS[$i]}] r$r', round(d['ms_per_step'],4), 'big', round(l.get('big_levels_ms',0),4), 'small', round(l.get('small_levels_ms',0),4), 'gaps', round(l.get('gaps_ms',0),4), 'cap', e.get('table_capacity'))"
+        python3 -c "import json; d=json.loads(open('$O/$label.json').read().strip().splitlines()[-1]); l=d.get('levels') or {}; e=d.get('engine') or {}; print('[${ENVS[$i]}] r$r', round(d['ms_per_step'],4), 'big', round(l.get('big_levels_ms',0),4), 'small', round(l.get('small_levels_ms',0),4), 'gaps', round(l.get('gaps_ms',0),4), 'cap', e.get('table_capacity'))"
     done
 done
 echo "env ab ok"
