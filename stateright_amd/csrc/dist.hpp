@@ -1518,7 +1518,7 @@ class DistEngine final : public EngineBase {
                 const u32 ppw_log2 = route_ppw_env_ >= 0 ? (u32)route_ppw_env_ : ppw_for(p.n_est);
                 const u32 grid = (u32)std::min<u64>(std::max<u64>(1, blocks_for(p.n_hi, 4u << ppw_log2)), route_grid_cap());
                 u64* row = comm_ ? rows_mine_.p : rows_all_.p + (u64)p.id * RW;
-                auto route = self_rec() ? expand_route<M, 1, true> : expand_route<M, 1, false>;
+                auto route = route_kernel(p);
                 route<<<grid, 256, route_lds(), stream_>>>(
                     m_, p.arena.p, p.apar.p, nb, p.arena_cap, p.view(), p.id, T_, p.send.p, (u32)p.bucket_cap,
                     p.sendc.p, p.lc, p.ctl, undiscovered, row, ppw_log2, filt_log2_, p.bucket_cap * REC, 0u,
@@ -1838,7 +1838,7 @@ class DistEngine final : public EngineBase {
             const u32 ppw_log2 = route_ppw_env_ >= 0 ? (u32)route_ppw_env_ : ppw_for(n_plan[p.id]);
             const u32 grid = (u32)std::min<u64>(std::max<u64>(1, blocks_for(n_plan[p.id], 4u << ppw_log2)), route_grid_cap());
             u64* row = comm_ ? rows_mine_.p : rows_all_.p + (u64)p.id * RW;
-            auto route = self_rec() ? expand_route<M, 1, true> : expand_route<M, 1, false>;
+            auto route = route_kernel(p);
             route<<<grid, 256, route_lds(), stream_>>>(
                 m_, p.arena.p, p.apar.p, 0, p.arena_cap, p.view(), p.id, T_, direct_ ? nullptr : p.send.p + DIST_HDR,
                 (u32)C, p.sendc.p, p.lc, p.ctl, undiscovered, row, ppw_log2, filt_log2_, S, 1u,
@@ -2445,6 +2445,20 @@ class DistEngine final : public EngineBase {
     // (SR_SELF_RECORDS_MIN; 0 = never): its rounds then wait on no visited-set probe
     // (not with an owner key: most successors are then local, and probing them in place is cheaper)
     u32 self_rec() const { return !okey_ && self_rec_min_ && T_ >= self_rec_min_ ? 1u : 0u; }
+    // The route kernel's form: self records (no probes), or probes of the local successors in
+    // rounds, or in per-lane queues (expand_fast's probe_loop rule: fingerprint-mode narrow states,
+    // a partition table of >= 2^27 slots, and here no sent cache). SR_ROUTE_QUEUE=0/1 forces it.
+    using RouteKernel = decltype(&expand_route<M, 1, false>);
+    RouteKernel route_kernel(const Part& p) const {
+        if (self_rec()) return expand_route<M, 1, true>;
+        constexpr bool fp_only = !(has_qkey<M>::value && M::W >= 2);
+        if constexpr (fp_only && W < 4) {
+            const bool big = p.view().mask + 1 >= (1ull << 27);
+            if (!p.sent_mask && (route_queue_env_ < 0 ? big : route_queue_env_ > 0)) return expand_route<M, -4, false>;
+        }
+        return expand_route<M, 1, false>;
+    }
+    int route_queue_env_ = std::getenv("SR_ROUTE_QUEUE") ? std::atoi(std::getenv("SR_ROUTE_QUEUE")) : -1;
     u32 rflags() const {
         const u32 ls = lstage_words_ ? lstage_words_ / W : 0u;  // SR_LSTAGE_WORDS: the local stage's size
         return self_rec() | (okey_ ? (u32)RF_LOCAL : 0u) | ls << RF_LSTAGE_SHIFT;

@@ -345,6 +345,184 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W <
         }
         wave_lds_sync();  // pst and the map are the wave's own
 
+        if constexpr (PB < 0) {
+            // Per-lane probe queues (expand_fast's, kernels.hpp; the host takes this form for big
+            // fingerprint-mode tables without a sent cache): R rounds expanded with every lane
+            // busy, remote successors staged as records at once, the local ones' keys kept in
+            // registers and probed one visited-set access per lane and iteration.
+            static_assert(!SELF, "self records probe nothing");
+            constexpr int R = -PB;
+            constexpr bool FP_ONLY = !(has_qkey<M>::value && M::W >= 2);
+            for (u32 s0 = w0; s0 < wend; s0 += 64u * R) {
+                u64 kh[FP_ONLY ? 1 : R], kt[R];
+                u32 vmask = 0;
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    if (!FP_ONLY) kh[FP_ONLY ? 0 : r] = 0;
+                    kt[r] = 0;
+                    const u32 i = s0 + (u32)r * 64u + (u32)lane;
+                    u64 q[W];
+                    bool ok = false, rem = false;
+                    u32 own = my_part;
+                    if (i < wend) {
+                        const u32 e = smap[wid][i - w0];
+                        const u32 p = e & 63, a = e >> 6;
+                        u64 ps[W];
+#pragma unroll
+                        for (int x = 0; x < W; ++x) ps[x] = pst[wid][p * W + x];
+                        ok = m.apply(ps, (int)a, q);
+                        if (ok) {
+                            ++succ;
+                            ok = !same_state<W>(q, ps);  // self-loop: counted, never routed
+                        }
+                        if (ok) {
+                            const ProbeKey pk = probe_key(m, t, q);
+                            const u64 key = t.qbits ? state_fp<M>(q) : pk.tag;
+                            if (fmask) {  // block-local duplicate filter (see expand_fast)
+                                const u64 old = atomicExch(reinterpret_cast<unsigned long long*>(&filt[(u32)(key >> 40) & fmask]),
+                                                           (unsigned long long)key);
+                                ok = old != key;
+                            }
+                            if (ok) {
+                                own = part_of(m, q, key, nparts);
+                                rem = self_rec || own != my_part;
+                                if (!rem) {
+                                    vmask |= 1u << r;
+                                    kt[r] = pk.tag;
+                                    if (!FP_ONLY) kh[FP_ONLY ? 0 : r] = pk.home;
+                                }
+                            }
+                        }
+                    }
+                    // remote records -> the chunk's record stage (one LDS atomic per wave)
+                    const u64 rmask = __ballot(rem);
+                    if (!rmask) continue;
+                    const u32 rcnt = __popcll(rmask);
+                    const u32 rbelow = __popcll(rmask & lanes_below);
+                    const int rleader = __builtin_ctzll(rmask);
+                    u32 rsb = 0;
+                    if (lane == rleader) rsb = atomicAdd(&rstage_n, rcnt);
+                    rsb = __shfl(rsb, rleader, 64);
+                    const u32 rin = rsb >= RSTAGE ? 0u : min(rcnt, RSTAGE - rsb);
+                    if (rem && rbelow < rin) {
+                        const u32 kk = rsb + rbelow;
+#pragma unroll
+                        for (int x = 0; x < W; ++x) rstage[kk * REC + x] = q[x];
+                        rown[kk] = (u8)own;
+                    }
+                    u64 om = __ballot(rem && rbelow >= rin);  // overflow (rare): per-wave reservations
+                    if (om && lane == 0) sent_any = 1;
+                    while (om) {
+                        const int leader = __builtin_ctzll(om);
+                        const u32 qo = __shfl(own, leader, 64);
+                        const bool mine = rem && rbelow >= rin && own == qo;
+                        const u64 qm = __ballot(mine);
+                        om &= ~qm;
+                        u32 gb = 0;
+                        if (lane == leader) gb = atomicAdd(&send_counts[qo * SENDC_STRIDE], (u32)__popcll(qm));
+                        gb = __shfl(gb, leader, 64);
+                        if (mine) {
+                            const u32 pos = gb + __popcll(qm & lanes_below);
+                            if (pos < bucket_cap) {
+                                u64* rec = sdst[qo] + (u64)pos * REC;
+                                u64 v = 0;
+#pragma unroll
+                                for (int x = 0; x < W; ++x) rec[x] = q[x], v += q[x];
+                                if (my_dsum) atomicAdd(reinterpret_cast<unsigned long long*>(&my_dsum[qo]), (unsigned long long)v);
+                            } else {
+                                atomicOr(&lc->err, (u32)ERR_FRONTIER_OVERFLOW);
+                            }
+                        }
+                    }
+                }
+                // the local successors' probes, one access per lane and iteration
+                u32 nmask = 0, st = 0, cr = 0, disp = 0;
+                u64 si = 0, tag = 0;
+                const u64 step = probe_step(t);
+                for (;;) {
+                    if (st == 0 && vmask) {
+                        cr = (u32)__builtin_ctz(vmask);
+                        vmask &= vmask - 1;
+                        tag = kt[0];
+#pragma unroll
+                        for (int r = 1; r < R; ++r)
+                            if (cr == (u32)r) tag = kt[r];
+                        if constexpr (FP_ONLY) {
+                            si = tag & t.mask;
+                        } else {
+                            si = kh[0];
+#pragma unroll
+                            for (int r = 1; r < R; ++r)
+                                if (cr == (u32)r) si = kh[FP_ONLY ? 0 : r];
+                        }
+                        st = 1;
+                        disp = 0;
+                    }
+                    if (!__ballot(st != 0)) break;
+                    u64 v = 0;
+                    if (st == 1) v = probe_load<0>(&t.keys[si]);
+                    if (st == 2) v = atomicCAS(reinterpret_cast<unsigned long long*>(&t.keys[si]), 0ull, (unsigned long long)tag);
+                    if (st != 0) {
+                        if (v == tag) {
+                            st = 0;
+                        } else if (v == 0) {
+                            if (st == 2) nmask |= 1u << cr;
+                            st = st == 1 ? 2u : 0u;
+                        } else if (++disp >= t.plimit) {
+                            atomicOr(&lc->err, (u32)ERR_TABLE_FULL);
+                            st = 0;
+                        } else {
+                            si = (si + 1) & t.mask;
+                            tag += step;
+                            st = 1;
+                        }
+                    }
+                }
+                // local new states -> the chunk's stage (their states recomputed from the map)
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const bool nw = nmask >> r & 1;
+                    const u64 mask = __ballot(nw);
+                    if (!mask) continue;
+                    u64 q[W];
+                    u32 p = 0;
+                    if (nw) {
+                        const u32 e = smap[wid][s0 + (u32)r * 64u + (u32)lane - w0];
+                        p = e & 63;
+                        u64 ps[W];
+#pragma unroll
+                        for (int x = 0; x < W; ++x) ps[x] = pst[wid][p * W + x];
+                        m.apply(ps, (int)(e >> 6), q);
+                    }
+                    const u32 cnt = __popcll(mask);
+                    const u32 below = __popcll(mask & lanes_below);
+                    const int leader = __builtin_ctzll(mask);
+                    u32 sb = 0;
+                    if (lane == leader) sb = atomicAdd(&stage_n, cnt);
+                    sb = __shfl(sb, leader, 64);
+                    const u32 in_stage = sb >= (u32)STAGE ? 0u : min(cnt, (u32)STAGE - sb);
+                    u32 gb = 0;
+                    if (cnt > in_stage && lane == leader) gb = atomicAdd(&lc->claims, cnt - in_stage);
+                    gb = __shfl(gb, leader, 64);
+                    if (!nw) continue;
+                    if (below < in_stage) {
+                        const u32 kk = sb + below;
+#pragma unroll
+                        for (int x = 0; x < W; ++x) stage[kk * W + x] = q[x];
+                        stage_par[kk] = (u32)(wave0 + p);
+                    } else {
+                        const u32 pos = gb + (below - in_stage);
+                        if (pos < next_cap) {
+                            store_state<W>(next, pos, q);
+                            next_par[pos] = gid_base + wave0 + p;
+                        } else {
+                            atomicOr(&lc->err, (u32)ERR_FRONTIER_OVERFLOW);
+                        }
+                        eval_props(m, q, pos, undiscovered, lc);
+                    }
+                }
+            }
+        } else
         for (u32 it = w0; it < wend; it += 64 * PB) {
             u64 ns[PB][W], key[PB], cur[PB];
             ProbeKey pk[PB];
