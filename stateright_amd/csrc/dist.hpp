@@ -1874,8 +1874,10 @@ class DistEngine final : public EngineBase {
         for (auto& p : parts_) {
             p.seq++;
             auto& r = ctx_->parts[p.res];
-            // four records per thread on the large grid (insert_grid), one otherwise
-            auto kern = ig > INSERT_GRID_MAX && W <= 2 ? insert_recv_lag<M, 4> : insert_recv_lag<M, 1>;
+            // four records per thread on the large grid (insert_grid), one otherwise; the four as
+            // parallel probe state machines (-4) unless SR_INSERT_MACHINES=0
+            auto kern = ig > INSERT_GRID_MAX && W <= 2 ? (insert_machines_ ? insert_recv_lag<M, -4> : insert_recv_lag<M, 4>)
+                                                         : insert_recv_lag<M, 1>;
             kern<<<ig, 256, 0, stream_>>>(m_, direct_ ? r.drecv[par].p : p.recv.p, S, (u32)C, p.id, T_, p.view(),
                                           p.arena.p, p.apar.p, p.arena_cap, p.lc, undiscovered, p.ctl,
                                           r.pub_dev[p.seq & 1], p.seq, dflags_ && fused_wait_ ? ctx_->dx.flags.p : nullptr,
@@ -2458,6 +2460,7 @@ class DistEngine final : public EngineBase {
         }
         return expand_route<M, 1, false>;
     }
+    bool insert_machines_ = !(std::getenv("SR_INSERT_MACHINES") && std::atoi(std::getenv("SR_INSERT_MACHINES")) == 0);
     int route_queue_env_ = std::getenv("SR_ROUTE_QUEUE") ? std::atoi(std::getenv("SR_ROUTE_QUEUE")) : -1;
     u32 rflags() const {
         const u32 ls = lstage_words_ ? lstage_words_ / W : 0u;  // SR_LSTAGE_WORDS: the local stage's size

@@ -784,14 +784,112 @@ __device__ __forceinline__ void insert_records(const M& m, RecAt rec_at, u32 tot
     // is resolved (one round of barriers per IPB x blockDim records). The host takes 4 for large
     // inserts; small ones, latency-bound, keep one (a separate instantiation: the batched form's
     // registers would lower the occupancy of the small ones).
-    const u64 per_round = (u64)gridDim.x * blockDim.x * IPB;
-    for (u64 g0 = (u64)blockIdx.x * blockDim.x * IPB; g0 < total; g0 += per_round) {
-        __syncthreads();  // every thread read the last fill (and the stage was reset) before appends
-        u64 ns[IPB][W], cur[IPB];
-        ProbeKey pk[IPB];
-        bool ok[IPB];
+    // IPB < 0: R = -IPB records per thread and round, each with a probe state machine of its own
+    // (home load, linear-probe step or claim CAS); every iteration issues the next access of EVERY
+    // unresolved record together, so a round costs its longest chain, not the sum of its records'
+    // chains (IPB > 1 resolves them one after the other).
+    if constexpr (IPB < 0) {
+        constexpr int R = -IPB;
+        const u64 per_round = (u64)gridDim.x * blockDim.x * R;
+        const u64 step = probe_step(t);
+        for (u64 g0 = (u64)blockIdx.x * blockDim.x * R; g0 < total; g0 += per_round) {
+            __syncthreads();  // every thread read the last fill (and the stage was reset) before appends
+            u64 ns[R][W], si[R], tag[R];
+            u32 st[R], disp[R];
+            bool nws[R];
 #pragma unroll
-        for (int j = 0; j < IPB; ++j) {
+            for (int j = 0; j < R; ++j) {
+                const u64 g = g0 + (u64)j * blockDim.x + threadIdx.x;
+                st[j] = g < total ? 1u : 0u;
+                disp[j] = 0;
+                nws[j] = false;
+                si[j] = tag[j] = 0;
+                if (st[j]) {
+                    const u64* rec = rec_at((u32)g);
+#pragma unroll
+                    for (int x = 0; x < W; ++x) ns[j][x] = rec[x], rsum += rec[x];
+                    const ProbeKey pk = probe_key(m, t, ns[j]);
+                    si[j] = pk.home;
+                    tag[j] = pk.tag;
+                }
+            }
+            for (;;) {
+                u32 live = 0;
+#pragma unroll
+                for (int j = 0; j < R; ++j) live |= st[j];
+                if (!__ballot(live != 0)) break;
+                u64 v[R];
+#pragma unroll
+                for (int j = 0; j < R; ++j) {
+                    v[j] = 0;
+                    if (st[j] == 1) v[j] = t.keys[si[j]];
+                    if (st[j] == 2) v[j] = atomicCAS(reinterpret_cast<unsigned long long*>(&t.keys[si[j]]), 0ull, (unsigned long long)tag[j]);
+                }
+#pragma unroll
+                for (int j = 0; j < R; ++j) {
+                    if (!st[j]) continue;
+                    if (v[j] == tag[j]) {
+                        st[j] = 0;
+                    } else if (v[j] == 0) {
+                        nws[j] = st[j] == 2;
+                        st[j] = st[j] == 1 ? 2u : 0u;
+                    } else if (++disp[j] >= t.plimit) {
+                        atomicOr(&lc->err, (u32)ERR_TABLE_FULL);
+                        st[j] = 0;
+                    } else {
+                        si[j] = (si[j] + 1) & t.mask;
+                        tag[j] += step;
+                        st[j] = 1;
+                    }
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < R; ++j) {
+                const bool nw = nws[j];
+                const u64 mask = __ballot(nw);
+                if (!mask) continue;
+                const u32 cnt = __popcll(mask), below = __popcll(mask & ((1ull << lane) - 1));
+                const int leader = __builtin_ctzll(mask);
+                u32 sb = 0;
+                if (lane == leader) sb = atomicAdd(&stage_n, cnt);
+                sb = __shfl(sb, leader, 64);
+                const u32 in_stage = sb >= STAGE ? 0u : min(cnt, STAGE - sb);
+                u32 gb = 0;
+                if (cnt > in_stage && lane == leader) gb = atomicAdd(&lc->claims, cnt - in_stage);
+                gb = __shfl(gb, leader, 64);
+                if (!nw) continue;
+                if (below < in_stage) {
+#pragma unroll
+                    for (int x = 0; x < W; ++x) stage[(sb + below) * W + x] = ns[j][x];
+                } else {
+                    const u32 pos = gb + (below - in_stage);
+                    if (pos < next_cap) {
+                        store_state<W>(next, pos, ns[j]);
+                        next_par[pos] = PAR_SEARCH;
+                    } else {
+                        atomicOr(&lc->err, (u32)ERR_FRONTIER_OVERFLOW);
+                    }
+                    eval_props(m, ns[j], pos, undiscovered, lc);
+                }
+            }
+            __syncthreads();
+            const u32 sn = min(stage_n, STAGE);
+            if (sn >= STAGE / 2) flush(sn);
+        }
+        __syncthreads();
+        const u32 sn = min(stage_n, STAGE);
+        if (sn) flush(sn);
+        return;
+    }
+    constexpr int PBI = IPB < 1 ? 1 : IPB;  // (the batched-round form below)
+    const u64 per_round = (u64)gridDim.x * blockDim.x * PBI;
+    for (u64 g0 = (u64)blockIdx.x * blockDim.x * PBI; g0 < total; g0 += per_round) {
+        __syncthreads();  // every thread read the last fill (and the stage was reset) before appends
+        u64 ns[PBI][W], cur[PBI];
+        ProbeKey pk[PBI];
+        bool ok[PBI];
+#pragma unroll
+        for (int j = 0; j < PBI; ++j) {
             const u64 g = g0 + (u64)j * blockDim.x + threadIdx.x;
             ok[j] = g < total;
             pk[j] = ProbeKey{0, 0};
@@ -803,15 +901,15 @@ __device__ __forceinline__ void insert_records(const M& m, RecAt rec_at, u32 tot
             }
         }
 #pragma unroll
-        for (int j = 0; j < IPB; ++j) cur[j] = ok[j] ? t.keys[pk[j].home] : 0;
-        bool nws[IPB];  // every claim of the round before any append (their CASes overlap)
+        for (int j = 0; j < PBI; ++j) cur[j] = ok[j] ? t.keys[pk[j].home] : 0;
+        bool nws[PBI];  // every claim of the round before any append (their CASes overlap)
 #pragma unroll
-        for (int j = 0; j < IPB; ++j) {
+        for (int j = 0; j < PBI; ++j) {
             nws[j] = false;
             if (ok[j] && cur[j] != pk[j].tag) find_or_claim_from(t, pk[j], cur[j], &nws[j], &lc->err);
         }
 #pragma unroll
-        for (int j = 0; j < IPB; ++j) {
+        for (int j = 0; j < PBI; ++j) {
             const bool nw = nws[j];
             const u64 mask = __ballot(nw);
             if (!mask) continue;  // wave-aggregated: one LDS atomic, the overflow with one claims atomic per wave

@@ -73,6 +73,8 @@ def test_paxos_counts_fixture_agrees():
     by = {r["client_count"]: r for r in PAXOS_COUNTS}
     assert sorted(by) == [1, 2, 3, 4, 5, 6]
     assert by[2]["unique_state_count"] == 16668
+    # only the C=2 row is pinned by the reference; the others say they are oracle-derived
+    assert by[2]["pinning"].startswith("pinned") and all(by[c]["pinning"].startswith("oracle-derived") for c in by if c != 2)
     for c in (1, 2):
         t = _by("paxos", [c])
         assert (by[c]["unique_state_count"], by[c]["state_count"], by[c]["max_depth"]) == \
