@@ -1320,12 +1320,9 @@ class Engine final : public EngineBase {
         const u32 lmax = W >= 4 ? SR_WIDE_PPW_LOG2_MAX : 6;  // expand_fast's PPW_LOG2_MAX
         u32 l = 2;
         while (l < lmax && (double)(2u << l) <= ppw) ++l;
-        // down to one parent per wave (lane = action slot, no successor map) for one-word masks
-        const u32 lmin = M::MW == 1 && W < 4 ? ppw_min_ : 2u;
-        while (l > lmin && ((c + (1u << l) - 1) >> l) < ppw_waves_) --l;
+        while (l > 2 && ((c + (1u << l) - 1) >> l) < ppw_waves_) --l;
         return l;
     }
-    u32 ppw_min_ = std::getenv("SR_PPW_MIN_LOG2") ? (u32)std::atoi(std::getenv("SR_PPW_MIN_LOG2")) : 2u;
     u64 ppw_waves_ = std::getenv("SR_PPW_WAVES") && std::atoll(std::getenv("SR_PPW_WAVES")) > 0
                          ? (u64)std::atoll(std::getenv("SR_PPW_WAVES")) : 1024;
 

@@ -905,14 +905,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W >
                 eval_props(m, ns, pos, undiscovered, lc);
             }
         };
-        // One parent per wave (the smallest levels, ppw_for): lane a takes action slot a of the
-        // wave's parent straight from its enabled mask, with no successor map.
-        const bool direct1 = PB == 1 && MW == 1 && ppw == 1;
-        const u64 mk0 = direct1 ? __shfl(mk[0], 0, 64) : 0ull;
         for (u32 w0 = 0; w0 < total; w0 += MAPCAP) {
-        const u32 wend = direct1 ? 64u : min(total, w0 + MAPCAP);
-        if (direct1) {
-        } else if (MW <= 2 && ppw <= 8) {
+        const u32 wend = min(total, w0 + MAPCAP);
+        if (MW <= 2 && ppw <= 8) {
             // Few parents per wave (small levels): the 64 lanes fill the map together, entry j
             // from parent p (the last whose exclusive offset is <= j) and its (j - offset)-th
             // enabled slot, instead of every parent lane writing its own successors one by one
@@ -1076,10 +1071,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W >
 #pragma unroll
             for (int j = 0; j < PB; ++j) {
                 const u32 i = it + j * 64 + lane;
-                ok[j] = direct1 ? (mk0 >> lane & 1) != 0 : i < wend;
+                ok[j] = i < wend;
                 par[j] = 0;
                 if (ok[j]) {
-                    const u32 e = direct1 ? (u32)lane << 6 : smap[wid][i - w0];
+                    const u32 e = smap[wid][i - w0];
                     const u32 p = e & 63, a = e >> 6;
                     u64 ps[W];
 #pragma unroll
