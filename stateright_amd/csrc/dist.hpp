@@ -2464,14 +2464,22 @@ class DistEngine final : public EngineBase {
     int route_queue_env_ = std::getenv("SR_ROUTE_QUEUE") ? std::atoi(std::getenv("SR_ROUTE_QUEUE")) : -1;
     u32 rflags() const {
         const u32 ls = lstage_words_ ? lstage_words_ / W : 0u;  // SR_LSTAGE_WORDS: the local stage's size
-        return self_rec() | (okey_ ? (u32)RF_LOCAL : 0u) | ls << RF_LSTAGE_SHIFT;
+        return self_rec() | (okey_ ? (u32)RF_LOCAL : 0u) | (ordered_flush() ? (u32)RF_ORDERED : 0u) | ls << RF_LSTAGE_SHIFT;
     }
+    // The owner-ordered record flush when the owners are other devices (RF_ORDERED; SR_ORDERED_FLUSH
+    // = 0 / 1 forces it off / on, e.g. to test it on one device).
+    bool ordered_flush() const {
+        if (ordered_env_ >= 0) return ordered_env_ > 0;
+        return comm_ && comm_->world > 1 && comm_->distinct_devices();
+    }
+    int ordered_env_ = std::getenv("SR_ORDERED_FLUSH") ? std::atoi(std::getenv("SR_ORDERED_FLUSH")) : -1;
     u32 lstage_words_ = std::getenv("SR_LSTAGE_WORDS") ? (u32)std::atoi(std::getenv("SR_LSTAGE_WORDS")) : 0u;
     const bool okey_ = uses_owner_key(m_);  // states owned by the model's owner key (kernels_dist.hpp part_of)
     u32 self_rec_min_ = std::getenv("SR_SELF_RECORDS_MIN") ? (u32)std::atoi(std::getenv("SR_SELF_RECORDS_MIN")) : 5u;
     size_t route_lds() const {
-        return (filt_log2_ ? (8u << filt_log2_) : 0u) + (size_t)rstage_recs() * (REC * 8 + 2 + 1) +
-               (size_t)route_local_stage(T_, W, rflags()) * (W * 8 + 4);
+        const size_t rs = rstage_recs();
+        return (filt_log2_ ? (8u << filt_log2_) : 0u) + rs * (REC * 8 + 2) + ((rs + 1) & ~(size_t)1) +
+               (ordered_flush() ? rs * 2 : 0) + (size_t)route_local_stage(T_, W, rflags()) * (W * 8 + 4);
     }
     // expand_route's grid: two device residencies at its LDS footprint (expand_fast's rule); the
     // kernel strides over further parents. SR_ROUTE_GRID_MAX > 0 overrides it.

@@ -143,7 +143,10 @@ template <int = 0> __global__ void peer_wait(const u32* flags, u32 nparts, u32 s
 // states are local: the stage of one partition.
 // rflags: RF_SELF (self records), RF_LOCAL (owner key: most successors stay local), and from bit 8
 // on the local stage's size in states when the host sets one (RF_LSTAGE_SHIFT; 0 = this default).
-enum RouteFlags : u32 { RF_SELF = 1, RF_LOCAL = 2, RF_LSTAGE_SHIFT = 8 };
+// RF_ORDERED: the record flush writes each owner's records as one contiguous run from consecutive
+// threads (owner-ordered): taken when the owners are other devices (stores over
+// xGMI into fine-grained peer memory); same-device owners keep the stage-order flush.
+enum RouteFlags : u32 { RF_SELF = 1, RF_LOCAL = 2, RF_ORDERED = 4, RF_LSTAGE_SHIFT = 8 };
 __host__ __device__ __forceinline__ u32 route_local_stage(u32 nparts, int W, u32 rflags) {
     if (rflags & RF_SELF) return 0u;
     if (rflags >> RF_LSTAGE_SHIFT) return rflags >> RF_LSTAGE_SHIFT;
@@ -198,7 +201,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W <
     for (u32 q = threadIdx.x; q < nparts; q += blockDim.x)
         sdst[q] = ptab ? ptab[q] + (u64)my_part * bucket_stride : send + (u64)q * bucket_stride;
     // Dynamic LDS: [filter: 2^filt_log2 fingerprints][record stage: rs x REC words][local stage:
-    // ls x W words][its parents' frontier ranks: ls u32][record ranks: rs u16][record owners: rs u8].
+    // ls x W words][its parents' frontier ranks: ls u32][record ranks: rs u16][record owners: rs u8]
+    // and, with RF_ORDERED, [the records in owner order: rs u16].
     // rs (records staged per chunk, all owners) is chosen on the host: 0 with one partition, so the
     // one-partition launch keeps expand_fast's occupancy; ls = route_local_stage(nparts).
     extern __shared__ u64 dyn[];
@@ -209,7 +213,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W <
     u32* stage_par = reinterpret_cast<u32*>(stage + (u64)STAGE * W);  // the gid is formed at flush
     u16* rrank = reinterpret_cast<u16*>(stage_par + STAGE);
     u8* rown = reinterpret_cast<u8*>(rrank + rs);
-    __shared__ u32 ocnt[MAX_PARTS], obase[MAX_PARTS];
+    u16* rperm = reinterpret_cast<u16*>(rown + ((rs + 1) & ~1u));  // RF_ORDERED only
+    const bool ordered = (rflags & RF_ORDERED) != 0;
+    __shared__ u32 ocnt[MAX_PARTS], obase[MAX_PARTS], lbase[MAX_PARTS + 1];
     __shared__ u64 ocsum[MAX_PARTS];  // the chunk's record-word sum per owner (dsum)
     __shared__ u64 pst[4][64 * W];
     // the wave's successor list, (parent, action) per successor (see expand_fast), in windows
@@ -255,6 +261,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W <
             if (fl) stage_n = 0;
             if (fr) rstage_n = 0;
         }
+        if (nr && ordered && threadIdx.x < 64) {  // the owners' runs in the chunk: exclusive prefix
+            const u32 c = threadIdx.x < nparts ? ocnt[threadIdx.x] : 0u;
+            u32 incl = c;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const u32 y = __shfl_up(incl, d, 64);
+                if ((int)threadIdx.x >= d) incl += y;
+            }
+            if (threadIdx.x < nparts) lbase[threadIdx.x] = incl - c;
+        }
         if (nr)
             for (u32 q = threadIdx.x; q < nparts; q += blockDim.x) {
                 const u32 c = ocnt[q];
@@ -265,6 +281,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W <
                     ocsum[q] = 0;
                 }
             }
+        if (nr && ordered) {
+            __syncthreads();  // lbase
+            for (u32 i = threadIdx.x; i < nr; i += blockDim.x) rperm[lbase[rown[i]] + rrank[i]] = (u16)i;
+        }
         for (u32 i = threadIdx.x; i < nl; i += blockDim.x) {
             const u32 pos = base + i;
             u64 ns[W];
@@ -280,7 +300,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W <
         }
         __syncthreads();
         for (u32 i = threadIdx.x; i < nr * REC; i += blockDim.x) {
-            const u32 rr = i / REC, x = i - rr * REC;
+            // ordered: thread i takes word x of the k-th record in owner order, so consecutive
+            // threads store consecutive words of one owner's run; else the k-th staged record
+            const u32 k = i / REC, x = i - k * REC;
+            const u32 rr = ordered ? rperm[k] : k;
             const u32 q = rown[rr];
             const u32 pos = obase[q] + rrank[rr];
             if (pos < bucket_cap) sdst[q][(u64)pos * REC + x] = rstage[rr * REC + x];
