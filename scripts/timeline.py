@@ -74,6 +74,7 @@ def main():
     print("level  frontier  grid  span_us  gap_us  entry_skew  exit_skew | median link us: " + " ".join(f"{x:>7}" for x in LINKS))
     prev_end = None
     total = 0.0
+    tails = []
     for i, bl in enumerate(launches):
         start = min(t[0] for t in bl)
         end = max(t[9] for t in bl)
@@ -95,9 +96,28 @@ def main():
             sub.append(statistics.median(d) if d else float("nan"))
         entry_skew = (statistics.median([t[0] for t in bl]) - start) * TICK_US
         exit_skew = (end - statistics.median([t[9] for t in bl if t[9]])) * TICK_US
+        # the reservation link (one device atomic on the level's single claims line) across workgroups:
+        # p90 and max, and when the chunks of the workgroups ended (p10 / p90 after the launch start)
+        res = sorted((t[7] - t[6]) * TICK_US for t in work if t[7] and t[6])
+        ends = sorted((t[6] - start) * TICK_US for t in work if t[6])
+        q = lambda v, f: v[min(len(v) - 1, int(f * len(v)))] if v else float("nan")
+        tails.append(f"{i:5d} reserve p90 {q(res, 0.9):6.2f} max {q(res, 1.0):6.2f} | chunks end p10 {q(ends, 0.1):6.1f} "
+                     f"p50 {q(ends, 0.5):6.1f} p90 {q(ends, 0.9):6.1f} max {q(ends, 1.0):6.1f} us")
+        # by workgroup index (the array index is blockIdx.x): quarters of the grid, entry and chunk end
+        nb = len(bl)
+        for qi in range(4):
+            part = [t for b, t in enumerate(bl) if t[1] and qi * nb // 4 <= b < (qi + 1) * nb // 4]
+            if not part:
+                continue
+            st = sorted((t[0] - start) * TICK_US for t in part)
+            en = sorted((t[6] - start) * TICK_US for t in part if t[6])
+            ch = sorted((t[6] - t[5]) * TICK_US for t in part if t[6] and t[5])
+            tails.append(f"        q{qi}: entry p50 {q(st, 0.5):6.1f} max {q(st, 1.0):6.1f} | chunk end p50 {q(en, 0.5):6.1f} "
+                         f"max {q(en, 1.0):6.1f} | chunks link p50 {q(ch, 0.5):6.1f} p90 {q(ch, 0.9):6.1f}")
         print(f"{i:5d} {fr:9d} {grid:5d} {span:8.1f} {gap:7.1f} {entry_skew:11.1f} {exit_skew:10.1f} | " +
               "                 " + " ".join(f"{x:7.2f}" for x in med) + "  | map: " + " ".join(f"{x:5.2f}" for x in sub))
     print(f"# sum of spans {total:.1f} us over {len(launches)} launches")
+    print("\n".join(tails))
 
 
 if __name__ == "__main__":

@@ -1312,7 +1312,7 @@ class Engine final : public EngineBase {
     // enabled action slots of its parents 64 at a time. Light models (a few ALU ops per successor)
     // amortise the wave's setup over ~16 such rounds; heavy ones (paxos: ~1.3K VALU ops per
     // successor) want ~4 rounds per wave and more waves to hide the probe latency. Small levels
-    // use fewer parents per wave until ~1K waves are in flight (minimum 4 parents per wave).
+    // use fewer parents per wave until ~2K waves are in flight (minimum 4 parents per wave).
     // Measured per level with SR_PPW_LOG2 sweeps (profiles/r01_ppw_levels.txt).
     u32 ppw_for(u64 c) const {
         const double rounds = W >= 4 ? 4.0 : 16.0;
@@ -1324,7 +1324,7 @@ class Engine final : public EngineBase {
         return l;
     }
     u64 ppw_waves_ = std::getenv("SR_PPW_WAVES") && std::atoll(std::getenv("SR_PPW_WAVES")) > 0
-                         ? (u64)std::atoll(std::getenv("SR_PPW_WAVES")) : 1024;
+                         ? (u64)std::atoll(std::getenv("SR_PPW_WAVES")) : 2048;
 
     // The frontier being expanded: the arena's second-to-last level.
     const u64* cur() const { return arena_.p + lstart_[lstart_.size() - 2] * W; }

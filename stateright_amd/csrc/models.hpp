@@ -310,15 +310,24 @@ struct BinaryClock {
 // 2+5rm+{0 TmRcvPrepared, 1 RmPrepare, 2 RmChooseToAbort, 3 RmRcvCommitMsg, 4 RmRcvAbortMsg}.
 // Every action returns Some (examples/2pc.rs:83-104), self-loops included.
 // -----------------------------------------------------------------------------------------------
-struct TwoPhase {
+// NC > 0: the rm count as a compile-time constant (the engine's specialization of the bench
+// configurations, reg_two_phase.hip); the device functions read it through N(), so their per-rm
+// loops unroll with constant shifts. NC = 0 reads the runtime n.
+template <int NC = 0>
+struct TwoPhaseT {
     static constexpr int W = 1, MW = 2, NPROPS = 3;
     int n;
+    SR_HD int N() const {
+        if constexpr (NC > 0) return NC;
+        else return n;
+    }
     // Owner key of the partitioned search: the per-RM tuples (rm_state, tm_prepared,
     // Prepared{rm} in msgs) of the first okey_rms resource managers (0: no key, own by
     // fingerprint). Only the five actions of those RMs change it; TmCommit/TmAbort and the other
     // RMs' actions keep a successor in its parent's partition.
     int okey_rms = 0;
     SR_HD bool owner_key(const u64* sp, u64* key) const {
+        const int n = N();
         const int k = okey_rms;
         const u64 s = sp[0], m = (1ull << k) - 1;
         *key = (s & ((1ull << (2 * k)) - 1)) | ((s >> (2 * n + 2)) & m) << (2 * k) | ((s >> (3 * n + 2)) & m) << (3 * k);
@@ -328,9 +337,10 @@ struct TwoPhase {
     // Per rm at most three of its five slots (a Working rm after TmAbort: Prepare, ChooseToAbort,
     // RcvAbort); TmCommit/TmAbort only while the TM is Init (then at most two per rm).
     int max_out_degree() const { return 2 + 3 * n; }
-    SR_HD u64 rmask() const { return (1ull << n) - 1; }
+    SR_HD u64 rmask() const { return (1ull << N()) - 1; }
     // per-rm bit vectors
     SR_HD u64 working(u64 s) const {  // rm_state == 0, one bit per rm
+        const int n = N();
         const u64 ev = 0x5555555555555555ull & ((1ull << (2 * n)) - 1);
         u64 w = ~(s | (s >> 1)) & ev;  // bit 2rm: field rm == 0
         // compress the even bits to bits 0..n-1
@@ -344,6 +354,7 @@ struct TwoPhase {
     // One 5-bit group per rm at slot 2 + 5rm (TmRcvPrepared, RmPrepare, RmChooseToAbort,
     // RmRcvCommitMsg, RmRcvAbortMsg), placed without per-action branches.
     SR_HD void enabled(const u64* sp, u64* m) const {
+        const int n = N();
         const u64 s = sp[0];
         const u64 tm = (s >> (2 * n)) & 3;
         const u64 prepared = (s >> (2 * n + 2)) & rmask();
@@ -367,6 +378,7 @@ struct TwoPhase {
     // other action can (RmPrepare and RmChooseToAbort need a Working rm and change it, TmCommit and
     // TmAbort need tm_state Init and change it).
     SR_HD void self_loops(const u64* sp, const u64* mk, u64* sl) const {
+        const int n = N();
         const u64 s = sp[0];
         const u64 tm = (s >> (2 * n)) & 3;
         const u64 prepared = (s >> (2 * n + 2)) & rmask();
@@ -395,6 +407,7 @@ struct TwoPhase {
     //   k = 3 RmRcvCommitMsg   rm_state <- 2
     //   k = 4 RmRcvAbortMsg    rm_state <- 3
     SR_HD bool apply(const u64* sp, int a, u64* o) const {
+        const int n = N();
         const u64 s = sp[0];
         const bool tm = a < 2;
         const u32 b = tm ? 0u : (u32)(a - 2), rm = b / 5, k = b - 5 * rm;
@@ -408,7 +421,7 @@ struct TwoPhase {
     }
     // rm_state fields, bit-parallel: bit 2rm of `ab` is set iff rm is Aborted (3), of `cm` iff
     // Committed (2) (the loop over the rms ran once per property for every new state).
-    SR_HD u64 even_mask() const { return 0x5555555555555555ull & ((1ull << (2 * n)) - 1); }
+    SR_HD u64 even_mask() const { return 0x5555555555555555ull & ((1ull << (2 * N())) - 1); }
     SR_HD bool discovers(int p, const u64* sp) const {
         const u64 s = sp[0], ev = even_mask();
         const u64 lo = s & ev, hi = (s >> 1) & ev;
@@ -450,6 +463,7 @@ struct TwoPhase {
     // reference's sort by rm_state alone (ties kept in index order), equal orbits always give equal
     // words, so the reduced state count does not depend on the visit order.
     SR_HD void canonical(const u64* sp, u64* o) const {
+        const int n = N();
         const u64 s = sp[0];
         u32 cnt[16];
 #pragma unroll
@@ -475,6 +489,7 @@ struct TwoPhase {
         return std::string(names[(id - 2) % 5]) + "(" + std::to_string((id - 2) / 5) + ")";
     }
 };
+using TwoPhase = TwoPhaseT<0>;
 
 // -----------------------------------------------------------------------------------------------
 // Increment (examples/increment.rs:109-197), n <= 15 threads: i (4 bits) then per thread
