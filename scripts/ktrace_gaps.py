@@ -1,16 +1,16 @@
 """Per-level kernel durations and the idle gap before each launch, from a rocprofv3 kernel trace of
 bench.py (scripts/ktrace.sh): the last complete check (dispatches after the last roots launch).
-    python3 scripts/ktrace_gaps.py gpurun_out/<dir>/.../trace_kernel_trace.csv
+    python3 scripts/ktrace_gaps.py gpurun_out/<dir>/.../trace_kernel_trace.csv [check index, -1 = last]
+(bench.py's last check is its counting pass, SR stats on: -2 is the last timed one.)
 """
 import csv
 import sys
 
 rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-starts = [i for i, r in enumerate(rows) if "roots" in r["Kernel_Name"]]
-a = starts[-2] if len(starts) > 1 else 0
-b = starts[-1] if len(starts) > 1 else len(rows)
-chk = rows[a:b]
+starts = [i for i, r in enumerate(rows) if "roots" in r["Kernel_Name"]] + [len(rows)]
+k = int(sys.argv[2]) if len(sys.argv) > 2 else -1
+chk = rows[starts[k - 1]:starts[k]]
 prev_end = None
 tot_k = tot_g = 0.0
 print(" idx  dur_us  gap_us  grid  kernel")

@@ -423,13 +423,20 @@ inline Tables& tables(int C, int device) {
 // for the other clients in ascending id (2 bits each). The field is a FUNCTION of the reference's
 // tester state (equal states <=> equal words still holds), so nothing is precomputed per history
 // and any client count fits; `linearizable` runs the tester's serialization search on it.
-struct PaxosHist {
+template <int CC = 0>
+struct PaxosHistT {
     u32 C = 2;
+    // CC > 0: the client count as a compile-time constant (PaxosT<W, CC>): the per-client loops of
+    // the tester and of `apply` unroll. The methods read it through NC().
+    SR_HD u32 NC() const {
+        if constexpr (CC > 0) return (u32)CC;
+        else return C;
+    }
     // Layout: every client's phase first (2 bits each: they sit in word 0's spare bits, where
     // `enabled` reads them with one shift), then the returned values (3 bits each), then each
     // client's Get `last` entries (2 bits per other client).
-    SR_HD u32 ret_off(u32 c) const { return 2 * C + 3 * c; }
-    SR_HD u32 last_off(u32 t, u32 u) const { return 5 * C + 2 * (C - 1) * t + 2 * (u < t ? u : u - 1); }
+    SR_HD u32 ret_off(u32 c) const { return 2 * NC() + 3 * c; }
+    SR_HD u32 last_off(u32 t, u32 u) const { return 5 * NC() + 2 * (NC() - 1) * t + 2 * (u < t ? u : u - 1); }
     SR_HD static u32 get(u64 lo, u64 hi, u32 off, u32 w) {
         const u64 v = off >= 64 ? hi >> (off - 64) : (lo >> off) | (off + w > 64 && off ? hi << (64 - off) : 0);
         return (u32)(v & ((1ull << w) - 1));
@@ -472,6 +479,7 @@ struct PaxosHist {
     // Checked against the search (`linearizable_search`) on every history of the paxos and
     // single-copy state spaces and on random histories (sr_selftest_models).
     SR_HD bool linearizable(u64 lo, u64 hi) const {
+        const u32 C = NC();
         u64 in = 0;  // byte b: the clusters that must precede cluster b (bit a)
         for (u32 t = 0; t < C; ++t) {
             if (phase(lo, hi, t) != 2) continue;  // completed Reads only
@@ -499,6 +507,7 @@ struct PaxosHist {
         return true;
     }
     SR_HD bool linearizable_search(u64 lo, u64 hi) const {
+        const u32 C = NC();
         // No completed Read: the completed ops are Writes invoked together at init, unordered in
         // real time, and any order of them (in-flight ops left out) is a valid serialization.
         // Packed scalars only (2-bit fields per client, 8-bit frames): an array indexed by client
@@ -606,26 +615,30 @@ struct PaxosHist {
     }
 };
 
+using PaxosHist = PaxosHistT<0>;
+
 // W = 11 holds the history of up to 4 clients in the 3 x 17 bits the servers leave free; W = 12
 // adds a word for 5 or 6 clients. `linearizable` runs the search once per new state (its property
 // check); caching its result in the state, computed at every client delivery, was no faster at 3
 // clients and 9 % slower at 6 (profiles/r04_paxos_lin_ab.txt).
-template <int WW>
+template <int WW, int CC = 0>
 struct PaxosT {
     static constexpr int W = WW, MW = 1, NPROPS = 2;
     static constexpr int NET0 = W - px::SLOTS / 2;  // first network word
     static_assert(NET0 == 3 || NET0 == 4, "servers (+ one history word) then the network");
-    int C = 2;
+    static_assert(CC == 0 || (CC >= 1 && CC <= (WW == 11 ? 4 : px::MAX_CLIENTS)), "client count of this encoding");
+    int C = 2;  // (= CC when CC > 0: the engines of the bench configurations, reg_paxos*.hip)
 
     static PaxosT make(int C) {
         if (C < 1 || C > max_clients()) throw Error(SR_ERR_UNSUPPORTED, "paxos: client_count out of this encoding's range");
+        if (CC > 0 && C != CC) throw Error(SR_ERR_ARG, "paxos: this engine is compiled for another client count");
         PaxosT m;
         m.C = C;
         return m;
     }
     static constexpr int max_clients() { return W == 11 ? 4 : px::MAX_CLIENTS; }
-    SR_HD PaxosHist hs() const {
-        PaxosHist h;
+    SR_HD PaxosHistT<CC> hs() const {
+        PaxosHistT<CC> h;
         h.C = (u32)C;
         return h;
     }
@@ -718,14 +731,14 @@ struct PaxosT {
                 if (i == dst) w[i] = (w[i] & ~px::SMASK) | nw;
         } else {  // RegisterActor::Client::on_msg (src/actor/register.rs:170-200), put_count = 1
             const u32 c = dst - 3, kind = px::e_kind(e);
-            const PaxosHist h = hs();
+            const PaxosHistT<CC> h = hs();
             u64 lo, hi;
             hist_get(s, lo, hi);
             const u32 ph = h.phase(lo, hi, c);
             if (ph == 0 && kind == px::PUTOK) {
                 // record_returns (WriteOk), then the Get is sent and recorded by record_invocations
                 out[nout++] = px::env(dst, (dst + 1) % 3, px::GET, 0, 0);  // request 2 * id
-                for (u32 u = 0; u < (u32)C; ++u)
+                for (u32 u = 0; u < h.NC(); ++u)
                     if (u != c) PaxosHist::put(lo, hi, h.last_off(c, u), 2, h.phase(lo, hi, u));
             } else if (ph == 1 && kind == px::GETOK) {
                 PaxosHist::put(lo, hi, h.ret_off(c), 3, px::e_val(e));  // record_returns (ReadOk(v))

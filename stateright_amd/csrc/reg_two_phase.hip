@@ -16,11 +16,13 @@ std::unique_ptr<EngineBase> reg_two_phase(const EngineArgs& a) {
     if (n < 1 || n > 14) throw Error(SR_ERR_UNSUPPORTED, "2pc: rm_count must be in 1..=14 (4n+4 <= 63 bits)");
     const TwoPhase m{(int)n, two_phase_owner_rms((int)n)};
     if (a.o->symmetry) return make_for(Canon<TwoPhase>(m), a);
-    // The single-GPU engine of the bench configurations (BASELINE configs[2], [3] on one GPU) with
-    // the rm count compiled in (TwoPhaseT<NC>). SR_2PC_GENERIC=1: the runtime-n engine (A/B).
-    if (!a.dist && !std::getenv("SR_2PC_GENERIC")) {
+    // The engines of the bench configurations with the rm count compiled in (TwoPhaseT<NC>: the
+    // per-rm loops unroll with constant shifts): BASELINE configs[2] (N = 9, 10) on one GPU and
+    // partitioned (the multi-GPU headline), configs[3] (N = 11) partitioned and on one GPU.
+    // SR_2PC_GENERIC=1: the runtime-n engine (A/B).
+    if (!std::getenv("SR_2PC_GENERIC")) {
         if (n == 9) return make_for(TwoPhaseT<9>{9, m.okey_rms}, a);
-        if (n == 10) return make_for(TwoPhaseT<10>{10, m.okey_rms}, a);
+        if (n == 10 && !a.dist) return make_for(TwoPhaseT<10>{10, m.okey_rms}, a);
         if (n == 11) return make_for(TwoPhaseT<11>{11, m.okey_rms}, a);
     }
     return make_for(m, a);
