@@ -580,10 +580,30 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_wave_barrier();
 }
 
+// Lane `src` of v, for a wave-uniform src: v_readlane into a scalar register (a __shfl is an LDS
+// permute, one LDS round trip on the chain).
+__device__ __forceinline__ u32 lane_u32(u32 v, u32 src) { return (u32)__builtin_amdgcn_readlane((int)v, (int)src); }
+
+// Inclusive prefix sum of v over the 64 lanes of a wave, VALU only: DPP row shifts 1, 2, 4, 8 scan
+// each row of 16 lanes, then row_bcast:15 adds row 0's total to row 1 (and row 2's to row 3) and
+// row_bcast:31 adds rows 0-1 to rows 2-3 (GFX9 DPP). The __shfl_up form was six dependent LDS
+// permutes (~0.5 us on a lone wave's chain).
+__device__ __forceinline__ u32 wave_incl_scan(u32 v) {
+    int x = (int)v;
+    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);  // row_shr:1
+    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);  // row_shr:2
+    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);  // row_shr:4
+    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);  // row_shr:8
+    x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);  // row_bcast:15 (rows 1, 3)
+    x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);  // row_bcast:31 (rows 2, 3)
+    return (u32)x;
+}
+// Sum of v over the wave, in every lane.
+__device__ __forceinline__ u32 wave_sum(u32 v) { return lane_u32(wave_incl_scan(v), 63); }
+
 // Sum of v over the workgroup, returned to every thread (one LDS round).
 __device__ __forceinline__ u32 block_sum(u32 v, u32* scratch) {
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+    v = wave_sum(v);
     if ((threadIdx.x & 63) == 0) scratch[threadIdx.x >> 6] = v;
     __syncthreads();
     u32 t = 0;
@@ -606,11 +626,8 @@ __device__ __forceinline__ u64 block_sum64(u64 v, u64* sc) {
 
 // Sums of a and b over the workgroup, returned to every thread (one LDS round for both).
 __device__ __forceinline__ void block_sum2(u32 a, u32 b, u32* scratch, u32& ta, u32& tb) {
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) {
-        a += __shfl_xor(a, d, 64);
-        b += __shfl_xor(b, d, 64);
-    }
+    a = wave_sum(a);
+    b = wave_sum(b);
     if ((threadIdx.x & 63) == 0) {
         scratch[2 * (threadIdx.x >> 6)] = a;
         scratch[2 * (threadIdx.x >> 6) + 1] = b;
@@ -857,14 +874,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W >
 #endif
         }
         // wave-inclusive scan of the counts
-        u32 incl = cnt;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            u32 y = __shfl_up(incl, d, 64);
-            if (lane >= d) incl += y;
-        }
+        const u32 incl = wave_incl_scan(cnt);
         u32 nidx = incl - cnt;  // this parent's next successor index (its entries are [excl, incl))
-        const u32 total = __shfl(incl, 63, 64);
+        const u32 total = lane_u32(incl, 63);
         if (lane == 0) enabled += total;
 #if SR_TIMELINE
         if (tl_first_chunk) SR_TL(11);
@@ -881,11 +893,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W >
             const int leader = __builtin_ctzll(mask);
             u32 sb = 0;
             if (lane == leader) sb = atomicAdd(&stage_n, cnt);
-            sb = __shfl(sb, leader, 64);
+            sb = lane_u32(sb, (u32)leader);
             const u32 in_stage = sb >= (u32)STAGE ? 0u : min(cnt, (u32)STAGE - sb);
             u32 gb = 0;
             if (cnt > in_stage && lane == leader) gb = atomicAdd(&lc->claims, cnt - in_stage);
-            gb = __shfl(gb, leader, 64);
+            gb = lane_u32(gb, (u32)leader);
             if (!nw) return;
             const u32 pr = wave0 + par;  // parent rank
             if (below < in_stage) {
@@ -918,7 +930,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W >
                 u32 p = 0;
 #pragma unroll
                 for (int q = 1; q < 8; ++q) {
-                    const u32 ex = (u32)__shfl((int)excl, q, 64);
+                    const u32 ex = lane_u32(excl, (u32)q);
                     if ((u32)q < ppw && ex <= j) p = (u32)q;
                 }
                 const u32 k = j - (u32)__shfl((int)excl, (int)p, 64);
@@ -1136,11 +1148,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W >
                 const int leader = __builtin_ctzll(mask);
                 u32 sb = 0;
                 if (lane == leader) sb = atomicAdd(&stage_n, cnt);
-                sb = __shfl(sb, leader, 64);
+                sb = lane_u32(sb, (u32)leader);
                 const u32 in_stage = sb >= (u32)STAGE ? 0u : min(cnt, (u32)STAGE - sb);
                 u32 gb = 0;
                 if (cnt > in_stage && lane == leader) gb = atomicAdd(&lc->claims, cnt - in_stage);
-                gb = __shfl(gb, leader, 64);
+                gb = lane_u32(gb, (u32)leader);
                 if (!nw[j]) continue;
                 const u32 pr = wave0 + par[j];  // parent rank
                 if (below < in_stage) {
@@ -1530,12 +1542,7 @@ constexpr int SCAN_TILE = SCAN_BLOCK * SCAN_ITEMS;
 __device__ __forceinline__ u32 block_exclusive_scan(u32 v, u32* total) {
     __shared__ u32 wsum[SCAN_BLOCK / 64];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    u32 x = v;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        u32 y = __shfl_up(x, d, 64);
-        if (lane >= d) x += y;
-    }
+    const u32 x = wave_incl_scan(v);
     if (lane == 63) wsum[wid] = x;
     __syncthreads();
     u32 base = 0, tot = 0;

@@ -345,14 +345,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W <
 #pragma unroll
             for (int i = 0; i < MW; ++i) cnt += __popcll(mk[i]);
         }
-        u32 incl = cnt;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            u32 y = __shfl_up(incl, d, 64);
-            if (lane >= d) incl += y;
-        }
+        const u32 incl = wave_incl_scan(cnt);
         u32 nidx = incl - cnt;
-        const u32 total = __shfl(incl, 63, 64);
+        const u32 total = lane_u32(incl, 63);
         if (lane == 0) enabled += total;
 
         for (u32 w0 = 0; w0 < total; w0 += MAPCAP) {
@@ -425,7 +420,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W <
                     const int rleader = __builtin_ctzll(rmask);
                     u32 rsb = 0;
                     if (lane == rleader) rsb = atomicAdd(&rstage_n, rcnt);
-                    rsb = __shfl(rsb, rleader, 64);
+                    rsb = lane_u32(rsb, (u32)rleader);
                     const u32 rin = rsb >= RSTAGE ? 0u : min(rcnt, RSTAGE - rsb);
                     if (rem && rbelow < rin) {
                         const u32 kk = rsb + rbelow;
@@ -437,13 +432,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W <
                     if (om && lane == 0) sent_any = 1;
                     while (om) {
                         const int leader = __builtin_ctzll(om);
-                        const u32 qo = __shfl(own, leader, 64);
+                        const u32 qo = lane_u32(own, (u32)leader);
                         const bool mine = rem && rbelow >= rin && own == qo;
                         const u64 qm = __ballot(mine);
                         om &= ~qm;
                         u32 gb = 0;
                         if (lane == leader) gb = atomicAdd(&send_counts[qo * SENDC_STRIDE], (u32)__popcll(qm));
-                        gb = __shfl(gb, leader, 64);
+                        gb = lane_u32(gb, (u32)leader);
                         if (mine) {
                             const u32 pos = gb + __popcll(qm & lanes_below);
                             if (pos < bucket_cap) {
@@ -522,11 +517,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W <
                     const int leader = __builtin_ctzll(mask);
                     u32 sb = 0;
                     if (lane == leader) sb = atomicAdd(&stage_n, cnt);
-                    sb = __shfl(sb, leader, 64);
+                    sb = lane_u32(sb, (u32)leader);
                     const u32 in_stage = sb >= (u32)STAGE ? 0u : min(cnt, (u32)STAGE - sb);
                     u32 gb = 0;
                     if (cnt > in_stage && lane == leader) gb = atomicAdd(&lc->claims, cnt - in_stage);
-                    gb = __shfl(gb, leader, 64);
+                    gb = lane_u32(gb, (u32)leader);
                     if (!nw) continue;
                     if (below < in_stage) {
                         const u32 kk = sb + below;
@@ -625,11 +620,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W <
                     const int leader = __builtin_ctzll(mask);
                     u32 sb = 0;
                     if (lane == leader) sb = atomicAdd(&stage_n, cnt);
-                    sb = __shfl(sb, leader, 64);
+                    sb = lane_u32(sb, (u32)leader);
                     const u32 in_stage = sb >= (u32)STAGE ? 0u : min(cnt, (u32)STAGE - sb);
                     u32 gb = 0;
                     if (cnt > in_stage && lane == leader) gb = atomicAdd(&lc->claims, cnt - in_stage);
-                    gb = __shfl(gb, leader, 64);
+                    gb = lane_u32(gb, (u32)leader);
                     if (nw[j]) {
                         if (below < in_stage) {
                             const u32 kk = sb + below;
@@ -656,7 +651,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W <
                 const int rleader = __builtin_ctzll(rmask);
                 u32 rsb = 0;
                 if (lane == rleader) rsb = atomicAdd(&rstage_n, rcnt);
-                rsb = __shfl(rsb, rleader, 64);
+                rsb = lane_u32(rsb, (u32)rleader);
                 const u32 rin = rsb >= RSTAGE ? 0u : min(rcnt, RSTAGE - rsb);
                 if (rem[j] && rbelow < rin) {
                     const u32 kk = rsb + rbelow;
@@ -669,13 +664,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W <
                 if (om && lane == 0) sent_any = 1;
                 while (om) {
                     const int leader = __builtin_ctzll(om);
-                    const u32 q = __shfl(own[j], leader, 64);
+                    const u32 q = lane_u32(own[j], (u32)leader);
                     const bool mine = rem[j] && rbelow >= rin && own[j] == q;
                     const u64 qm = __ballot(mine);
                     om &= ~qm;
                     u32 gb = 0;
                     if (lane == leader) gb = atomicAdd(&send_counts[q * SENDC_STRIDE], (u32)__popcll(qm));
-                    gb = __shfl(gb, leader, 64);
+                    gb = lane_u32(gb, (u32)leader);
                     if (mine) {
                         const u32 pos = gb + __popcll(qm & lanes_below);
                         if (pos < bucket_cap) {
@@ -875,11 +870,11 @@ __device__ __forceinline__ void insert_records(const M& m, RecAt rec_at, u32 tot
                 const int leader = __builtin_ctzll(mask);
                 u32 sb = 0;
                 if (lane == leader) sb = atomicAdd(&stage_n, cnt);
-                sb = __shfl(sb, leader, 64);
+                sb = lane_u32(sb, (u32)leader);
                 const u32 in_stage = sb >= STAGE ? 0u : min(cnt, STAGE - sb);
                 u32 gb = 0;
                 if (cnt > in_stage && lane == leader) gb = atomicAdd(&lc->claims, cnt - in_stage);
-                gb = __shfl(gb, leader, 64);
+                gb = lane_u32(gb, (u32)leader);
                 if (!nw) continue;
                 if (below < in_stage) {
 #pragma unroll
@@ -940,11 +935,11 @@ __device__ __forceinline__ void insert_records(const M& m, RecAt rec_at, u32 tot
             const int leader = __builtin_ctzll(mask);
             u32 sb = 0;
             if (lane == leader) sb = atomicAdd(&stage_n, cnt);
-            sb = __shfl(sb, leader, 64);
+            sb = lane_u32(sb, (u32)leader);
             const u32 in_stage = sb >= STAGE ? 0u : min(cnt, STAGE - sb);
             u32 gb = 0;
             if (cnt > in_stage && lane == leader) gb = atomicAdd(&lc->claims, cnt - in_stage);
-            gb = __shfl(gb, leader, 64);
+            gb = lane_u32(gb, (u32)leader);
             if (!nw) continue;
             if (below < in_stage) {
 #pragma unroll
