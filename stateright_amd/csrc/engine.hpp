@@ -315,7 +315,8 @@ class Engine final : public EngineBase {
         if (make_table_view(m_, nullptr, nullptr, min_table_cap(m_)).qbits) filt_log2_ = 0;
         if (const char* e = std::getenv("SR_PIPELINE")) pipeline_ = std::atoi(e) != 0;
         if (const char* e = std::getenv("SR_QUERY_LOG2")) query_mask_ = (1ull << std::atoi(e)) - 1;
-        if (const char* e = std::getenv("SR_GRID_MAX")) grid_max_ = (u32)std::max(0, std::atoi(e));  // <= 0: unset
+        if (const char* e = std::getenv("SR_GRID_MAX")) grid_env_ = (u32)std::max(0, std::atoi(e));  // <= 0: unset
+        if (const char* e = std::getenv("SR_WIDE_NOPF")) wide_nopf_ = std::atoi(e) ? 1 : 0;
         if (const char* e = std::getenv("SR_TABLE_RECYCLE")) table_recycle_ = std::atoi(e) != 0;
     }
     ~Engine() override = default;
@@ -1128,16 +1129,29 @@ class Engine final : public EngineBase {
     // avoid a partial last wave of workgroups. The measured gain is small and of the order of the
     // ±3% run-to-run noise (`profiles/r01_grid_sweep.jsonl`, `r01_gridcap_default.jsonl`); the cap
     // is printed with verbose=1. SR_GRID_MAX > 0 overrides it (<= 0 or unparsable: the default).
-    u32 expand_grid_cap() {
-        if (grid_max_) return grid_max_;
+    u32 expand_grid_cap(bool nopf = false) {
+        u32& cap = nopf ? grid_max_nopf_ : grid_max_;
+        if (cap) return cap;
+        if (grid_env_) return cap = grid_env_;
         int per_cu = 0, cus = 0;
         const size_t dyn = filt_log2_ ? (8u << filt_log2_) : 0u;
         const void* k = probe_loop() < 0 ? (const void*)expand_fast<M, -4, 0> : (const void*)expand_fast<M, 1, 0>;
+        if constexpr (W >= 4)
+            if (nopf) k = (const void*)expand_fast<M, 1, 0, false, true>;
         SR_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 256, dyn));
         SR_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, o_.device));
-        grid_max_ = per_cu > 0 && cus > 0 ? (u32)(2 * per_cu * cus) : ~0u;
-        if (o_.verbose) std::fprintf(stderr, "[sr] expand grid cap %u blocks (%d per CU x %d CUs x 2)\n", grid_max_, per_cu, cus);
-        return grid_max_;
+        cap = per_cu > 0 && cus > 0 ? (u32)(2 * per_cu * cus) : ~0u;
+        if (o_.verbose) std::fprintf(stderr, "[sr] expand grid cap %u blocks (%d per CU x %d CUs x 2)%s\n", cap, per_cu, cus, nopf ? " [no prefetch]" : "");
+        return cap;
+    }
+    // Wide states: the kernel without the register prefetch of the next chunk's parents when every
+    // chunk of the level has its own workgroup within that kernel's grid cap (DESIGN.md §3 "Wide
+    // states"); the prefetching kernel when workgroups stride over chunks. SR_WIDE_NOPF=0/1 forces.
+    bool use_nopf(u64 chunks) {
+        if constexpr (W < 4) return false;
+        if (o_.counters || wide_nopf_ == 0) return false;
+        if (wide_nopf_ == 1) return true;
+        return chunks <= expand_grid_cap(true);
     }
 
     // One expand_fast launch over a whole level whose frontier starts at arena offset `fbase`:
@@ -1148,7 +1162,9 @@ class Engine final : public EngineBase {
         const u64 nbase = fbase + (dev_n ? 0 : n);  // start of the next level (dev_n: + n on the device)
         const u32 ncap = (u32)std::min<u64>(arena_cap_ - nbase, 0xffffffffu);
         const u32 ppw_log2 = ppw_env_ >= 0 ? (u32)ppw_env_ : ppw_for(shape);
-        const u32 grid = std::min(expand_grid_cap(), std::max<u32>(1, blocks_for((shape + (1u << ppw_log2) - 1) >> ppw_log2, 4)));
+        const u32 chunks = std::max<u32>(1, blocks_for((shape + (1u << ppw_log2) - 1) >> ppw_log2, 4));
+        const bool nopf = use_nopf(chunks);
+        const u32 grid = std::min(expand_grid_cap(nopf), chunks);
         seq_launch_[sq] = launch_frontier.size();
         // a slotted launch: it counts into its own slot and is published by its successor
         SlotWork sw = slot_work(dev_n);
@@ -1167,6 +1183,7 @@ class Engine final : public EngineBase {
                     undiscovered, nullptr, sq, 0u, ppw_log2, filt_log2_, sw);
             };
             if (o_.counters) launch(expand_fast<M, 1, 0, true>);
+            else if (nopf) launch_nopf(launch);
             else if (probe_loop() < 0) launch(expand_fast<M, -4, 0>);
             else launch(expand_fast<M, 1, 0>);
         }, n);
@@ -1232,7 +1249,9 @@ class Engine final : public EngineBase {
                     u64* next = arena_.p + nbase * W;
                     u32* npar = apar_.p + nbase;
                     const u32 ppw_log2 = ppw_env_ >= 0 ? (u32)ppw_env_ : ppw_for(c);
-                    const u32 grid = std::min(expand_grid_cap(), blocks_for((c + (1u << ppw_log2) - 1) >> ppw_log2, 4));
+                    const u32 chunks = std::max<u32>(1, blocks_for((c + (1u << ppw_log2) - 1) >> ppw_log2, 4));
+                    const bool nopf = use_nopf(chunks);
+                    const u32 grid = std::min(expand_grid_cap(nopf), chunks);
                     SlotWork sw{};
                     sw.flags = repair ? SLOT_REPAIR : 0u;
                     if (emask_ && peb) {
@@ -1246,6 +1265,7 @@ class Engine final : public EngineBase {
                                 last ? 1u : 0u, ppw_log2, filt_log2_, sw);
                         };
                         if (o_.counters) launch(expand_fast<M, 1, 0, true>);
+                        else if (nopf) launch_nopf(launch);
                         else if (probe_loop() < 0) launch(expand_fast<M, -4, 0>);
                         else launch(expand_fast<M, 1, 0>);
                     });
@@ -1348,6 +1368,14 @@ class Engine final : public EngineBase {
     int ppw_env_ = -1;
     bool table_recycle_ = true;  // the visited set is returned zeroed (~Engine)
     u32 grid_max_ = 0;      // cap on expand_fast's grid, 0 = two device residencies (SR_GRID_MAX)
+    u32 grid_max_nopf_ = 0;  // ... of its wide no-prefetch form
+    u32 grid_env_ = 0;       // SR_GRID_MAX
+    int wide_nopf_ = -1;     // SR_WIDE_NOPF: -1 chosen per level (use_nopf), 0 never, 1 always
+    // the no-prefetch form exists for wide states only (it is the prefetching kernel otherwise)
+    template <class L>
+    void launch_nopf(L& launch) {
+        if constexpr (W >= 4) launch(expand_fast<M, 1, 0, false, true>);
+    }
     u64 query_mask_ = 4095;  // spins between hipStreamQuery calls in wait_publish (SR_QUERY_LOG2)
     bool pipeline_ = true;  // FAST-order level pipelining (SR_PIPELINE=0 disables, for A/B runs)
     DBuf<u64> slots_;                 // SLOTS per-level counter slots (the pipelined loop)

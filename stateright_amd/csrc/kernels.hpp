@@ -44,6 +44,10 @@ constexpr int MAX_PARTS = 64;  // visited-set partitions (one per GPU, or virtua
 #ifndef SR_WIDE_STAGE_WORDS
 #define SR_WIDE_STAGE_WORDS 2048
 #endif
+// expand_fast's waves per SIMD for wide states (their VGPR budget: 3 -> <= 168, 4 -> <= 128).
+#ifndef SR_WIDE_WAVES
+#define SR_WIDE_WAVES 3
+#endif
 
 // ERR_EXCHANGE: the direct exchange delivered a receive slot whose sequence tag or checksum does
 // not match what its source stored (kernels_dist.hpp): the check is redone on the collective exchange.
@@ -702,8 +706,8 @@ __device__ u64* g_timeline;
 // the kernel's time.
 // Wide states (W >= 4: paxos, the actor models) run three waves per SIMD (<= 168 VGPRs): their
 // levels are latency-bound, and paxos' device-side history search had pushed them to two.
-template <class M, int PB, int POL, bool STATS = false>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W >= 4 ? 3 : PB < 0 ? 6 : 1))) expand_fast(M m, const u64* __restrict__ frontier, u32 lo, u32 hi,
+template <class M, int PB, int POL, bool STATS = false, bool NOPF = false>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W >= 4 ? SR_WIDE_WAVES : PB < 0 ? 6 : 1))) expand_fast(M m, const u64* __restrict__ frontier, u32 lo, u32 hi,
                                                    TableView t, u64* __restrict__ next, u32* __restrict__ next_par,
                                                    u32 next_cap, LevelCounters* lc, u32 undiscovered,
                                                    HostCounters* hc, u32 seq, u32 reset, u32 ppw_log2,
@@ -725,7 +729,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W >
 #ifndef SR_MAPCAP
 #define SR_MAPCAP 1024
 #endif
-    constexpr u32 MAPCAP = SR_MAPCAP;
+    // (wide states: ~2 successors per parent and <= 32 parents per wave fill a quarter of it)
+#ifndef SR_WIDE_MAPCAP
+#define SR_WIDE_MAPCAP 256
+#endif
+    constexpr u32 MAPCAP = W >= 4 ? SR_WIDE_MAPCAP : SR_MAPCAP;
     static_assert(MW * 64 <= 1024, "action ids must fit 10 bits");
     __shared__ u16 smap[4][MAPCAP];
     __shared__ u32 stage_n, base, scratch[8];
@@ -807,14 +815,33 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W >
     // chunk's probes instead of stalling the chunk start.
     const u64 cstride = (u64)nblk * chunk;
     if (!spec_first && lane < (int)ppw && r_first < hi) load_state<W>(frontier, r_first, nxt);
-    for (u64 c0 = lo + (u64)blockIdx.x * chunk; c0 < hi; c0 += cstride) {
+    // Wide states without the register prefetch (NOPF: PF false): the first chunk's parents go to
+    // the wave's LDS copy here, later chunks load theirs at the chunk start. The W-word prefetch
+    // holds 2W VGPRs through every probe round, and a wide kernel's residency is set by its VGPRs
+    // (paxos C=3: 146 -> 124 VGPRs, 3 -> 4 blocks per CU). The host takes this form for levels
+    // whose chunks all fit the grid (no block strides, so nothing is prefetched anyway).
+    constexpr bool PF = W < 4 || !NOPF;
+    const u64 c_first = lo + (u64)blockIdx.x * chunk;
+    if constexpr (!PF) {
+        if (lane < (int)ppw && r_first < hi) {
+#pragma unroll
+            for (int i = 0; i < W; ++i) pst[wid][lane * W + i] = nxt[i];
+        }
+    }
+    for (u64 c0 = c_first; c0 < hi; c0 += cstride) {
         const u32 wave0 = (u32)(c0 + ((u64)wid << ppw_log2));  // first parent of the wave
         const u32 r = wave0 + lane;
         u32 cnt = 0;
         u64 s[W];
+        if constexpr (PF) {
 #pragma unroll
-        for (int i = 0; i < W; ++i) s[i] = nxt[i];
-        if (lane < (int)ppw && r + cstride < hi) load_state<W>(frontier, r + cstride, nxt);
+            for (int i = 0; i < W; ++i) s[i] = nxt[i];
+            if (lane < (int)ppw && r + cstride < hi) load_state<W>(frontier, r + cstride, nxt);
+        } else if (c0 != c_first && lane < (int)ppw && r < hi) {
+            load_state<W>(frontier, r, s);  // (the wave's previous parents were last read by its own rounds)
+#pragma unroll
+            for (int i = 0; i < W; ++i) pst[wid][lane * W + i] = s[i];
+        }
         // the stage's fill is read by every thread at the end of the previous chunk before any
         // wave appends again (and the wave's parents are no longer read)
         __syncthreads();
@@ -827,7 +854,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W >
             static_assert(MW == 1 && M::ESLOTS <= 64 && 64 % M::ESLOTS == 0, "enabled_slot: ESLOTS must divide 64");
             static_assert(!has_self_loops<M>::value, "enabled_slot: no self_loops hook");
             constexpr u32 ES = M::ESLOTS, PPP = 64 / ES;
-            if (lane < (int)ppw && r < hi) {
+            if (PF && lane < (int)ppw && r < hi) {
 #pragma unroll
                 for (int i = 0; i < W; ++i) pst[wid][lane * W + i] = s[i];
             }
@@ -851,6 +878,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W >
 #endif
         } else
         if (lane < ppw && r < hi) {
+            if constexpr (!PF) {
+#pragma unroll
+                for (int i = 0; i < W; ++i) s[i] = pst[wid][lane * W + i];  // (this lane's own LDS words)
+            }
             m.enabled(s, mk);
 #if SR_TIMELINE
             if (tl_first_chunk) SR_TL(2);
@@ -865,8 +896,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W >
                     mk[i] &= ~sl[i];
                 }
             }
+            if constexpr (PF) {
 #pragma unroll
-            for (int i = 0; i < W; ++i) pst[wid][lane * W + i] = s[i];
+                for (int i = 0; i < W; ++i) pst[wid][lane * W + i] = s[i];
+            }
 #pragma unroll
             for (int i = 0; i < MW; ++i) cnt += __popcll(mk[i]);
 #if SR_TIMELINE
