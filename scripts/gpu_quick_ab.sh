@@ -1,32 +1,27 @@
 #!/bin/bash
-# Wide states: the base library (register prefetch of the next chunk's parents, 146 VGPRs, 3 blocks
-# per CU) against the current one (the no-prefetch kernel chosen per level when no block strides;
-# SR_WIDE_NOPF=0 forces the prefetching kernel, with the 256-entry wide successor map).
+# The visited set as ordinary (SR_TABLE_KIND=0), fine-grained (1) and uncached (2) device memory: does a
+# kernel boundary after a big level cost the write-back of the L2s' dirty table lines?
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 T=${1:-q}
 O=gpurun_out/$T
 mkdir -p $O
-export SR_LIB_DIGEST_CHECK=0
-LIB=stateright_amd/libstateright_gpu.so
-cp "$LIB" gpurun_ab/lib_cur.so || exit 1
-timeout -k 10 500 python -u -m pytest tests/test_gpu_actor.py tests/test_gpu_parity.py -m gpu -x -q -k "paxos or actor or single or abd or ping or register" --timeout 120 --timeout-method thread > $O/parity.log 2>&1 || { tail -30 $O/parity.log; exit 1; }
-tail -1 $O/parity.log
-run() {  # label lib env... -- bench args
-    local label=$1 lib=$2; shift 2
+SR_TABLE_KIND=2 timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread > $O/parity_uc.log 2>&1 || { tail -30 $O/parity_uc.log; exit 1; }
+tail -1 $O/parity_uc.log
+run() {  # label env -- bench args
+    local label=$1; shift
     local envs=()
     while [ "$1" != "--" ]; do envs+=("$1"); shift; done; shift
-    cp "gpurun_ab/lib_$lib.so" "$LIB" || exit 1
-    env "${envs[@]}" timeout -k 10 200 python -u bench.py --cpu-baseline 0 --config4-steps 0 --no-hint-steps 0 "$@" > "$O/$label.json" 2> "$O/$label.err" || { tail -5 "$O/$label.err"; cp gpurun_ab/lib_cur.so "$LIB"; exit 1; }
+    env "${envs[@]}" timeout -k 10 200 python -u bench.py --cpu-baseline 0 --config4-steps 0 --no-hint-steps 0 "$@" > "$O/$label.json" 2> "$O/$label.err" || { tail -5 "$O/$label.err"; exit 1; }
     python3 -c "import json; d=json.loads(open('$O/$label.json').read().strip().splitlines()[-1]); l=d.get('levels') or {}; print('$label', round(d['ms_per_step'],4), 'small', round(l.get('small_levels_ms',0),4), 'big', round(l.get('big_levels_ms',0),4), 'gaps', round(l.get('gaps_ms',0),4))"
 }
-for r in 1 2 3; do
-    for cfg in "px3:--model paxos --clients 3 --steps 200 --warmup 5" "px6:--model paxos --clients 6 --steps 30 --warmup 2" "sc4:--model single_copy --clients 4 --steps 100 --warmup 5"; do
+for r in 1 2; do
+    for cfg in "tp9:--steps 50 --warmup 3" "tp10:--rm-count 10 --steps 5 --warmup 1" "px3:--model paxos --clients 3 --steps 200 --warmup 5"; do
         name=${cfg%%:*}; args=${cfg#*:}
-        run ${name}_base_r$r base SR_X=0 -- $args || exit 1
-        run ${name}_cur_r$r cur SR_X=0 -- $args || exit 1
-        run ${name}_cur_pf_r$r cur SR_WIDE_NOPF=0 -- $args || exit 1
+        run ${name}_k0_r$r SR_TABLE_KIND=0 -- $args || exit 1
+        run ${name}_k2_r$r SR_TABLE_KIND=2 -- $args || exit 1
+        run ${name}_k1_r$r SR_TABLE_KIND=1 -- $args || exit 1
     done
 done
-cp gpurun_ab/lib_cur.so "$LIB"
+SR_TABLE_KIND=2 bash scripts/ktrace.sh $T/kt_tp9_k2 --steps 20 --warmup 3 --cpu-baseline 0 --config4-steps 0 --no-hint-steps 0 || exit 1
 echo "quick ab ok"

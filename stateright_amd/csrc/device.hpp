@@ -100,7 +100,8 @@ class DevicePool {
     // kind 0: ordinary (coarse-grained) device memory; kind 1: fine-grained device memory
     // (hipDeviceMallocFinegrained), which a system-scope acquire makes coherent with stores that
     // ANOTHER device issued over xGMI while a kernel runs (the direct exchange's flags and receive
-    // buffers: its owner's L2 must not serve a line it cached before a peer's store).
+    // buffers: its owner's L2 must not serve a line it cached before a peer's store); kind 2:
+    // uncached device memory (hipDeviceMallocUncached: no line of it is held dirty in an L2).
     void* alloc(int dev, size_t bytes, int kind = 0) {
         bytes = round(bytes);
         {
@@ -116,7 +117,9 @@ class DevicePool {
         }
         void* p = nullptr;
         auto raw = [&]() {
-            return kind == 1 ? hipExtMallocWithFlags(&p, bytes, hipDeviceMallocFinegrained) : hipMalloc(&p, bytes);
+            return kind == 1   ? hipExtMallocWithFlags(&p, bytes, hipDeviceMallocFinegrained)
+                   : kind == 2 ? hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached)
+                               : hipMalloc(&p, bytes);
         };
         const auto t0 = std::chrono::steady_clock::now();
         hipError_t e = raw();
@@ -140,17 +143,17 @@ class DevicePool {
     // Blocks handed back while the work that zeroes them is still in flight: `ready` is recorded
     // behind that work. A check returns its visited set this way as soon as its last level is
     // done, and the clear then runs while the host finishes that check and sets up the next one.
-    void free_zeroed(int dev, void* p, size_t bytes, hipEvent_t ready) {
+    void free_zeroed(int dev, void* p, size_t bytes, hipEvent_t ready, int kind = 0) {
         std::lock_guard<std::mutex> g(mu_);
-        zeroed_[{dev, round(bytes)}].push_back({p, ready});
+        zeroed_[{dev, round(bytes), kind}].push_back({p, ready});
     }
     // A zeroed block of this size if one is pooled, with `s` ordered after its clear on the device
     // (the host does not wait), else nullptr. A block whose clear has finished is preferred.
-    void* alloc_zeroed(int dev, size_t bytes, hipStream_t s) {
+    void* alloc_zeroed(int dev, size_t bytes, hipStream_t s, int kind = 0) {
         Zeroed z{nullptr, nullptr};
         {
             std::lock_guard<std::mutex> g(mu_);
-            auto& fl = zeroed_[{dev, round(bytes)}];
+            auto& fl = zeroed_[{dev, round(bytes), kind}];
             if (fl.empty()) return nullptr;
             size_t pick = 0;
             for (size_t i = 0; i < fl.size(); ++i)
@@ -166,7 +169,7 @@ class DevicePool {
         if (e != hipSuccess) {
             (void)hipEventSynchronize(z.ready);
             (void)hipEventDestroy(z.ready);
-            free(dev, z.p, bytes);  // not known to be ordered for this stream: an ordinary block
+            free(dev, z.p, bytes, kind);  // not known to be ordered for this stream: an ordinary block
             return nullptr;
         }
         (void)hipEventDestroy(z.ready);  // the wait holds what it needs
@@ -181,7 +184,7 @@ class DevicePool {
                 v.clear();
             }
         for (auto& [k, v] : zeroed_)
-            if (k.first == dev) {
+            if (std::get<0>(k) == dev) {
                 for (auto& z : v) {
                     (void)hipEventSynchronize(z.ready);
                     (void)hipEventDestroy(z.ready);
@@ -221,7 +224,7 @@ class DevicePool {
     // whose clear is still in flight is left for the check it was released for (alloc() has no
     // stream to order after it).
     void* take_zeroed_locked(int dev, size_t bytes) {
-        auto it = zeroed_.find({dev, bytes});
+        auto it = zeroed_.find({dev, bytes, 0});
         if (it == zeroed_.end()) return nullptr;
         auto& fl = it->second;
         for (size_t i = 0; i < fl.size(); ++i) {
@@ -237,7 +240,7 @@ class DevicePool {
     }
     std::mutex mu_;
     std::map<std::tuple<int, size_t, int>, std::vector<void*>> free_;
-    std::map<std::pair<int, size_t>, std::vector<Zeroed>> zeroed_;
+    std::map<std::tuple<int, size_t, int>, std::vector<Zeroed>> zeroed_;
     std::map<int, uint64_t> epoch_;
 };
 
@@ -268,13 +271,14 @@ struct DBuf {
     }
     // All-zero bytes, ordered before the work enqueued on `s` afterwards: a pooled zeroed block,
     // or a fresh one cleared on `s`.
-    void alloc_zero(int d, size_t count, hipStream_t s) {
+    void alloc_zero(int d, size_t count, hipStream_t s, int k = 0) {
         reset();
         dev = d;
         n = count ? count : 1;
-        p = static_cast<T*>(DevicePool::get().alloc_zeroed(d, n * sizeof(T), s));
+        kind = k;
+        p = static_cast<T*>(DevicePool::get().alloc_zeroed(d, n * sizeof(T), s, k));
         if (p) return;
-        p = static_cast<T*>(DevicePool::get().alloc(d, n * sizeof(T)));
+        p = static_cast<T*>(DevicePool::get().alloc(d, n * sizeof(T), k));
         SR_HIP(hipMemsetAsync(p, 0, n * sizeof(T), s));
     }
     // Hands the block back to be zeroed on `s` behind the work enqueued there so far (alloc_zero
@@ -284,9 +288,10 @@ struct DBuf {
         hipEvent_t ready = nullptr;
         if (hipEventCreateWithFlags(&ready, hipEventDisableTiming) == hipSuccess) {
             if (hipMemsetAsync(p, 0, n * sizeof(T), s) == hipSuccess && hipEventRecord(ready, s) == hipSuccess) {
-                DevicePool::get().free_zeroed(dev, p, n * sizeof(T), ready);
+                DevicePool::get().free_zeroed(dev, p, n * sizeof(T), ready, kind);
                 p = nullptr;
                 n = 0;
+                kind = 0;
                 return;
             }
             (void)hipEventDestroy(ready);

@@ -14,6 +14,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <immintrin.h>
 #include <memory>
 #include <string>
@@ -317,6 +318,8 @@ class Engine final : public EngineBase {
         if (const char* e = std::getenv("SR_QUERY_LOG2")) query_mask_ = (1ull << std::atoi(e)) - 1;
         if (const char* e = std::getenv("SR_GRID_MAX")) grid_env_ = (u32)std::max(0, std::atoi(e));  // <= 0: unset
         if (const char* e = std::getenv("SR_WIDE_NOPF")) wide_nopf_ = std::atoi(e) ? 1 : 0;
+        if (const char* e = std::getenv("SR_CHAIN_MAX")) chain_max_ = (u64)std::max(0ll, std::atoll(e));
+        if (const char* e = std::getenv("SR_TABLE_KIND")) table_kind_ = std::atoi(e);
         if (const char* e = std::getenv("SR_TABLE_RECYCLE")) table_recycle_ = std::atoi(e) != 0;
     }
     ~Engine() override = default;
@@ -484,7 +487,7 @@ class Engine final : public EngineBase {
     void alloc_table(u64 cap) {
         cap_ = cap;
         lmax_ = max_load(cap);
-        keys_.alloc_zero(o_.device, cap, stream_);
+        keys_.alloc_zero(o_.device, cap, stream_, table_kind_);
         if (fifo_) {
             meta_.alloc(o_.device, cap);
             SR_HIP(hipMemsetAsync(meta_.p, 0xff, cap * sizeof(u64), stream_));
@@ -1036,21 +1039,36 @@ class Engine final : public EngineBase {
             return true;
         };
         u32 sq = sq_level0;  // enqueued before the roots' outcome was read
+        // Launches enqueued beyond the one waited for, in level order: one (the next level, its
+        // frontier size read on the device), or two while the levels are small (the second CHAINED:
+        // its frontier's offset is read on the device too). A level the host has to read before the
+        // next is enqueued costs the host's turnaround (its publish seen, the launch issued: ~10-15
+        // us) whenever the level in flight is shorter than that, which small levels are.
+        std::deque<u32> ahead;
         vt0_ = Clock::now();
         for (;;) {
-            // enqueue the next level before waiting for this one
             const double g = std::max(ratio_, 1.0) * 1.5;
             const u64 est1 = (u64)((double)n * g) + 1024;     // the next frontier
-            const u64 est2 = (u64)((double)est1 * g) + 1024;  // the states it will claim
+            const u64 est2 = (u64)((double)est1 * g) + 1024;  // the states it will claim (= the frontier after)
+            const u64 est3 = (u64)((double)est2 * g) + 1024;  // ... and those that one will claim
             const u64 nb_next = lstart_.back();
-            const bool spec = !pessimistic_ && (double)(unique + est1 + est2) < lmax_ * (double)cap_ &&
-                              nb_next + est1 + est2 <= arena_cap_;
             // launch shape: a tight estimate (the grid strides over any excess)
             const u64 shape = (u64)((double)n * std::max(ratio_, 0.05) * 1.1) + 64;
-            u32 sq_next = spec ? launch_expand(nb_next, 0, true, shape, undiscovered) : 0;
-            if (!spec) publish_pending_slot();  // otherwise the enqueued level publishes this one
+            // enqueue the next level before waiting for this one
+            if (ahead.empty()) {
+                const bool spec = !pessimistic_ && (double)(unique + est1 + est2) < lmax_ * (double)cap_ &&
+                                  nb_next + est1 + est2 <= arena_cap_;
+                if (spec) ahead.push_back(launch_expand(nb_next, 0, true, shape, undiscovered));
+            }
+            // ... and the one after it while the next is small (a launch shorter than the host's turnaround)
+            if (ahead.size() == 1 && chain_max_ && est1 <= chain_max_ && !pessimistic_ &&
+                (double)(unique + est1 + est2 + est3) < lmax_ * (double)cap_ && nb_next + est1 + est2 + est3 <= arena_cap_) {
+                const u64 shape2 = (u64)((double)shape * std::max(ratio_, 0.05) * 1.1) + 64;
+                ahead.push_back(launch_expand(0, 0, true, shape2, undiscovered, 0, true));
+            }
+            if (ahead.empty()) publish_pending_slot();  // otherwise the enqueued level publishes this one
 
-            bool spec_ok = spec;
+            bool spec_ok = !ahead.empty();
             if (!wait_publish(sq, true)) {  // lc_ = this level's counters
                 if (lc_.err == ERR_DEFERRED) {
                     // a speculative launch whose frontier outgrew the room planned for it expanded
@@ -1076,8 +1094,14 @@ class Engine final : public EngineBase {
                 launch_probes[it->second] = lc_.probes;
                 launch_cas[it->second] = lc_.cas;
             }
-            if (!account(lc_, spec_ok ? " (next enqueued)" : "")) break;
-            sq = spec_ok ? sq_next : launch_sync(n, undiscovered);
+            if (!spec_ok) ahead.clear();  // (launches behind a failed level expanded nothing)
+            if (!account(lc_, ahead.size() == 2 ? " (next two enqueued)" : spec_ok ? " (next enqueued)" : "")) break;
+            if (!ahead.empty()) {
+                sq = ahead.front();
+                ahead.pop_front();
+            } else {
+                sq = launch_sync(n, undiscovered);
+            }
         }
         // A speculative level past the end may still be in flight: the host waits for it, but the
         // visited set's clear for the next check is enqueued behind it first (release_table), so
@@ -1157,8 +1181,11 @@ class Engine final : public EngineBase {
     // One expand_fast launch over a whole level whose frontier starts at arena offset `fbase`:
     // n states (dev_n = 0), or the previous level's claims read on the device (dev_n = 1, `shape`
     // is then an estimate used only for the launch shape; the grid strides over any excess).
-    u32 launch_expand(u64 fbase, u32 n, bool dev_n, u64 shape, u32 undiscovered, u32 flags = 0) {
+    // chained (dev_n only): enqueued two levels ahead, the frontier's arena offset is not known to
+    // the host either: the launch reads it, and the unique count, from the previous slot (SlotWork.chain).
+    u32 launch_expand(u64 fbase, u32 n, bool dev_n, u64 shape, u32 undiscovered, u32 flags = 0, bool chained = false) {
         const u32 sq = next_seq();
+        if (chained) fbase = 0;  // (read on the device)
         const u64 nbase = fbase + (dev_n ? 0 : n);  // start of the next level (dev_n: + n on the device)
         const u32 ncap = (u32)std::min<u64>(arena_cap_ - nbase, 0xffffffffu);
         const u32 ppw_log2 = ppw_env_ >= 0 ? (u32)ppw_env_ : ppw_for(shape);
@@ -1169,9 +1196,16 @@ class Engine final : public EngineBase {
         // a slotted launch: it counts into its own slot and is published by its successor
         SlotWork sw = slot_work(dev_n);
         sw.flags = flags;
+        sw.arena = arena_.p;
+        sw.apar = apar_.p;
+        sw.arena_cap = arena_cap_;
+        sw.fbase = fbase;
+        // unique states before the frontier (level 0 is launched before the roots' claims are read: 0)
+        const u64 u = unique.load();
+        sw.ubase = dev_n ? u : u >= n ? u - n : 0ull;
+        if (chained) sw.chain = slot(slot_k_ - 1);
         if (dev_n) {  // speculative: the device checks its frontier against the room left (ERR_DEFERRED)
-            const double room = lmax_ * (double)cap_ - (double)unique.load();
-            sw.room = room > 0 ? (u64)room : 0ull;
+            sw.room = (u64)(lmax_ * (double)cap_);  // (the device adds the unique states before the level)
             sw.gmul = (u32)std::min(64.0 * 256.0, std::ceil(std::max(recent_ratio(), 1.0) * 1.5 * 256.0));
         }
         LevelCounters* lc = slot(slot_k_);
@@ -1371,6 +1405,10 @@ class Engine final : public EngineBase {
     u32 grid_max_nopf_ = 0;  // ... of its wide no-prefetch form
     u32 grid_env_ = 0;       // SR_GRID_MAX
     int wide_nopf_ = -1;     // SR_WIDE_NOPF: -1 chosen per level (use_nopf), 0 never, 1 always
+    // The pipelined loop enqueues a second level ahead (chained) while the next frontier is
+    // estimated at <= this many states (SR_CHAIN_MAX; 0: never).
+    u64 chain_max_ = 16384;
+    int table_kind_ = 0;  // DevicePool memory kind of the visited set (SR_TABLE_KIND, measurement knob)
     // the no-prefetch form exists for wide states only (it is the prefetching kernel otherwise)
     template <class L>
     void launch_nopf(L& launch) {

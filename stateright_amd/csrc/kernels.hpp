@@ -214,6 +214,9 @@ struct LevelCounters {
     u32 prev_claims;       // claims of the last level (set by a resetting publish): the size of the
                            // frontier a pipelined launch expands, read on the device
     u32 prev_err;          // always 0 (the err word a launch reading prev_claims sees)
+    // Written by a slotted launch of the pipelined loop for a launch chained to it (SlotWork.chain):
+    u64 next_base;         // arena offset of the frontier this launch produces
+    u64 unique;            // unique states inserted before this launch's claims (its frontier included)
 };
 static_assert(offsetof(LevelCounters, err) == offsetof(LevelCounters, claims) + 4, "claims/err pair");
 static_assert(offsetof(LevelCounters, prev_err) == offsetof(LevelCounters, prev_claims) + 4, "prev pair");
@@ -401,8 +404,20 @@ struct SlotWork {
     // nn * (1 + g) exceeds that room, or nn * g the arena left after it, is not expanded (ERR_DEFERRED):
     // the host's plan assumed a smaller frontier, and overfilling a linear-probe table makes every
     // probe walk long runs (increment_lock's x5 levels: a 4 M-slot table at 0.78 load, then past it).
-    u64 room = 0;
+    u64 room = 0;  // (absolute: the growth threshold; the device adds the unique states before the level)
     u32 gmul = 0;  // 0: no check
+    // Slotted launches of the pipelined loop record their frontier's successor offset and the unique
+    // count in their slot (LevelCounters.next_base / .unique; arena != nullptr). `fbase` is this launch's
+    // frontier offset in the arena and `ubase` the unique states before that frontier, both known to
+    // the host, unless the launch is CHAINED: enqueued two levels ahead (the host has not read the
+    // level before it), it takes both from the previous slot `chain`, and its frontier, next frontier
+    // and arena room from `arena` / `apar` / `arena_cap`.
+    const LevelCounters* chain = nullptr;
+    u64* arena = nullptr;
+    u32* apar = nullptr;
+    u64 arena_cap = 0;
+    u64 fbase = 0;
+    u64 ubase = 0;
 };
 
 // One wave (lane = 0..63): publish sw.pub to sw.hc, then reset sw.zero.
@@ -781,7 +796,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W >
     // the two round trips overlap instead of following each other.
     const u64 r_first = lo + (u64)blockIdx.x * chunk + ((u64)wid << ppw_log2) + lane;
     u64 nxt[W];  // the wave's parents of its next chunk (here: its first)
-    const bool spec_first = sw.prev_n && lane < (int)ppw && r_first < next_cap;
+    const bool chained = sw.chain != nullptr;  // (its frontier's offset is read below)
+    const bool spec_first = sw.prev_n && !chained && lane < (int)ppw && r_first < next_cap;
     if (spec_first) load_state<W>(frontier, r_first, nxt);
     if (sw.prev_n) {
         // Pipelined launch (enqueued before the host saw the previous level finish): the frontier
@@ -789,11 +805,20 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W >
         // that failed (its err word, loaded with its claims) it expands nothing: the host repairs
         // or restarts that level and its frontier is not final.
         const u64 ce = __hip_atomic_load(reinterpret_cast<const u64*>(sw.prev_n), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        u64 fb = sw.fbase, ub = sw.ubase;
+        if (chained) {
+            fb = __hip_atomic_load(&sw.chain->next_base, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            ub = __hip_atomic_load(&sw.chain->unique, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            frontier = sw.arena + fb * W;
+            next = sw.arena + fb * W;
+            next_par = sw.apar + fb;
+            next_cap = (u32)min(sw.arena_cap > fb ? sw.arena_cap - fb : 0ull, 0xffffffffull);
+        }
         u32 nn = (ce >> 32) ? 0u : (u32)ce;
         if (sw.gmul && nn) {
             const u64 grow = ((u64)nn * sw.gmul) >> 8;
             const u64 left = next_cap > nn ? (u64)(next_cap - nn) : 0ull;
-            if ((u64)nn + grow > sw.room || grow > left) {
+            if (ub + nn + grow > sw.room || grow > left) {
                 nn = 0;
                 if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(&lc->err, (u32)ERR_DEFERRED);
             }
@@ -802,6 +827,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W >
         next += (u64)nn * W;
         next_par += nn;
         next_cap = next_cap > nn ? next_cap - nn : 0u;
+        if (sw.arena && blockIdx.x == 0 && threadIdx.x == 0) {  // for a launch chained to this one
+            lc->next_base = fb + nn;
+            lc->unique = ub + nn;
+        }
+    } else if (sw.arena && blockIdx.x == 0 && threadIdx.x == 0) {
+        lc->next_base = sw.fbase + (hi - lo);
+        lc->unique = sw.ubase + (hi - lo);
     }
     SR_TL(1);
     const u32 fmask = filt_log2 ? (1u << filt_log2) - 1 : 0;
