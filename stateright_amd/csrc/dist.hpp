@@ -1739,9 +1739,9 @@ class DistEngine final : public EngineBase {
             const u64 fb = hlstart_[level], nb = fb + n;
             const u32 ncap = (u32)std::min<u64>(cap_states - nb, 0xffffffffu);
             const u32 ppw_log2 = std::max<u32>(2, std::min<u32>(6, ppw_for(n)));
-            const u32 grid = std::max<u32>(1, blocks_for((n + (1u << ppw_log2) - 1) >> ppw_log2, 4));
+            const u32 grid = std::max<u32>(1, blocks_for((n + (1u << ppw_log2) - 1) >> ppw_log2, (u32)expand_wpb<M>()));
             p0.seq++;
-            expand_fast<M, 1, 0><<<grid, 256, filt_log2_ ? (8u << filt_log2_) : 0u, stream_>>>(
+            expand_fast<M, 1, 0><<<grid, 64 * expand_wpb<M>(), filt_log2_ ? (8u << filt_log2_) : 0u, stream_>>>(
                 m_, harena_.p + fb * W, 0u, (u32)n, hv, harena_.p + nb * W, hpar_.p + nb, ncap, p0.lc, und, p0.hc_dev, p0.seq,
                 1u, ppw_log2, filt_log2_, SlotWork{});
             SR_HIP(hipGetLastError());

@@ -299,6 +299,7 @@ int fingerprint_chain(const M& m, const std::vector<u64>& st, std::vector<u64>& 
 template <class M>
 class Engine final : public EngineBase {
     static constexpr int W = M::W;
+    static constexpr u32 WPB = (u32)expand_wpb<M>();  // expand_fast's waves per workgroup
 
   public:
     Engine(M m, const sr_opts& o)
@@ -1162,7 +1163,7 @@ class Engine final : public EngineBase {
         const void* k = probe_loop() < 0 ? (const void*)expand_fast<M, -4, 0> : (const void*)expand_fast<M, 1, 0>;
         if constexpr (W >= 4)
             if (nopf) k = (const void*)expand_fast<M, 1, 0, false, true>;
-        SR_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 256, dyn));
+        SR_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 64 * WPB, dyn));
         SR_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, o_.device));
         cap = per_cu > 0 && cus > 0 ? (u32)(2 * per_cu * cus) : ~0u;
         if (o_.verbose) std::fprintf(stderr, "[sr] expand grid cap %u blocks (%d per CU x %d CUs x 2)%s\n", cap, per_cu, cus, nopf ? " [no prefetch]" : "");
@@ -1189,7 +1190,7 @@ class Engine final : public EngineBase {
         const u64 nbase = fbase + (dev_n ? 0 : n);  // start of the next level (dev_n: + n on the device)
         const u32 ncap = (u32)std::min<u64>(arena_cap_ - nbase, 0xffffffffu);
         const u32 ppw_log2 = ppw_env_ >= 0 ? (u32)ppw_env_ : ppw_for(shape);
-        const u32 chunks = std::max<u32>(1, blocks_for((shape + (1u << ppw_log2) - 1) >> ppw_log2, 4));
+        const u32 chunks = std::max<u32>(1, blocks_for((shape + (1u << ppw_log2) - 1) >> ppw_log2, WPB));
         const bool nopf = use_nopf(chunks);
         const u32 grid = std::min(expand_grid_cap(nopf), chunks);
         seq_launch_[sq] = launch_frontier.size();
@@ -1212,7 +1213,7 @@ class Engine final : public EngineBase {
         const u32 svc = sw.pub || sw.zero ? 1u : 0u;  // the extra service workgroup (SlotWork)
         timed([&] {
             auto launch = [&](auto kern) {
-                kern<<<grid + svc, 256, filt_log2_ ? (8u << filt_log2_) : 0u, stream_>>>(
+                kern<<<grid + svc, 64 * WPB, filt_log2_ ? (8u << filt_log2_) : 0u, stream_>>>(
                     m_, arena_.p + fbase * W, 0u, n, view(), arena_.p + nbase * W, apar_.p + nbase, ncap, lc,
                     undiscovered, nullptr, sq, 0u, ppw_log2, filt_log2_, sw);
             };
@@ -1283,7 +1284,7 @@ class Engine final : public EngineBase {
                     u64* next = arena_.p + nbase * W;
                     u32* npar = apar_.p + nbase;
                     const u32 ppw_log2 = ppw_env_ >= 0 ? (u32)ppw_env_ : ppw_for(c);
-                    const u32 chunks = std::max<u32>(1, blocks_for((c + (1u << ppw_log2) - 1) >> ppw_log2, 4));
+                    const u32 chunks = std::max<u32>(1, blocks_for((c + (1u << ppw_log2) - 1) >> ppw_log2, WPB));
                     const bool nopf = use_nopf(chunks);
                     const u32 grid = std::min(expand_grid_cap(nopf), chunks);
                     SlotWork sw{};
@@ -1294,7 +1295,7 @@ class Engine final : public EngineBase {
                     }
                     timed([&] {
                         auto launch = [&](auto kern) {
-                            kern<<<grid, 256, filt_log2_ ? (8u << filt_log2_) : 0u, stream_>>>(
+                            kern<<<grid, 64 * WPB, filt_log2_ ? (8u << filt_log2_) : 0u, stream_>>>(
                                 m_, cur(), ulo, uhi, view(), next, npar, ncap, lc_d_, undiscovered, hcd(sq), sq,
                                 last ? 1u : 0u, ppw_log2, filt_log2_, sw);
                         };

@@ -40,6 +40,13 @@ constexpr int MAX_PARTS = 64;  // visited-set partitions (one per GPU, or virtua
 #ifndef SR_STAGE_WORDS
 #define SR_STAGE_WORDS 1024
 #endif
+// expand_fast's waves per workgroup for narrow states (W < 4): the block-local duplicate filter
+// is shared by the workgroup, so its reach is the parents of a whole chunk (waves x ppw).
+#ifndef SR_NARROW_WPB
+#define SR_NARROW_WPB 4
+#endif
+template <class M>
+constexpr int expand_wpb() { return M::W >= 4 ? 4 : SR_NARROW_WPB; }
 // ... and for wide states (W >= 4), whose blocks per CU are set by registers, not LDS.
 #ifndef SR_WIDE_STAGE_WORDS
 #define SR_WIDE_STAGE_WORDS 2048
@@ -722,20 +729,21 @@ __device__ u64* g_timeline;
 // Wide states (W >= 4: paxos, the actor models) run three waves per SIMD (<= 168 VGPRs): their
 // levels are latency-bound, and paxos' device-side history search had pushed them to two.
 template <class M, int PB, int POL, bool STATS = false, bool NOPF = false>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W >= 4 ? SR_WIDE_WAVES : PB < 0 ? 6 : 1))) expand_fast(M m, const u64* __restrict__ frontier, u32 lo, u32 hi,
+__global__ void __launch_bounds__(64 * expand_wpb<M>()) __attribute__((amdgpu_waves_per_eu(M::W >= 4 ? SR_WIDE_WAVES : PB < 0 ? 6 : 1))) expand_fast(M m, const u64* __restrict__ frontier, u32 lo, u32 hi,
                                                    TableView t, u64* __restrict__ next, u32* __restrict__ next_par,
                                                    u32 next_cap, LevelCounters* lc, u32 undiscovered,
                                                    HostCounters* hc, u32 seq, u32 reset, u32 ppw_log2,
                                                    u32 filt_log2, SlotWork sw) {
     constexpr int W = M::W, MW = M::MW;
-    constexpr int STAGE = (W >= 4 ? SR_WIDE_STAGE_WORDS : SR_STAGE_WORDS) / W;
+    constexpr int STAGE = (W >= 4 ? SR_WIDE_STAGE_WORDS : SR_STAGE_WORDS * expand_wpb<M>() / 4) / W;
     extern __shared__ u64 filt[];       // 2^filt_log2 fingerprints (dynamic LDS; 0 = no filter)
     __shared__ u64 stage[STAGE * W];
     __shared__ u32 stage_par[STAGE];
     // Parents per wave at most: wide states (paxos, W = 11) take few parents per wave (ppw_for), and
     // staging 64 of them cost 22.5 KB of LDS per block, which capped residency at 3 blocks per CU.
     constexpr u32 PPW_LOG2_MAX = W >= 4 ? SR_WIDE_PPW_LOG2_MAX : 6;
-    __shared__ u64 pst[4][(1 << PPW_LOG2_MAX) * W];     // parent states of each wave
+    constexpr int WPB = expand_wpb<M>();
+    __shared__ u64 pst[WPB][(1 << PPW_LOG2_MAX) * W];     // parent states of each wave
     // The wave's successor list, one u16 per successor: parent (bits 0-5) | action << 6, written by
     // the parent lanes (a ctz loop over their enabled masks) in windows of MAPCAP successors. A
     // successor lane reads its (parent, action) with one LDS load; the binary search over the
@@ -750,8 +758,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W >
 #endif
     constexpr u32 MAPCAP = W >= 4 ? SR_WIDE_MAPCAP : SR_MAPCAP;
     static_assert(MW * 64 <= 1024, "action ids must fit 10 bits");
-    __shared__ u16 smap[4][MAPCAP];
-    __shared__ u32 stage_n, base, scratch[8];
+    __shared__ u16 smap[WPB][MAPCAP];
+    __shared__ u32 stage_n, base, scratch[2 * WPB];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     if (threadIdx.x == 0) stage_n = 0;
     // The previous level's publish and the slot reset (SlotWork) run in one extra workgroup, the
