@@ -1,7 +1,7 @@
 #!/bin/bash
-# Waves per workgroup of expand_fast for narrow states (SR_NARROW_WPB: the LDS duplicate filter's reach is
-# the workgroup's chunk of waves x ppw parents) x the filter size (SR_FILTER_LOG2), 2pc N=9: ms per check
-# and visited-set probes per check (counting pass). cur = WPB 4.
+# Paxos: the cost of the per-state linearizability test (lib_nolin: -DSR_PX_NOLIN, the test skipped;
+# a measurement build, its discoveries are wrong) against the current library (the unpacked,
+# branch-free test); paxos/actor parity first.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 T=${1:-q}
@@ -10,11 +10,8 @@ mkdir -p $O
 export SR_LIB_DIGEST_CHECK=0
 LIB=stateright_amd/libstateright_gpu.so
 cp "$LIB" gpurun_ab/lib_cur.so || exit 1
-for v in wpb8 wpb16; do
-    cp gpurun_ab/lib_$v.so "$LIB" || exit 1
-    timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q -k "two_phase or 2pc or tp or config" --timeout 120 --timeout-method thread > $O/parity_$v.log 2>&1 || { tail -30 $O/parity_$v.log; cp gpurun_ab/lib_cur.so "$LIB"; exit 1; }
-    echo "$v $(tail -1 $O/parity_$v.log)"
-done
+timeout -k 10 500 python -u -m pytest tests/test_gpu_actor.py tests/test_gpu_parity.py tests/test_gpu_fingerprints.py -m gpu -x -q -k "paxos or actor or single or abd or ping or register or fingerprint" --timeout 120 --timeout-method thread > $O/parity.log 2>&1 || { tail -30 $O/parity.log; exit 1; }
+tail -1 $O/parity.log
 run() {  # label lib env -- bench args
     local label=$1 lib=$2; shift 2
     local envs=()
@@ -24,12 +21,10 @@ run() {  # label lib env -- bench args
     python3 -c "import json; d=json.loads(open('$O/$label.json').read().strip().splitlines()[-1]); l=d.get('levels') or {}; r=d['roofline']; print('$label', round(d['ms_per_step'],4), 'small', round(l.get('small_levels_ms',0),4), 'big', round(l.get('big_levels_ms',0),4), 'probes', round(r.get('probes_per_step',0)/1e6,2), 'M')"
 }
 for r in 1 2; do
-    run cur_f9_r$r cur SR_FILTER_LOG2=9 -- --steps 50 --warmup 3 || exit 1
-    run wpb8_f9_r$r wpb8 SR_FILTER_LOG2=9 -- --steps 50 --warmup 3 || exit 1
-    run wpb8_f10_r$r wpb8 SR_FILTER_LOG2=10 -- --steps 50 --warmup 3 || exit 1
-    run wpb8_f11_r$r wpb8 SR_FILTER_LOG2=11 -- --steps 50 --warmup 3 || exit 1
-    run wpb16_f11_r$r wpb16 SR_FILTER_LOG2=11 -- --steps 50 --warmup 3 || exit 1
-    run wpb16_f12_r$r wpb16 SR_FILTER_LOG2=12 -- --steps 50 --warmup 3 || exit 1
+    run px6_cur_r$r cur SR_X=0 -- --model paxos --clients 6 --steps 30 --warmup 2 || exit 1
+    run px6_nolin_r$r nolin SR_X=0 -- --model paxos --clients 6 --steps 30 --warmup 2 || exit 1
+    run px3_cur_r$r cur SR_X=0 -- --model paxos --clients 3 --steps 200 --warmup 5 || exit 1
+    run px3_nolin_r$r nolin SR_X=0 -- --model paxos --clients 3 --steps 200 --warmup 5 || exit 1
 done
 cp gpurun_ab/lib_cur.so "$LIB"
 echo "quick ab ok"

@@ -478,33 +478,49 @@ struct PaxosHistT {
     // factorially (a single-copy register with 4 clients: 4.6 ms for one history on a host core).
     // Checked against the search (`linearizable_search`) on every history of the paxos and
     // single-copy state spaces and on random histories (sr_selftest_models).
+    // The fields are unpacked once (phases, the returned values and every Get's `last` entries, each
+    // a contiguous run of the 128-bit field), and every loop runs its maximal trip count unrolled
+    // with the clients past C masked out: the per-client rows are independent chains the wave
+    // issues interleaved, and no branch depends on the history. The loop form was a dependent chain
+    // of ~1 000 instructions on every workgroup's last flush (2.4-3.6 us per level of paxos C=6, 11 %
+    // of its check: profiles/r05_paxos_lin.txt).
     SR_HD bool linearizable(u64 lo, u64 hi) const {
+        constexpr u32 MC = px::MAX_CLIENTS;
         const u32 C = NC();
+        const u32 phases = (u32)lo & ((1u << (2 * C)) - 1);  // 2 bits per client (2C <= 12)
+        const u32 rets = get(lo, hi, 2 * C, 3 * C);           // 3 bits per client (3C <= 18)
+        const u32 lb = 5 * C, lw = 2 * C * (C - 1);             // the `last` runs: lw <= 60 bits from bit lb <= 30
+        const u64 lasts = lw ? ((lo >> lb) | (hi << (64 - lb))) & ((1ull << lw) - 1) : 0ull;
         u64 in = 0;  // byte b: the clusters that must precede cluster b (bit a)
-        for (u32 t = 0; t < C; ++t) {
-            if (phase(lo, hi, t) != 2) continue;  // completed Reads only
-            const u32 r = ret(lo, hi, t);
-            auto edge = [&](u32 a) {
-                if (a != r) in |= 1ull << (8 * r + a);
-            };
-            edge(t + 1);
-            for (u32 u = 0; u < C; ++u) {
-                if (u == t) continue;
-                const u32 l = last(lo, hi, t, u);
-                if (l >= 1) edge(u + 1);
-                if (l >= 2) edge(ret(lo, hi, u));
+#pragma unroll
+        for (u32 t = 0; t < MC; ++t) {
+            const u32 r = rets >> (3 * t) & 7;
+            const u32 sh = 2 * (C - 1) * t;
+            const u64 lt = sh < 64 ? lasts >> sh : 0ull;  // t's `last` entries, ascending other client
+            u32 row = 1u << (t + 1);                       // t's own Write
+#pragma unroll
+            for (u32 k = 0; k + 1 < MC; ++k) {
+                const u32 u = k < t ? k : k + 1, l = (u32)(lt >> (2 * k)) & 3u;
+                const u32 e = (l >= 1 ? 1u << (u + 1) : 0u) | (l >= 2 ? 1u << (rets >> (3 * u) & 7) : 0u);
+                row |= k + 1 < C ? e : 0u;
             }
+            row &= ~(1u << r);  // (an op of the Read's own cluster is no constraint)
+            const bool read_done = t < C && (phases >> (2 * t) & 3u) == 2u;  // completed Reads only
+            in |= read_done ? (u64)(row & 0xffu) << (8 * r) : 0ull;
         }
-        if (in & 0xffull) return false;  // an op of a value cluster before a Read of the initial value
+        // An op of a value cluster before a Read of the initial value, or a cycle among the value
+        // clusters: each round removes the clusters nothing alive precedes, and C rounds empty an
+        // acyclic graph.
         u32 alive = ((1u << (C + 1)) - 1) & ~1u;
-        while (alive) {
+#pragma unroll
+        for (u32 round = 0; round < MC; ++round) {
             u32 rm = 0;
-            for (u32 b = 1; b <= C; ++b)
-                if ((alive >> b & 1) && !((u32)(in >> (8 * b)) & alive & 0xffu)) rm |= 1u << b;
-            if (!rm) return false;  // the clusters left form a cycle
+#pragma unroll
+            for (u32 b = 1; b <= MC; ++b)
+                rm |= (alive >> b & 1) && !((u32)(in >> (8 * b)) & alive & 0xffu) ? 1u << b : 0u;
             alive &= ~rm;
         }
-        return true;
+        return !(in & 0xffull) && alive == 0;
     }
     SR_HD bool linearizable_search(u64 lo, u64 hi) const {
         const u32 C = NC();
@@ -776,6 +792,9 @@ struct PaxosT {
 
     SR_HD bool discovers(int p, const u64* s) const {
         if (p == 0) {  // always "linearizable" (examples/paxos.rs:251-254): once per new state
+#ifdef SR_PX_NOLIN
+            return false;  // (measurement build only: the test's cost)
+#endif
             u64 lo, hi;
             hist_get(s, lo, hi);
             return !hs().linearizable(lo, hi);

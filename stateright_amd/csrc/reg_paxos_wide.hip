@@ -5,5 +5,10 @@
 #include "paxos.hpp"
 
 namespace sr {
-std::unique_ptr<EngineBase> reg_paxos_wide(const EngineArgs& a) { return make_for(PaxosWide::make((int)a.p[0]), a); }
+std::unique_ptr<EngineBase> reg_paxos_wide(const EngineArgs& a) {
+#ifdef SR_PX6_CC
+    if (a.p[0] == 6 && !std::getenv("SR_PAXOS_GENERIC")) return make_for(PaxosT<12, 6>::make(6), a);
+#endif
+    return make_for(PaxosWide::make((int)a.p[0]), a);
+}
 }  // namespace sr
