@@ -1,7 +1,5 @@
 #!/bin/bash
-# Paxos: the cost of the per-state linearizability test (lib_nolin: -DSR_PX_NOLIN, the test skipped;
-# a measurement build, its discoveries are wrong) against the current library (the unpacked,
-# branch-free test); paxos/actor parity first.
+# Paxos / single-copy register: actor/paxos parity, then ms per check of the current library.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 T=${1:-q}
@@ -22,9 +20,8 @@ run() {  # label lib env -- bench args
 }
 for r in 1 2; do
     run px6_cur_r$r cur SR_X=0 -- --model paxos --clients 6 --steps 30 --warmup 2 || exit 1
-    run px6_nolin_r$r nolin SR_X=0 -- --model paxos --clients 6 --steps 30 --warmup 2 || exit 1
     run px3_cur_r$r cur SR_X=0 -- --model paxos --clients 3 --steps 200 --warmup 5 || exit 1
-    run px3_nolin_r$r nolin SR_X=0 -- --model paxos --clients 3 --steps 200 --warmup 5 || exit 1
+    run sc4_cur_r$r cur SR_X=0 -- --model single_copy --clients 4 --steps 100 --warmup 5 || exit 1
 done
 cp gpurun_ab/lib_cur.so "$LIB"
 echo "quick ab ok"

@@ -726,8 +726,7 @@ struct SingleCopySys {
         u64 lo = o[1], hi = o[2];
         const u32 ph = h.phase(lo, hi, c);
         if (kind == PUTOK) {
-            for (u32 u = 0; u < C; ++u)
-                if (u != c) PaxosHist::put(lo, hi, h.last_off(c, u), 2, h.phase(lo, hi, u));
+            h.record_get(lo, hi, c);
         } else {
             PaxosHist::put(lo, hi, h.ret_off(c), 3, m & 7);
         }

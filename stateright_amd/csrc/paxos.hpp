@@ -454,6 +454,12 @@ struct PaxosHistT {
         }
     }
     SR_HD u32 phase(u64 lo, u64, u32 c) const { return (u32)(lo >> (2 * c)) & 3u; }  // 2C <= 12 bits
+    // record_invocations of client c's Get: its `last` entries = every other client's phase, in
+    // ascending id — the phase field without c's own two bits, stored with one put.
+    SR_HD void record_get(u64& lo, u64& hi, u32 c) const {
+        const u32 ph = (u32)lo & ((1u << (2 * NC())) - 1);
+        put(lo, hi, 5 * NC() + 2 * (NC() - 1) * c, 2 * (NC() - 1), (ph & ((1u << (2 * c)) - 1)) | (ph >> (2 * c + 2)) << (2 * c));
+    }
     SR_HD u32 ret(u64 lo, u64 hi, u32 c) const { return get(lo, hi, ret_off(c), 3); }
     // completed-op count of client u when client t invoked its Get
     SR_HD u32 last(u64 lo, u64 hi, u32 t, u32 u) const { return get(lo, hi, last_off(t, u), 2); }
@@ -754,8 +760,7 @@ struct PaxosT {
             if (ph == 0 && kind == px::PUTOK) {
                 // record_returns (WriteOk), then the Get is sent and recorded by record_invocations
                 out[nout++] = px::env(dst, (dst + 1) % 3, px::GET, 0, 0);  // request 2 * id
-                for (u32 u = 0; u < h.NC(); ++u)
-                    if (u != c) PaxosHist::put(lo, hi, h.last_off(c, u), 2, h.phase(lo, hi, u));
+                h.record_get(lo, hi, c);
             } else if (ph == 1 && kind == px::GETOK) {
                 PaxosHist::put(lo, hi, h.ret_off(c), 3, px::e_val(e));  // record_returns (ReadOk(v))
             } else {
