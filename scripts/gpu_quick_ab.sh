@@ -1,5 +1,6 @@
 #!/bin/bash
-# Paxos / single-copy register: actor/paxos parity, then ms per check of the current library.
+# Paxos / single-copy register: the wide-state fingerprint as one dependent chain of W mixes (cur) or W
+# independent mixes and one of their sum (lib_fps: -DSR_FP_SHALLOW), alternating.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 T=${1:-q}
@@ -18,10 +19,12 @@ run() {  # label lib env -- bench args
     env "${envs[@]}" timeout -k 10 200 python -u bench.py --cpu-baseline 0 --config4-steps 0 --no-hint-steps 0 "$@" > "$O/$label.json" 2> "$O/$label.err" || { tail -5 "$O/$label.err"; cp gpurun_ab/lib_cur.so "$LIB"; exit 1; }
     python3 -c "import json; d=json.loads(open('$O/$label.json').read().strip().splitlines()[-1]); l=d.get('levels') or {}; r=d['roofline']; print('$label', round(d['ms_per_step'],4), 'small', round(l.get('small_levels_ms',0),4), 'big', round(l.get('big_levels_ms',0),4), 'probes', round(r.get('probes_per_step',0)/1e6,2), 'M')"
 }
-for r in 1 2; do
-    run px6_cur_r$r cur SR_X=0 -- --model paxos --clients 6 --steps 30 --warmup 2 || exit 1
-    run px3_cur_r$r cur SR_X=0 -- --model paxos --clients 3 --steps 200 --warmup 5 || exit 1
-    run sc4_cur_r$r cur SR_X=0 -- --model single_copy --clients 4 --steps 100 --warmup 5 || exit 1
+for r in 1 2 3; do
+    for v in cur fps; do
+        run px6_${v}_r$r $v SR_X=0 -- --model paxos --clients 6 --steps 30 --warmup 2 || exit 1
+        run px3_${v}_r$r $v SR_X=0 -- --model paxos --clients 3 --steps 200 --warmup 5 || exit 1
+        run sc4_${v}_r$r $v SR_X=0 -- --model single_copy --clients 4 --steps 100 --warmup 5 || exit 1
+    done
 done
 cp gpurun_ab/lib_cur.so "$LIB"
 echo "quick ab ok"

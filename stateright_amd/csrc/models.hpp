@@ -160,9 +160,14 @@ SR_HD u64 fingerprint(const u64* s) {
     if constexpr (W == 1) {
         return fmix64(s[0] ^ 0x8000000000000000ull);
     } else {
-        u64 h = 0x9E3779B97F4A7C15ull;
+        // every word mixed on its own (position-keyed), then one mix of their sum: two mixes deep
+        // instead of a chain of W (a lone wave of a small paxos level waits on that chain: C=3
+        // 0.62 -> 0.61 ms, profiles/r05_paxos_lin.txt; round 4 had measured no gain, before the
+        // linearizability test's chain was cut)
+        u64 acc = 0;
 #pragma unroll
-        for (int i = 0; i < W; ++i) h = fmix64(h ^ (s[i] + 0x632BE59BD9B4E019ull * (u64)(i + 1)));
+        for (int i = 0; i < W; ++i) acc += fmix64(s[i] ^ (0x632BE59BD9B4E019ull * (u64)(i + 1)));
+        const u64 h = fmix64(acc ^ 0x9E3779B97F4A7C15ull);
         return h ? h : 1;
     }
 }
