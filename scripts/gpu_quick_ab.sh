@@ -1,30 +1,23 @@
 #!/bin/bash
-# Paxos / single-copy register: the wide-state fingerprint as one dependent chain of W mixes (cur) or W
-# independent mixes and one of their sum (lib_fps: -DSR_FP_SHALLOW), alternating.
+# The visited set in ordinary (SR_TABLE_KIND=0) or uncached (2) device memory for big tables: 2pc N=10 / N=11
+# and increment_lock N=11 (quotient table, CAS-bound), alternating.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 T=${1:-q}
 O=gpurun_out/$T
 mkdir -p $O
-export SR_LIB_DIGEST_CHECK=0
-LIB=stateright_amd/libstateright_gpu.so
-cp "$LIB" gpurun_ab/lib_cur.so || exit 1
-timeout -k 10 500 python -u -m pytest tests/test_gpu_actor.py tests/test_gpu_parity.py tests/test_gpu_fingerprints.py -m gpu -x -q -k "paxos or actor or single or abd or ping or register or fingerprint" --timeout 120 --timeout-method thread > $O/parity.log 2>&1 || { tail -30 $O/parity.log; exit 1; }
-tail -1 $O/parity.log
-run() {  # label lib env -- bench args
-    local label=$1 lib=$2; shift 2
+run() {  # label env -- bench args
+    local label=$1; shift
     local envs=()
     while [ "$1" != "--" ]; do envs+=("$1"); shift; done; shift
-    cp "gpurun_ab/lib_$lib.so" "$LIB" || exit 1
-    env "${envs[@]}" timeout -k 10 200 python -u bench.py --cpu-baseline 0 --config4-steps 0 --no-hint-steps 0 "$@" > "$O/$label.json" 2> "$O/$label.err" || { tail -5 "$O/$label.err"; cp gpurun_ab/lib_cur.so "$LIB"; exit 1; }
-    python3 -c "import json; d=json.loads(open('$O/$label.json').read().strip().splitlines()[-1]); l=d.get('levels') or {}; r=d['roofline']; print('$label', round(d['ms_per_step'],4), 'small', round(l.get('small_levels_ms',0),4), 'big', round(l.get('big_levels_ms',0),4), 'probes', round(r.get('probes_per_step',0)/1e6,2), 'M')"
+    env "${envs[@]}" timeout -k 10 200 python -u bench.py --cpu-baseline 0 --config4-steps 0 --no-hint-steps 0 "$@" > "$O/$label.json" 2> "$O/$label.err" || { tail -5 "$O/$label.err"; exit 1; }
+    python3 -c "import json; d=json.loads(open('$O/$label.json').read().strip().splitlines()[-1]); l=d.get('levels') or {}; print('$label', round(d['ms_per_step'],4), 'small', round(l.get('small_levels_ms',0),4), 'big', round(l.get('big_levels_ms',0),4))"
 }
-for r in 1 2 3; do
-    for v in cur fps; do
-        run px6_${v}_r$r $v SR_X=0 -- --model paxos --clients 6 --steps 30 --warmup 2 || exit 1
-        run px3_${v}_r$r $v SR_X=0 -- --model paxos --clients 3 --steps 200 --warmup 5 || exit 1
-        run sc4_${v}_r$r $v SR_X=0 -- --model single_copy --clients 4 --steps 100 --warmup 5 || exit 1
+for r in 1 2; do
+    for k in 0 2; do
+        run tp10_k${k}_r$r SR_TABLE_KIND=$k -- --rm-count 10 --steps 5 --warmup 1 || exit 1
+        run tp11_k${k}_r$r SR_TABLE_KIND=$k -- --rm-count 11 --steps 2 --warmup 1 || exit 1
+        run il11_k${k}_r$r SR_TABLE_KIND=$k -- --model increment_lock --threads 11 --steps 3 --warmup 1 || exit 1
     done
 done
-cp gpurun_ab/lib_cur.so "$LIB"
 echo "quick ab ok"
