@@ -6,6 +6,9 @@ import collections
 import csv
 import glob
 import sys
+import os
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from kname import is_timed_expand  # noqa: E402
 
 O = sys.argv[1]
 CUS = 256
@@ -19,7 +22,7 @@ def load(n, p):
     if not files:
         return per, dur
     for r in csv.DictReader(open(files[0])):
-        if "expand_fast" not in r["Kernel_Name"] or "true>" in r["Kernel_Name"]:
+        if not is_timed_expand(r["Kernel_Name"]):
             continue
         per[r["Dispatch_Id"]][r["Counter_Name"]] = float(r["Counter_Value"])
         dur[r["Dispatch_Id"]] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])

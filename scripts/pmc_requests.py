@@ -12,6 +12,8 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from stateright_amd.build import source_digest  # noqa: E402
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from kname import is_timed_expand  # noqa: E402
 
 LABELS = {"2pc9": "2pc N=9", "2pc10": "2pc N=10", "2pc11": "2pc N=11", "inclock10": "increment_lock N=10",
           "inclock11": "increment_lock N=11", "paxos3": "paxos C=3"}
@@ -31,7 +33,7 @@ def dispatches(d, want=None):
 
 
 def expand(name):  # the timed expand kernel (not the counting instantiation, STATS = true)
-    return "expand_fast<" in name and "true>" not in name
+    return is_timed_expand(name)
 
 
 def main(o):

@@ -11,13 +11,15 @@ for n in 9 11; do
 done
 python3 - $O <<'PY'
 import csv, glob, sys, collections
+sys.path.insert(0, 'scripts')
+from kname import is_timed_expand
 O = sys.argv[1]
 for n in (9, 11):
     (f,) = glob.glob(f"{O}/n{n}/*counter_collection.csv")
     per = collections.defaultdict(dict)
     dur = {}
     for r in csv.DictReader(open(f)):
-        if "expand_fast" not in r["Kernel_Name"] or "true>" in r["Kernel_Name"]:
+        if not is_timed_expand(r["Kernel_Name"]):
             continue
         per[r["Dispatch_Id"]][r["Counter_Name"]] = float(r["Counter_Value"])
         dur[r["Dispatch_Id"]] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])

@@ -12,12 +12,14 @@ mkdir -p $O
 timeout -s KILL 180 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM --kernel-trace --output-format csv -d $O/p3 -o p -- python3 bench.py --model paxos --clients $C --steps 3 --warmup 1 --cpu-baseline 0 --config4-steps 0 --no-hint-steps 0 > $O/p3.log 2>&1 || { echo "pmc failed"; tail -3 $O/p3.log; exit 1; }
 python3 - $O $C $LPC $SPC <<'PY'
 import csv, glob, sys, collections
+sys.path.insert(0, 'scripts')
+from kname import is_timed_expand
 O, C, LPC, SPC = sys.argv[1], int(sys.argv[2]), float(sys.argv[3]), float(sys.argv[4])
 (f,) = glob.glob(f"{O}/p3/*counter_collection.csv")
 per = collections.defaultdict(dict)
 dur = {}
 for r in csv.DictReader(open(f)):
-    if "expand_fast" not in r["Kernel_Name"] or "true>" in r["Kernel_Name"]:
+    if not is_timed_expand(r["Kernel_Name"]):
         continue
     per[r["Dispatch_Id"]][r["Counter_Name"]] = float(r["Counter_Value"])
     dur[r["Dispatch_Id"]] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])

@@ -5,6 +5,9 @@ import collections
 import csv
 import glob
 import sys
+import os
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from kname import is_timed_expand  # noqa: E402
 
 O, ENVS = sys.argv[1], sys.argv[2:]
 CUS = 256
@@ -15,7 +18,7 @@ def big(i, p):
     per, dur = collections.defaultdict(dict), {}
     for f in files:
         for r in csv.DictReader(open(f)):
-            if "expand_fast" not in r["Kernel_Name"] or "true>" in r["Kernel_Name"]:
+            if not is_timed_expand(r["Kernel_Name"]):
                 continue
             per[r["Dispatch_Id"]][r["Counter_Name"]] = float(r["Counter_Value"])
             dur[r["Dispatch_Id"]] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
