@@ -1143,8 +1143,15 @@ class Engine final : public EngineBase {
     u32 launch_sync(u64 n, u32 undiscovered) {
         const u64 d_eff = pessimistic_ ? D_ : std::min<u64>(D_, (u64)std::ceil(2.0 * recent_ratio() + 1.0));
         const double need = (double)(unique + n * d_eff);
-        if (need > lmax_ * (double)cap_) grow_table(nullptr, 0, growth_slots((u64)(need / lmax_) + 1));
         const u64 fbase = lstart_[lstart_.size() - 2];
+        if (need > lmax_ * (double)cap_) {
+            grow_table(nullptr, 0, growth_slots((u64)(need / lmax_) + 1));
+            // The arena takes its next step (x4) with the table: a table that had to grow holds nearly
+            // as many states as the arena (both start at 2^22), and the arena's own step, a copy and
+            // a second stop of the level pipeline, would follow a level later (2pc N=9 without a
+            // hint: levels 9 and 10).
+            if ((double)arena_cap_ < lmax_ * (double)cap_) ensure_arena(arena_cap_ + 1, fbase + n);
+        }
         ensure_arena(fbase + n + n * d_eff, fbase + n);
         return launch_expand(fbase, (u32)n, false, n, undiscovered);
     }
