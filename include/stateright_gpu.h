@@ -58,7 +58,7 @@ enum sr_model_id {
     SR_MODEL_DGRAPH = 6,          /* (expectation, len, v.., len, v..) src/test_util.rs:47-116 */
     SR_MODEL_PAXOS = 7,           /* (client_count<=6) examples/paxos.rs:93-263 + src/actor/model.rs */
     /* ActorModel fixtures (src/actor/model.rs:176-327 over stateright_amd/csrc/actor.hpp): */
-    SR_MODEL_PINGPONG = 9,        /* (max_nat<=7, lossy, duplicating, maintains_history)
+    SR_MODEL_PINGPONG = 9,        /* (max_nat<=14, lossy, duplicating, maintains_history)
                                      src/actor/actor_test_util.rs:4-96                     */
     SR_MODEL_ACTOR_FIXTURE = 10,  /* (kind: 0 undeliverable envelope, 1 timer) src/actor/model.rs:697-733 */
     SR_MODEL_ABD = 11,            /* (client_count<=3, server_count<=3) examples/linearizable-register.rs */

@@ -2,7 +2,7 @@
 // actor system's state and transition rules, `ActorGpu<Sys>`, over a system description Sys (the
 // actors' `on_start` / `on_msg` / `on_timeout`, the history's `record_msg_in` / `record_msg_out`,
 // the boundary and the properties), with the reference's actor fixtures on top:
-//   PingPongSys   ping-pong (src/actor/actor_test_util.rs:4-96), lossy / duplicating options
+//   PingPongSysT  ping-pong (src/actor/actor_test_util.rs:4-96), lossy / duplicating options
 //   FixtureSys    the undeliverable-message and timer fixtures (src/actor/model.rs:697-733)
 //   AbdSys        the ABD linearizable register (examples/linearizable-register.rs)
 //   SingleCopySys the single-copy register (examples/single-copy-register.rs)
@@ -247,9 +247,14 @@ struct ActorGpu : Sys {
 // ---------------------------------------------------------------------------------------------
 // Ping-pong (src/actor/actor_test_util.rs:4-96). Word 0: actor counts (4 bits each), history
 // (#in, #out) 8 bits each. Message: pong << 8 | value (the oracle's key order (pong, value)).
+// The duplicating network keeps every Ping(v) and Pong(v) ever sent, 2 * (max_nat + 1) envelopes
+// within the boundary: KK = 16 slots hold max_nat <= 7, KK = 32 slots (17-word states) max_nat
+// <= 14 (a count reaches max_nat + 1 <= 15 in its 4 bits before the boundary drops the state).
 // ---------------------------------------------------------------------------------------------
-struct PingPongSys {
-    static constexpr int K = 16, AW = 1, NACT = 2, NPROPS = 6, NET = 16;
+template <int KK>
+struct PingPongSysT {
+    static constexpr int K = KK, AW = 1, NACT = 2, NPROPS = 6, NET = KK;
+    static constexpr u32 MAX_NAT = KK / 2 - 1 < 14 ? KK / 2 - 1 : 14;
     u32 max_nat = 1;
     bool lossy = false, duplicating = true, maintains_history = false;
     SR_HD u32 nact() const { return 2; }
@@ -784,7 +789,8 @@ struct SingleCopySys {
 
 }  // namespace act
 
-using PingPong = act::ActorGpu<act::PingPongSys>;
+using PingPong = act::ActorGpu<act::PingPongSysT<16>>;      // max_nat <= 7
+using PingPongWide = act::ActorGpu<act::PingPongSysT<32>>;  // max_nat 8..=14
 using ActorFixture = act::ActorGpu<act::FixtureSys>;
 using AbdRegister = act::ActorGpu<act::AbdSys>;
 using SingleCopyRegister = act::ActorGpu<act::SingleCopySys>;

@@ -310,12 +310,20 @@ static int with_host_model(int model, const i64* p, int np, F&& f) {
             return p[0] <= Paxos::max_clients() ? f(Paxos::make((int)p[0])) : f(PaxosWide::make((int)p[0]));
         case SR_MODEL_PINGPONG: {
             need(1);
-            if (p[0] < 0 || p[0] > 7) throw Error(SR_ERR_UNSUPPORTED, "ping-pong: max_nat must be in 0..=7");
-            PingPong m;
-            m.max_nat = (u32)p[0];
-            m.lossy = np > 1 && p[1] != 0;
-            m.duplicating = np > 2 ? p[2] != 0 : true;
-            m.maintains_history = np > 3 && p[3] != 0;
+            if (p[0] < 0 || p[0] > (i64)PingPongWide::MAX_NAT) throw Error(SR_ERR_UNSUPPORTED, "ping-pong: max_nat must be in 0..=14");
+            auto fill = [&](auto& m) {
+                m.max_nat = (u32)p[0];
+                m.lossy = np > 1 && p[1] != 0;
+                m.duplicating = np > 2 ? p[2] != 0 : true;
+                m.maintains_history = np > 3 && p[3] != 0;
+            };
+            if (p[0] <= (i64)PingPong::MAX_NAT) {
+                PingPong m;
+                fill(m);
+                return f(m);
+            }
+            PingPongWide m;
+            fill(m);
             return f(m);
         }
         case SR_MODEL_ACTOR_FIXTURE: {

@@ -150,7 +150,8 @@ class PingPong(_Model):
     .into_model()` (src/actor/actor_test_util.rs:4-96) with `.lossy_network(..)` and
     `.duplicating_network(..)` (src/actor/model.rs:52-66; the reference defaults to a lossless
     duplicating network). Action ids: Deliver = envelope code * 4 + 1, Drop = code * 4 + 2
-    (stateright_amd/csrc/actor.hpp)."""
+    (stateright_amd/csrc/actor.hpp). `max_nat` <= 7 runs on a 16-slot network encoding, 8..=14 on a
+    32-slot one (its states describe 32 envelopes instead of 16)."""
     MODEL_ID = N.SR_MODEL_PINGPONG
 
     def __init__(self, max_nat, maintains_history=False, lossy=False, duplicating=True):

@@ -24,6 +24,8 @@ CASES = [
     (N.SR_MODEL_SINGLE_COPY, [4, 1], 400233),     # bench.sh's `check 4`
     (N.SR_MODEL_PINGPONG, [5], None),
     (N.SR_MODEL_PINGPONG, [3, 1, 0, 1], None),
+    (N.SR_MODEL_PINGPONG, [9, 1], None),          # 32-slot encoding: first 200 000 of 1 048 574
+    (N.SR_MODEL_PINGPONG, [14, 0, 1, 1], 29),    # 32-slot encoding, max_nat 14
     (N.SR_MODEL_ACTOR_FIXTURE, [0], 1),
     (N.SR_MODEL_ACTOR_FIXTURE, [1], 2),
     (N.SR_MODEL_2PC, [5], 8832),                  # examples/2pc.rs:127-134

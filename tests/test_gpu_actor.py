@@ -37,6 +37,11 @@ CASES = [
     (PINGPONG, pingpong_params(2, lossy=False, duplicating=False, maintains_history=True)),
     (PINGPONG, pingpong_params(3, lossy=True, duplicating=False, maintains_history=True)),
     (PINGPONG, pingpong_params(7, lossy=True)),
+    # max_nat >= 8: the 32-slot encoding (17-word states, stateright_amd/csrc/actor.hpp PingPongSysT)
+    (PINGPONG, pingpong_params(8, lossy=True)),
+    (PINGPONG, pingpong_params(10, lossy=True, duplicating=False, maintains_history=True)),
+    (PINGPONG, pingpong_params(12, lossy=True, duplicating=False)),
+    (PINGPONG, pingpong_params(14, lossy=False, maintains_history=True)),
     (ACTOR_FIXTURE, [0]),
     (ACTOR_FIXTURE, [1]),
     (ABD, [1, 2]),
@@ -78,7 +83,12 @@ def test_counts_match_oracle(case, order):
     assert c.is_done() == o.is_done
 
 
-@pytest.mark.parametrize("case", CASES + EARLY_EXIT, ids=ids)
+# the oracle's description holds 16 envelopes (oracle/actor.hpp PingPongSys::NET): visits and paths
+# are compared for the 16-slot encoding; the 32-slot one describes 32 envelopes
+NARROW = [c for c in CASES if not (c[0] == PINGPONG and c[1][0] > 7)]
+
+
+@pytest.mark.parametrize("case", NARROW + EARLY_EXIT, ids=ids)
 def test_fifo_visits_and_paths_identical(case):
     mid, params = case
     o = oracle(mid, params, record_visits=True)
@@ -145,6 +155,21 @@ def test_pingpong_lossy_duplicating():
     c.assert_no_discovery("delta within 1")
     c.assert_discovery("must reach max", PINGPONG_DROP_FIRST_PING)
     assert c.action_name(PINGPONG_DROP_FIRST_PING[0]) == "Drop(Envelope { src: Id(0), dst: Id(1), msg: Ping(0) })"
+
+
+@pytest.mark.parametrize("max_nat", [9, 10, 11])
+def test_pingpong_lossy_duplicating_closed_form(max_nat):
+    # the lossy duplicating network past the 16-slot encoding: every subset of the 2 (n + 1) envelopes
+    # sent with the counts they imply, 4^(n+1) - 2 states (the oracle's 65 534 / 262 142 / 1 048 574
+    # at n = 7 / 8 / 9), (4n + 1) 4^n + 1 generated, depth 4n + 1; 4 094 at n = 5 is the reference's
+    # golden (src/actor/model.rs:612-642)
+    n = max_nat
+    c = sr.PingPong(n).lossy_network().checker().spawn_bfs().join()
+    assert (c.unique_state_count(), c.state_count(), c.max_depth()) == (4 ** (n + 1) - 2, (4 * n + 1) * 4 ** n + 1,
+                                                                         4 * n + 1)
+    c.assert_no_discovery("delta within 1")
+    c.assert_discovery("must reach max", PINGPONG_DROP_FIRST_PING)
+    assert c.discovery("can reach max").last_state()[:2] in ((n - 1, n), (n, n))
 
 
 def test_pingpong_perfect_delivery():
