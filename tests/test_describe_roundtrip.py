@@ -24,7 +24,9 @@ CASES = [
     (N.SR_MODEL_SINGLE_COPY, [4, 1], 400233),     # bench.sh's `check 4`
     (N.SR_MODEL_PINGPONG, [5], None),
     (N.SR_MODEL_PINGPONG, [3, 1, 0, 1], None),
-    (N.SR_MODEL_PINGPONG, [9, 1], None),          # 32-slot encoding: first 200 000 of 1 048 574
+    (N.SR_MODEL_PINGPONG, [8, 1], 262142),        # 32-slot encoding: the oracle's count (4^9 - 2)
+    (N.SR_MODEL_PINGPONG, [9, 1], 1048574),       # 32-slot encoding: 4^10 - 2
+    (N.SR_MODEL_PINGPONG, [10, 1, 0, 1], 42),     # 32-slot encoding: the oracle's count
     (N.SR_MODEL_PINGPONG, [14, 0, 1, 1], 29),    # 32-slot encoding, max_nat 14
     (N.SR_MODEL_ACTOR_FIXTURE, [0], 1),
     (N.SR_MODEL_ACTOR_FIXTURE, [1], 2),
@@ -38,7 +40,7 @@ CASES = [
 def test_describe_roundtrip(model, params, want):
     lib = N.load()
     p = (ctypes.c_int64 * len(params))(*params)
-    cap = max(200000, want or 0)
+    cap = max(200000, (want or 0) + 1)  # one past the count: the walk ended by itself
     n = lib.sr_selftest_describe(model, p, len(params), cap)
     assert n > 0, N.last_error()
     if want is not None:
