@@ -962,6 +962,7 @@ class DistEngine final : public EngineBase {
         u64 uniq = 0;                    // states claimed in this partition's visited set
         const M* model = nullptr;
         TableView view() const { return make_table_view(*model, keys.p, nullptr, cap); }
+        u64 words() const { return table_words(view(), cap); }  // u64 words of the table
     };
 
   public:
@@ -986,9 +987,9 @@ class DistEngine final : public EngineBase {
             parts_[i].id = comm_ ? (u32)comm_->rank : i;
             parts_[i].model = &m_;
         }
-        if (make_table_view(m_, nullptr, nullptr, min_table_cap(m_)).qbits) {
-            // exact quotient-mode tables: the LDS filter and the sent cache compare fingerprints,
-            // which are not exact for multi-word states
+        if (!filter_exact(m_)) {
+            // exact multi-word quotient-mode tables: the LDS filter and the sent cache compare
+            // fingerprints, which are not exact for multi-word states
             filt_log2_ = 0;
             send_cache_max_parts_ = 0;
         }
@@ -1367,8 +1368,8 @@ class DistEngine final : public EngineBase {
         ok.swap(p.keys);
         const u64 old_cap = p.cap;
         p.cap *= 2;
-        p.keys.alloc(o_.device, p.cap);
-        SR_HIP(hipMemsetAsync(p.keys.p, 0, p.cap * 8, stream_));
+        p.keys.alloc(o_.device, p.words());
+        SR_HIP(hipMemsetAsync(p.keys.p, 0, p.words() * 8, stream_));
         rehash<<<blocks_for(old_cap, 256), 256, 0, stream_>>>(make_table_view(m_, ok.p, nullptr, old_cap), old_cap, p.view(), &p.lc->err);
         SR_HIP(hipGetLastError());
         SR_HIP(stream_sync(stream_));
@@ -1426,8 +1427,8 @@ class DistEngine final : public EngineBase {
             while ((double)cap * std::min(0.5, lmax(cap)) < (double)per_part * grow_factor_) cap <<= 1;
             p.uniq = 0;
             p.cap = cap;
-            p.keys.alloc(o_.device, cap);
-            SR_HIP(hipMemsetAsync(p.keys.p, 0, cap * 8, stream_));
+            p.keys.alloc(o_.device, p.words());
+            SR_HIP(hipMemsetAsync(p.keys.p, 0, p.words() * 8, stream_));
             p.arena_cap = 0;
             p.last = HostCounters{};
             p.lstart.assign(1, 0);
@@ -1691,12 +1692,13 @@ class DistEngine final : public EngineBase {
         const u64 cap_states = head_max_ * (u64)(D_ + 4) * 2 + 4096;
         u64 hcap = std::max<u64>(1u << 12, min_table_cap(m_));
         while ((double)hcap * std::min(0.5, lmax(hcap)) < (double)cap_states) hcap <<= 1;
-        if (hkeys_.n < hcap) hkeys_.alloc(o_.device, hcap);
+        const u64 hwords = table_words(make_table_view(m_, nullptr, nullptr, hcap), hcap);
+        if (hkeys_.n < hwords) hkeys_.alloc(o_.device, hwords);
         if (harena_.n < cap_states * W) {
             harena_.alloc(o_.device, cap_states * W);
             hpar_.alloc(o_.device, cap_states);
         }
-        SR_HIP(hipMemsetAsync(hkeys_.p, 0, hcap * 8, stream_));
+        SR_HIP(hipMemsetAsync(hkeys_.p, 0, hwords * 8, stream_));
         const TableView hv = make_table_view(m_, hkeys_.p, nullptr, hcap);
         hlstart_.assign(1, 0);
         SR_HIP(hipMemcpyAsync(harena_.p, rev.data(), rev.size() * 8, hipMemcpyHostToDevice, stream_));
@@ -2453,8 +2455,8 @@ class DistEngine final : public EngineBase {
     using RouteKernel = decltype(&expand_route<M, 1, false>);
     RouteKernel route_kernel(const Part& p) const {
         if (self_rec()) return expand_route<M, 1, true>;
-        constexpr bool fp_only = !(has_qkey<M>::value && M::W >= 2);
-        if constexpr (fp_only && W < 4) {
+        constexpr bool queue_ok = W == 1 || !has_qkey<M>::value;  // not multi-word quotient tables
+        if constexpr (queue_ok && W < 4) {
             const bool big = p.view().mask + 1 >= (1ull << 27);
             if (!p.sent_mask && (route_queue_env_ < 0 ? big : route_queue_env_ > 0)) return expand_route<M, -4, false>;
         }

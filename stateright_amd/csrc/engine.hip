@@ -779,6 +779,44 @@ int32_t sr_selftest_tables(void) {
             seen[y] = 1;
         }
     }
+    // qmix (one-word keys) is a bijection on B bits
+    for (u32 B = 2; B <= 20; ++B) {
+        std::vector<u8> seen(1u << B, 0);
+        for (u64 x = 0; x < (1ull << B); ++x) {
+            const u64 y = qmix(x, B);
+            if (y >> B || seen[y]) {
+                set_error("qmix is not a bijection on " + std::to_string(B) + " bits");
+                return SR_ERR_ARG;
+            }
+            seen[y] = 1;
+        }
+    }
+    // narrow (32-bit) quotient slots: 2pc N=9..12 keys in their tables, and a table larger than
+    // the key space (remainder 1 bit); the filter key gives the permuted key back
+    const u32 ncases[][2] = {{40, 25}, {40, 22}, {44, 27}, {48, 29}, {52, 31}, {16, 22}, {62, 40}};
+    u64 rn = 0x452821E638D01377ull;
+    for (auto& c : ncases) {
+        const u32 q = c[0] > c[1] ? c[0] - c[1] : 1u;
+        TableView t{nullptr, nullptr, (1ull << c[1]) - 1, q, 32 - q, c[0]};
+        t.s32 = 1;
+        if (q + SLOT32_DMIN > 32) {
+            t.s32 = 0;
+            t.dbits = 64 - q;
+        }
+        for (int i = 0; i < 100000; ++i) {
+            rn = fmix64(rn + 0x9E3779B97F4A7C15ull);
+            const u64 key = rn & ((1ull << c[0]) - 1);
+            const u64 h = qmix(key, c[0]);
+            const ProbeKey pk = quot_probe(t, h);
+            const u64 d = (rn >> 40) % 500;
+            const u64 slotv = pk.tag + d;
+            if ((t.s32 && slotv >> 32) || quot_decode(t, (pk.home + d) & t.mask, slotv) != h || pk.home > t.mask ||
+                filter_key(t, pk) != h + 1) {
+                set_error("narrow quotient slot encode/decode mismatch at B=" + std::to_string(c[0]));
+                return SR_ERR_ARG;
+            }
+        }
+    }
     // quotient slot values decode to the key at every displacement (B = 89, k = 33: increment_lock
     // N=12's table; B = 68, k = 20)
     const u32 cases[][2] = {{89, 33}, {68, 20}, {82, 26}, {120, 64}};

@@ -312,9 +312,9 @@ class Engine final : public EngineBase {
         if (const char* e = std::getenv("SR_TABLE_LOAD")) table_load_ = std::atof(e), load_env_ = true;
         if (const char* e = std::getenv("SR_PPW_LOG2")) ppw_env_ = std::atoi(e);
         if (const char* e = std::getenv("SR_FILTER_LOG2")) filt_log2_ = (u32)std::atoi(e);
-        // The LDS duplicate filter compares fingerprints: exact only in fingerprint mode (one-word
-        // states); an exact quotient-mode table (multi-word states with a key) runs without it.
-        if (make_table_view(m_, nullptr, nullptr, min_table_cap(m_)).qbits) filt_log2_ = 0;
+        // The LDS duplicate filter must be injective on states (kernels.hpp filter_key): one-word
+        // states in either mode; a multi-word quotient-mode table runs without it.
+        if (!filter_exact(m_)) filt_log2_ = 0;
         if (const char* e = std::getenv("SR_PIPELINE")) pipeline_ = std::atoi(e) != 0;
         if (const char* e = std::getenv("SR_QUERY_LOG2")) query_mask_ = (1ull << std::atoi(e)) - 1;
         if (const char* e = std::getenv("SR_GRID_MAX")) grid_env_ = (u32)std::max(0, std::atoi(e));  // <= 0: unset
@@ -488,7 +488,7 @@ class Engine final : public EngineBase {
     void alloc_table(u64 cap) {
         cap_ = cap;
         lmax_ = max_load(cap);
-        keys_.alloc_zero(o_.device, cap, stream_, table_kind_);
+        keys_.alloc_zero(o_.device, table_words(make_table_view(m_, nullptr, nullptr, cap), cap), stream_, table_kind_);
         if (fifo_) {
             meta_.alloc(o_.device, cap);
             SR_HIP(hipMemsetAsync(meta_.p, 0xff, cap * sizeof(u64), stream_));
@@ -1404,8 +1404,8 @@ class Engine final : public EngineBase {
     // N=9 (2^25 slots) +6 % (profiles/r05_probe_loops.txt). Fingerprint-mode narrow states only.
     int probe_loop() const {
         if (probe_batch_) return probe_batch_ < 0 ? -4 : 1;
-        constexpr bool fp_only = !(has_qkey<M>::value && M::W >= 2);
-        return fp_only && W < 4 && cap_ >= (1ull << 27) ? -4 : 1;
+        constexpr bool queue_ok = W == 1 || !has_qkey<M>::value;  // not multi-word quotient tables
+        return queue_ok && W < 4 && cap_ >= (1ull << 27) ? -4 : 1;
     }
     int ppw_env_ = -1;
     bool table_recycle_ = true;  // the visited set is returned zeroed (~Engine)

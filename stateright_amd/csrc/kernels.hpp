@@ -71,15 +71,35 @@ enum ErrBits { ERR_TABLE_FULL = 1, ERR_FRONTIER_OVERFLOW = 2, ERR_PEER_TIMEOUT =
 //    the slot stores the other qbits = B - k bits (the remainder) above dbits = 64 - qbits bits
 //    holding 1 + the linear-probe displacement from home. A slot value determines the key exactly,
 //    so the visited set is exact at 8 bytes per slot, for states far wider than 64 bits.
+//  * narrow quotient mode (s32 = 1, one-word keys of B <= 62 bits whose remainder leaves >= 10
+//    displacement bits in 32): the same encoding in 32-bit slots, dbits = 32 - qbits. 2pc N=9's
+//    40-bit key in a 2^25-slot table is a 15-bit remainder + 17 displacement bits: 128 MiB instead
+//    of 256, so the table and a level's streamed frontier fit the 256 MiB Infinity Cache together.
 struct TableView {
-    u64* keys;
+    u64* keys;      // cap slots of 8 bytes, or of 4 bytes when s32 (then (cap + 1) / 2 words)
     u64* meta;
     u64 mask;
     u32 qbits = 0;  // quotient mode: remainder bits per slot (0: fingerprint mode)
-    u32 dbits = 0;  // quotient mode: displacement bits (64 - qbits)
+    u32 dbits = 0;  // quotient mode: displacement bits (slot bits - qbits)
     u32 bbits = 0;  // quotient mode: key bits B
     u32 plimit = MAX_PROBE;  // probe limit: slots past home a probe may visit (quotient: 2^dbits - 2)
+    u32 s32 = 0;    // 32-bit slots (narrow quotient mode)
 };
+
+// Visited-set slot access (8- or 4-byte slots; 0 = vacant in both). POL: probe_load's policy.
+template <int POL, class T>
+__device__ __forceinline__ T probe_load(const T* p);
+template <int POL = 0>
+__device__ __forceinline__ u64 slot_load(const TableView& t, u64 i) {
+    if (t.s32) return (u64)probe_load<POL>(reinterpret_cast<const u32*>(t.keys) + i);
+    return probe_load<POL>(t.keys + i);
+}
+__device__ __forceinline__ u64 slot_cas(const TableView& t, u64 i, u64 tag) {
+    if (t.s32) return (u64)atomicCAS(reinterpret_cast<u32*>(t.keys) + i, 0u, (u32)tag);
+    return atomicCAS(reinterpret_cast<unsigned long long*>(t.keys + i), 0ull, (unsigned long long)tag);
+}
+// u64 words that hold a table of cap slots
+SR_HD u64 table_words(const TableView& t, u64 cap) { return t.s32 ? (cap + 1) / 2 : cap; }
 
 // The probe limit of an encoding: quotient mode stores 1 + the displacement in dbits bits.
 SR_HD u32 encoding_probe_limit(u32 qbits, u32 dbits) {
@@ -132,6 +152,20 @@ SR_HD u128 qperm(u128 x, u32 B) {
     return ((u128)a << hb) | b;
 }
 
+// A bijection on B-bit integers (B <= 63) for one-word keys: the murmur3 finalizer's steps with
+// every product taken mod 2^B (multiplying by an odd constant and x ^= x >> r are both invertible
+// on B bits). Two multiplies instead of qperm's four 64-bit mixes: it runs once per successor.
+SR_HD u64 qmix(u64 x, u32 B) {
+    const u64 m = (1ull << B) - 1;
+    const u32 r = (B + 1) / 2;
+    x ^= x >> r;
+    x = (x * 0xff51afd7ed558ccdull) & m;
+    x ^= x >> r;
+    x = (x * 0xc4ceb9fe1a85ec53ull) & m;
+    x ^= x >> r;
+    return x;
+}
+
 SR_HD u64 probe_step(const TableView& t) { return t.qbits ? 1ull : 0ull; }
 SR_HD ProbeKey fp_probe(const TableView& t, u64 fp) { return ProbeKey{fp & t.mask, fp}; }
 SR_HD ProbeKey quot_probe(const TableView& t, u128 h) {
@@ -156,14 +190,47 @@ inline u32 forced_probe_limit() {
     const char* e = std::getenv("SR_DISP_LIMIT");
     return e ? (u32)std::max(1, std::atoi(e)) : 0u;
 }
+// One-word keys (W == 1, B <= 62 bits; 2pc: 4N+4) take the narrow 32-bit slots whenever the
+// remainder leaves >= SLOT32_DMIN displacement bits, else 8-byte quotient slots. Their remainder
+// is max(1, B - k) bits: a table larger than the key space (2pc N=3's 16-bit key in the default
+// 2^22 slots) homes its keys in the first 2^(B-1) slots, still exact. SR_SLOT32=0 (measurement
+// knob) keeps one-word keys in 8-byte slots.
+constexpr u32 SLOT32_DMIN = 10;
+inline bool slot32_enabled() {
+    static const bool on = !std::getenv("SR_SLOT32") || std::atoi(std::getenv("SR_SLOT32")) != 0;
+    return on;
+}
+// Whether model M keys its visited set by its packed key (quotient mode) rather than by a
+// fingerprint; fixed per model instance, since a fingerprint cannot be turned back into a key.
+template <class M>
+inline bool quotient_model(const M& m) {
+    if constexpr (has_qkey<M>::value) {
+        const int B = m.qkey_bits();
+        if constexpr (M::W == 1) return B >= 2 && B <= 62;
+        else return B <= 120;
+    }
+    (void)m;
+    return false;
+}
 template <class M>
 inline TableView make_table_view(const M& m, u64* keys, u64* meta, u64 cap, bool natural = false) {
     TableView v{keys, meta, cap - 1};
-    if constexpr (has_qkey<M>::value && M::W >= 2) {
+    if constexpr (has_qkey<M>::value) {
         const u32 B = (u32)m.qkey_bits();
         u32 k = 0;
         while ((1ull << k) < cap) ++k;
-        if (B <= 120 && B > k && B - k <= 56) {
+        if constexpr (M::W == 1) {
+            if (quotient_model(m)) {
+                v.qbits = B > k ? B - k : 1u;
+                v.bbits = B;
+                if (slot32_enabled() && v.qbits + SLOT32_DMIN <= 32) {
+                    v.s32 = 1;
+                    v.dbits = 32 - v.qbits;
+                } else {
+                    v.dbits = 64 - v.qbits;
+                }
+            }
+        } else if (B <= 120 && B > k && B - k <= 56) {
             v.qbits = B - k;
             v.dbits = 64 - v.qbits;
             v.bbits = B;
@@ -175,19 +242,43 @@ inline TableView make_table_view(const M& m, u64* keys, u64* meta, u64 cap, bool
 }
 template <class M>
 inline u64 min_table_cap(const M& m) {
-    if constexpr (has_qkey<M>::value && M::W >= 2) {
+    if constexpr (has_qkey<M>::value) {
         const int B = m.qkey_bits();
-        if (B > 56 && B <= 96) return 1ull << (B - 56);
+        if (M::W == 1 && quotient_model(m) && B > 56) return 1ull << (B - 56);
+        if (M::W >= 2 && B > 56 && B <= 96) return 1ull << (B - 56);
     }
     return 1;
 }
 
+// The permuted key of a quotient-mode table (a bijection of the packed key; its top bits are the
+// home slot).
+template <class M>
+SR_HD u128 quot_hash(const M& m, const TableView& t, const u64* s) {
+    if constexpr (M::W == 1) return qmix((u64)m.qkey(s), t.bbits);
+    else return qperm(m.qkey(s), t.bbits);
+}
+
 template <class M>
 SR_HD ProbeKey probe_key(const M& m, const TableView& t, const u64* s) {
-    if constexpr (has_qkey<M>::value && M::W >= 2) {
-        if (t.qbits) return quot_probe(t, qperm(m.qkey(s), t.bbits));
+    if constexpr (has_qkey<M>::value) {
+        if (t.qbits) return quot_probe(t, quot_hash(m, t, s));
     }
     return fp_probe(t, state_fp<M>(s));
+}
+
+// Key of the block-local duplicate filter (expand_fast): injective on states wherever the host
+// turns the filter on. Fingerprint mode: the slot value (a bijection of a one-word state).
+// Quotient mode with B <= 63: the permuted key + 1 (home and remainder put back together).
+SR_HD u64 filter_key(const TableView& t, const ProbeKey& k) {
+    return t.qbits ? ((k.home << t.qbits) | (k.tag >> t.dbits)) + 1 : k.tag;
+}
+SR_HD u32 filter_index(const TableView& t, u64 fk) { return t.qbits ? (u32)fk : (u32)(fk >> 40); }
+// Whether the duplicate filter is exact for M's tables (filter_key injective). Multi-word quotient
+// tables (increment_lock N >= 9: every successor is new, nothing to filter) run without it.
+template <class M>
+inline bool filter_exact(const M& m) {
+    const TableView v = make_table_view(m, nullptr, nullptr, min_table_cap(m), true);
+    return !v.qbits || (M::W == 1 && v.bbits <= 63);
 }
 
 constexpr u32 NO_PARENT = 0xffffffffu;
@@ -465,8 +556,8 @@ __global__ void slot_publish_kernel(SlotWork sw) {
 
 // Probe loads of the visited set. POL selects the cache policy of the plain probe load:
 // 0 default, 1 agent-scope relaxed atomic load (sc1), 2 non-temporal, 3 system-scope (sc0 sc1).
-template <int POL>
-__device__ __forceinline__ u64 probe_load(const u64* p) {
+template <int POL, class T>
+__device__ __forceinline__ T probe_load(const T* p) {
     if constexpr (POL == 1) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     else if constexpr (POL == 2) return __builtin_nontemporal_load(p);
     else if constexpr (POL == 3) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -489,8 +580,7 @@ __device__ __forceinline__ u64 find_or_claim_from(const TableView& t, const Prob
         }
         if (cur == 0) {
             if (cas) ++*cas;
-            u64 prev = atomicCAS(reinterpret_cast<unsigned long long*>(&t.keys[i]), 0ull,
-                                 (unsigned long long)key);
+            const u64 prev = slot_cas(t, i, key);
             if (prev == 0) {
                 *is_new = true;
                 return i;
@@ -502,7 +592,7 @@ __device__ __forceinline__ u64 find_or_claim_from(const TableView& t, const Prob
         }
         i = (i + 1) & t.mask;
         key += step;
-        cur = probe_load<POL>(&t.keys[i]);
+        cur = slot_load<POL>(t, i);
         if (probes) ++*probes;
     }
     atomicOr(err, (u32)ERR_TABLE_FULL);
@@ -511,7 +601,7 @@ __device__ __forceinline__ u64 find_or_claim_from(const TableView& t, const Prob
 }
 
 __device__ __forceinline__ u64 find_or_claim(const TableView& t, const ProbeKey& k, bool* is_new, u32* err) {
-    return find_or_claim_from(t, k, t.keys[k.home], is_new, err);
+    return find_or_claim_from(t, k, slot_load(t, k.home), is_new, err);
 }
 
 // Lookup only.
@@ -519,7 +609,7 @@ __device__ __forceinline__ u64 find_slot(const TableView& t, const ProbeKey& k) 
     const u64 step = probe_step(t);
     u64 i = k.home, key = k.tag;
     for (int probe = 0; probe < MAX_PROBE; ++probe) {
-        u64 cur = t.keys[i];
+        const u64 cur = slot_load(t, i);
         if (cur == key) return i;
         if (cur == 0) return ~0ull;
         i = (i + 1) & t.mask;
@@ -1043,7 +1133,7 @@ __global__ void __launch_bounds__(64 * expand_wpb<M>()) __attribute__((amdgpu_wa
             // (their states recomputed from the map: only ~1 successor in 8 is new).
             constexpr int R = -PB;
             // without a packed key the table is always in fingerprint mode: home = tag & mask
-            constexpr bool FP_ONLY = !(has_qkey<M>::value && M::W >= 2);
+            constexpr bool FP_ONLY = !has_qkey<M>::value;
             for (u32 s0 = w0; s0 < wend; s0 += 64u * R) {
                 u64 kh[FP_ONLY ? 1 : R], kt[R];  // home slot and slot value of round r's successor
                 u32 vmask = 0;     // bit r: round r's successor is probed
@@ -1066,9 +1156,10 @@ __global__ void __launch_bounds__(64 * expand_wpb<M>()) __attribute__((amdgpu_wa
                         if (ok) {
                             const ProbeKey k = probe_key(m, t, q);
                             if (fmask) {  // block-local duplicate filter (see the round loop below)
-                                const u64 old = atomicExch(reinterpret_cast<unsigned long long*>(&filt[(u32)(k.tag >> 40) & fmask]),
-                                                           (unsigned long long)k.tag);
-                                ok = old != k.tag;
+                                const u64 fk = filter_key(t, k);
+                                const u64 old = atomicExch(reinterpret_cast<unsigned long long*>(&filt[filter_index(t, fk) & fmask]),
+                                                           (unsigned long long)fk);
+                                ok = old != fk;
                             }
                             if (!FP_ONLY) kh[FP_ONLY ? 0 : r] = k.home;
                             kt[r] = k.tag;
@@ -1104,8 +1195,8 @@ __global__ void __launch_bounds__(64 * expand_wpb<M>()) __attribute__((amdgpu_wa
                     }
                     if (!__ballot(st != 0)) break;
                     u64 v = 0;
-                    if (st == 1) v = probe_load<POL>(&t.keys[si]);
-                    if (st == 2) v = atomicCAS(reinterpret_cast<unsigned long long*>(&t.keys[si]), 0ull, (unsigned long long)tag);
+                    if (st == 1) v = slot_load<POL>(t, si);
+                    if (st == 2) v = slot_cas(t, si, tag);
                     if constexpr (STATS) {
                         probes += st == 1;
                         cas += st == 2;
@@ -1177,11 +1268,13 @@ __global__ void __launch_bounds__(64 * expand_wpb<M>()) __attribute__((amdgpu_wa
                 // (commuting actions), and a hit is a duplicate of a state whose probe another lane
                 // of this block owns — counted, never probed again. A miss (or an eviction) only
                 // costs the ordinary probe, so the filter never changes which states are new.
-                // (Fingerprint mode only: the host turns it off for a quotient-mode table.)
+                // (Keyed on filter_key, injective on states; the host turns the filter off for
+                // multi-word quotient-mode tables.)
                 if (fmask && ok[j]) {
-                    const u64 old = atomicExch(reinterpret_cast<unsigned long long*>(&filt[(u32)(pk[j].tag >> 40) & fmask]),
-                                               (unsigned long long)pk[j].tag);
-                    if (old == pk[j].tag) {
+                    const u64 fk = filter_key(t, pk[j]);
+                    const u64 old = atomicExch(reinterpret_cast<unsigned long long*>(&filt[filter_index(t, fk) & fmask]),
+                                               (unsigned long long)fk);
+                    if (old == fk) {
                         ++succ;
                         ok[j] = false;
                     }
@@ -1189,7 +1282,7 @@ __global__ void __launch_bounds__(64 * expand_wpb<M>()) __attribute__((amdgpu_wa
             }
 #pragma unroll
             for (int j = 0; j < PB; ++j) {
-                cur[j] = ok[j] ? probe_load<POL>(&t.keys[pk[j].home]) : 0;
+                cur[j] = ok[j] ? slot_load<POL>(t, pk[j].home) : 0;
                 if constexpr (STATS) probes += ok[j];
             }
 #if SR_TIMELINE
@@ -1574,7 +1667,7 @@ __global__ void __launch_bounds__(256) roots_start(M m, TableView t, InlineState
 template <int = 0> __global__ void rehash(TableView from, u64 from_cap, TableView to, u32* err) {
     u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= from_cap) return;
-    u64 k = from.keys[i];
+    const u64 k = slot_load(from, i);
     if (!k) return;
     bool is_new;
     u64 slot = find_or_claim(to, reprobe(from, to, i, k), &is_new, err);
@@ -1588,7 +1681,7 @@ template <int = 0> __global__ void __launch_bounds__(256) table_max_disp(TableVi
     u32 best = 0;
     const u64 dmask = t.qbits ? (1ull << t.dbits) - 1 : 0;
     for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < cap; i += (u64)gridDim.x * blockDim.x) {
-        const u64 v = t.keys[i];
+        const u64 v = slot_load(t, i);
         if (!v) continue;
         const u64 d = t.qbits ? (v & dmask) - 1 : (i - (v & t.mask)) & t.mask;
         best = max(best, (u32)min<u64>(d, 0xffffffffull));
@@ -1604,7 +1697,7 @@ template <int = 0> __global__ void remap_slots(u32* cand, u64 n, TableView from,
     if (i >= n) return;
     u32 s = cand[i];
     if (s == CAND_NONE) return;
-    cand[i] = (u32)find_slot(to, reprobe(from, to, s, from.keys[s]));
+    cand[i] = (u32)find_slot(to, reprobe(from, to, s, slot_load(from, s)));
 }
 
 // ---- exclusive scan of u32 counts (3-phase: tile sums, scan of sums, tile scan + carry) ----

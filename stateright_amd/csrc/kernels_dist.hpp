@@ -370,7 +370,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W <
             // registers and probed one visited-set access per lane and iteration.
             static_assert(!SELF, "self records probe nothing");
             constexpr int R = -PB;
-            constexpr bool FP_ONLY = !(has_qkey<M>::value && M::W >= 2);
+            constexpr bool FP_ONLY = !has_qkey<M>::value;
             for (u32 s0 = w0; s0 < wend; s0 += 64u * R) {
                 u64 kh[FP_ONLY ? 1 : R], kt[R];
                 u32 vmask = 0;
@@ -478,8 +478,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W <
                     }
                     if (!__ballot(st != 0)) break;
                     u64 v = 0;
-                    if (st == 1) v = probe_load<0>(&t.keys[si]);
-                    if (st == 2) v = atomicCAS(reinterpret_cast<unsigned long long*>(&t.keys[si]), 0ull, (unsigned long long)tag);
+                    if (st == 1) v = slot_load<0>(t, si);
+                    if (st == 2) v = slot_cas(t, si, tag);
                     if (st != 0) {
                         if (v == tag) {
                             st = 0;
@@ -589,7 +589,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W <
             // eviction or a race only re-sends (the owner dedups).
 #pragma unroll
             for (int j = 0; j < PB; ++j)
-                cur[j] = SELF || !ok[j] ? 0 : !rem[j] ? probe_load<0>(&t.keys[pk[j].home]) : sent ? sent[key[j] & sent_mask] : 0;
+                cur[j] = SELF || !ok[j] ? 0 : !rem[j] ? slot_load<0>(t, pk[j].home) : sent ? sent[key[j] & sent_mask] : 0;
 #pragma unroll
             for (int j = 0; j < PB; ++j) {
                 if (SELF || !(sent && rem[j])) continue;
@@ -840,8 +840,8 @@ __device__ __forceinline__ void insert_records(const M& m, RecAt rec_at, u32 tot
 #pragma unroll
                 for (int j = 0; j < R; ++j) {
                     v[j] = 0;
-                    if (st[j] == 1) v[j] = t.keys[si[j]];
-                    if (st[j] == 2) v[j] = atomicCAS(reinterpret_cast<unsigned long long*>(&t.keys[si[j]]), 0ull, (unsigned long long)tag[j]);
+                    if (st[j] == 1) v[j] = slot_load(t, si[j]);
+                    if (st[j] == 2) v[j] = slot_cas(t, si[j], tag[j]);
                 }
 #pragma unroll
                 for (int j = 0; j < R; ++j) {
@@ -919,7 +919,7 @@ __device__ __forceinline__ void insert_records(const M& m, RecAt rec_at, u32 tot
             }
         }
 #pragma unroll
-        for (int j = 0; j < PBI; ++j) cur[j] = ok[j] ? t.keys[pk[j].home] : 0;
+        for (int j = 0; j < PBI; ++j) cur[j] = ok[j] ? slot_load(t, pk[j].home) : 0;
         bool nws[PBI];  // every claim of the round before any append (their CASes overlap)
 #pragma unroll
         for (int j = 0; j < PBI; ++j) {

@@ -436,6 +436,10 @@ struct TwoPhaseT {
         return ab != 0 && cm != 0;             // always "consistent" violated
     }
     int init_states(u64* out) const { out[0] = 0; return 1; }
+    // Exact key (quotient visited set): the packed word itself, 4N+4 bits. At N=9 a 2^25-slot
+    // table keeps a 15-bit remainder and 17 displacement bits in a 32-bit slot (kernels.hpp).
+    int qkey_bits() const { return 4 * N() + 4; }
+    SR_HD unsigned __int128 qkey(const u64* s) const { return s[0]; }
     int expectation(int p) const { return p == 2 ? ALWAYS : SOMETIMES; }
     const char* prop_name(int p) const {
         return p == 0 ? "abort agreement" : p == 1 ? "commit agreement" : "consistent";

@@ -64,6 +64,8 @@ def gpu(model, params, order, **kw):
         b = b.target_state_count(kw["target"])
     if kw.get("counters"):
         b = b.counters()
+    if kw.get("hint"):
+        b = b.capacity_hint(kw["hint"])
     c = b.spawn_bfs().join()
     return c, rec
 
@@ -350,17 +352,19 @@ def test_probe_limit_overflow_doubles_the_table(case, order, pipe, monkeypatch):
     # the visited set in the middle of the check (quotient mode: one more displacement bit) and
     # finishes the level on it (repair pass: the missing successors are claimed, none is counted
     # twice), instead of restarting the check; counts stay exact in both orders, with and without
-    # level pipelining, in quotient (increment_lock, 2 words) and fingerprint (2pc) mode.
-    monkeypatch.setenv("SR_DISP_LIMIT", "6")
-    monkeypatch.setenv("SR_PIPELINE", pipe)
+    # level pipelining, in 8-byte quotient slots (increment_lock, 2 words) and 32-bit ones (2pc, one
+    # word: its 296 448 states in the default 2^22 slots displace at most 5 slots, so its limit is 3).
     model, params = case
+    limit = 3 if model == TWO_PHASE else 6
+    monkeypatch.setenv("SR_DISP_LIMIT", str(limit))
+    monkeypatch.setenv("SR_PIPELINE", pipe)
     o = oracle(model, params)
     c, _ = gpu(model, params, order, counters=True)
     assert (c.unique_state_count(), c.state_count(), c.max_depth()) == (o.unique_state_count, o.state_count, o.max_depth)
     assert sorted(c.discoveries()) == o.discovery_names()
     st = c.stats()
     assert st["table_doublings"] > 0 and st["restarts"] == 0
-    assert st["displacement_limit"] == 6 and 0 < st["max_displacement"] < 6
+    assert st["displacement_limit"] == limit and 0 < st["max_displacement"] < limit
 
 
 def test_displacement_stats_increment_lock_10():
