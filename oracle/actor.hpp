@@ -62,6 +62,15 @@ struct Out {
 //   bool on_timeout(Id, AState&, Out<Msg>&)                      (true: Cow::Owned)
 //   std::optional<Hist> record_in / record_out(const Hist&, const Envelope<Msg>&)
 //   bool within_boundary(const State&);  properties;  hashing / description / Debug text.
+// Envelopes a state description holds: Sys::net() where the system sizes it per instance, else
+// Sys::NET.
+template <class Sys>
+auto net_capacity_impl(const Sys& s, int) -> decltype(s.net()) { return s.net(); }
+template <class Sys>
+int net_capacity_impl(const Sys&, long) { return Sys::NET; }
+template <class Sys>
+int net_capacity(const Sys& s) { return net_capacity_impl(s, 0); }
+
 template <class Sys>
 struct ActorModel {
     using AState = typename Sys::AState;
@@ -201,8 +210,9 @@ struct ActorModel {
         std::vector<i64> net;
         for (auto& e : s.network) net.push_back(env_code(e));
         std::sort(net.begin(), net.end());
-        if (net.size() > (size_t)Sys::NET) throw std::runtime_error("network larger than the description's capacity");
-        net.resize(Sys::NET, -1);
+        const size_t cap = (size_t)net_capacity(sys);
+        if (net.size() > cap) throw std::runtime_error("network larger than the description's capacity");
+        net.resize(cap, -1);
         d.insert(d.end(), net.begin(), net.end());
         return d;
     }
@@ -240,6 +250,8 @@ struct PingPongMsg {
 
 struct PingPongSys {
     static constexpr int NET = 16;
+    // the GPU encoding's network slots: 16, or 32 past max_nat 7 (stateright_amd/csrc/actor.hpp)
+    int net() const { return max_nat > 7 ? 32 : 16; }
     using AState = u32;  // count
     using Msg = PingPongMsg;
     using Hist = std::pair<u32, u32>;  // (#in, #out)

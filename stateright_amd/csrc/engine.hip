@@ -283,7 +283,7 @@ namespace sr {
 // A registered model built for host use only (no device tables), handed to f: the models whose
 // description determines the state (`undescribe`), for sr_model_fingerprint and the self-test.
 template <class F>
-static int with_host_model(int model, const i64* p, int np, F&& f) {
+static i64 with_host_model(int model, const i64* p, int np, F&& f) {
     auto need = [&](int k) {
         if (np < k) throw Error(SR_ERR_ARG, "model " + std::to_string(model) + " needs " + std::to_string(k) + " params");
     };
@@ -406,8 +406,9 @@ extern "C" {
 
 int32_t sr_model_fingerprint(int32_t model, const int64_t* p, int32_t np, const int64_t* d, int32_t width, uint64_t* fp) {
     try {
-        const int r = with_host_model(model, p, np, [&](const auto& m) { return described_fingerprint(m, d, width, fp); });
-        if (r != SR_OK) set_error(r == SR_ERR_UNSUPPORTED ? "model has no state description inverse" : "bad description width");
+        std::string why;
+        const int r = (int)with_host_model(model, p, np, [&](const auto& m) { return (i64)described_fingerprint(m, d, width, fp, &why); });
+        if (r != SR_OK) set_error(why);
         return r;
     } catch (const Error& x) {
         set_error(x.what());
@@ -418,7 +419,7 @@ int32_t sr_model_fingerprint(int32_t model, const int64_t* p, int32_t np, const 
 int64_t sr_selftest_describe(int32_t model, const int64_t* p, int32_t np, int64_t max_states) {
     try {
         std::string why;
-        const i64 r = with_host_model(model, p, np, [&](const auto& m) { return (int)describe_roundtrip(m, max_states, why); });
+        const i64 r = with_host_model(model, p, np, [&](const auto& m) { return (i64)describe_roundtrip(m, max_states, why); });
         if (r < 0) set_error(why);
         return r;
     } catch (const Error& x) {

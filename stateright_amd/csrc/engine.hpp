@@ -1161,13 +1161,16 @@ class Engine final : public EngineBase {
     // avoid a partial last wave of workgroups. The measured gain is small and of the order of the
     // ±3% run-to-run noise (`profiles/r01_grid_sweep.jsonl`, `r01_gridcap_default.jsonl`); the cap
     // is printed with verbose=1. SR_GRID_MAX > 0 overrides it (<= 0 or unparsable: the default).
+    // The cap is cached per kernel form (the probe loop switches to the queue form once
+    // the table grows past 2^27 slots, whose occupancy differs from the rounds form's).
     u32 expand_grid_cap(bool nopf = false) {
-        u32& cap = nopf ? grid_max_nopf_ : grid_max_;
+        const int form = nopf ? 2 : probe_loop() < 0 ? 1 : 0;
+        u32& cap = grid_max_[form];
         if (cap) return cap;
         if (grid_env_) return cap = grid_env_;
         int per_cu = 0, cus = 0;
         const size_t dyn = filt_log2_ ? (8u << filt_log2_) : 0u;
-        const void* k = probe_loop() < 0 ? (const void*)expand_fast<M, -4, 0> : (const void*)expand_fast<M, 1, 0>;
+        const void* k = form == 1 ? (const void*)expand_fast<M, -4, 0> : (const void*)expand_fast<M, 1, 0>;
         if constexpr (W >= 4)
             if (nopf) k = (const void*)expand_fast<M, 1, 0, false, true>;
         SR_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 64 * WPB, dyn));
@@ -1409,8 +1412,8 @@ class Engine final : public EngineBase {
     }
     int ppw_env_ = -1;
     bool table_recycle_ = true;  // the visited set is returned zeroed (~Engine)
-    u32 grid_max_ = 0;      // cap on expand_fast's grid, 0 = two device residencies (SR_GRID_MAX)
-    u32 grid_max_nopf_ = 0;  // ... of its wide no-prefetch form
+    u32 grid_max_[3] = {0, 0, 0};  // cap on expand_fast's grid per form (rounds, queue, wide no-prefetch);
+                                   // 0 = not computed yet (two device residencies, or SR_GRID_MAX)
     u32 grid_env_ = 0;       // SR_GRID_MAX
     int wide_nopf_ = -1;     // SR_WIDE_NOPF: -1 chosen per level (use_nopf), 0 never, 1 always
     // The pipelined loop enqueues a second level ahead (chained) while the next frontier is
@@ -1470,16 +1473,32 @@ namespace sr {
 // The fingerprint of a state given by its canonical description (the integers of
 // sr_gpu_bfs_discovery_path / `describe`): what a host that holds the state compares with a
 // discovery's fingerprint chain (`Path::from_fingerprints`, src/checker/path.rs:20-86).
+// The description must be canonical: undescribe masks its fields, so a malformed or contradictory
+// description (a paxos Get return value for a client still in phase 1, a field out of range) would
+// otherwise map to some state and a plausible fingerprint. It is described again and compared.
 template <class M>
-int described_fingerprint(const M& m, const i64* d, int width, u64* fp) {
+int described_fingerprint(const M& m, const i64* d, int width, u64* fp, std::string* why = nullptr) {
     if constexpr (has_undescribe<M>::value) {
-        if (!d || !fp || width != m.describe_width()) return SR_ERR_ARG;
+        if (!d || !fp || width != m.describe_width()) {
+            if (why) *why = "bad description width";
+            return SR_ERR_ARG;
+        }
         u64 s[M::W];
         m.undescribe(d, s);
+        std::vector<i64> back((size_t)width);
+        m.describe(s, back.data());
+        for (int i = 0; i < width; ++i)
+            if (back[i] != d[i]) {
+                if (why)
+                    *why = "not a canonical state description (element " + std::to_string(i) + ": " + std::to_string(d[i]) +
+                           " describes back as " + std::to_string(back[i]) + ")";
+                return SR_ERR_ARG;
+            }
         *fp = state_fp<M>(s);
         return SR_OK;
     } else {
         (void)m, (void)d, (void)width, (void)fp;
+        if (why) *why = "model has no state description inverse";
         return SR_ERR_UNSUPPORTED;
     }
 }

@@ -54,7 +54,9 @@ def test_paxos_description_carries_the_history():
     from stateright_amd.plugin import model_fingerprint
     m = Paxos(2)
     # widths: 3 servers x 9, C op counts, 16 envelopes, C x C history values
-    base = [0] * 27 + [2, 2] + [-1] * 16 + [0, 0, 0, 0]
+    # history per client c: its Get's return value (-1: not returned; op count 2 = Get invoked),
+    # then how many ops of the other client had completed at that Get
+    base = [0] * 27 + [2, 2] + [-1] * 16 + [-1, 0, -1, 0]
     for i in range(3):
         base[i * 9 + 2] = -1
         base[i * 9 + 3:i * 9 + 6] = [-1, -1, -1]
@@ -69,3 +71,17 @@ def test_dgraph_has_no_inverse():
     from stateright_amd.models import DGraph
     with pytest.raises(ValueError):
         model_fingerprint(DGraph.with_property(N.SR_EVENTUALLY).with_path([0, 1]), [0])
+
+
+def test_malformed_description_is_rejected():
+    # undescribe masks its fields, so a description that is not a state's canonical one
+    # (here a 2pc rm_state of 7, masked to 3) must not yield a plausible fingerprint
+    from stateright_amd import TwoPhaseSys
+    from stateright_amd.plugin import model_fingerprint
+    m = TwoPhaseSys(3)
+    good = [0] * (3 * 3 + 3)
+    assert model_fingerprint(m, good) != 0
+    bad = list(good)
+    bad[0] = 7
+    with pytest.raises(ValueError, match="canonical"):
+        model_fingerprint(m, bad)
