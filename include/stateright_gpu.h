@@ -270,6 +270,35 @@ int32_t sr_dist_barrier(sr_dist* comm);
 int32_t sr_dist_allreduce_f64(sr_dist* comm, double* values, int32_t n, int32_t op);
 void sr_dist_free(sr_dist* comm);
 
+/* The partitioned search's HOST protocol without a GPU (tests): `world` processes on the
+ * shared-memory segment `name` (as sr_dist_shm_init, host buffers only) run a 2pc check whose
+ * device side is a CPU stand-in (expansion, routing by part_of, the direct exchange's per-slot
+ * checksum, one row per partition and level), while the level rows, their error precedence, the
+ * pipelined bucket plan and the outcome vote are the engine's own code (dist.hpp). Faults are
+ * injected where the device would raise them. Returns SR_OK with *out filled, or the error every
+ * rank agreed to fail with (sr_last_error). */
+typedef struct sr_dist_host_opts {
+    uint32_t struct_size;
+    int32_t rm_count;               /* 2pc resource managers (1..=7) */
+    uint64_t cmin;                  /* minimum planned bucket capacity (records per pair) */
+    int32_t corrupt_level;          /* >= 0: a record this rank receives at that level is altered after
+                                       its source checksummed it (once); -1: none */
+    int32_t capacity_fail_at_end;   /* this rank alone fails with a capacity error at the end (once) */
+    int32_t fail_at_end;            /* this rank alone fails with another error at the end (once) */
+    int32_t plan_div;               /* > 1: the planned capacities divided by it (an under-estimate) */
+} sr_dist_host_opts;
+typedef struct sr_dist_host_result {
+    uint64_t unique, state_count, local_unique;  /* global counts; states this rank's partition holds */
+    uint32_t max_depth, levels;
+    uint32_t attempts, restarts, fallbacks, disagreements;
+    uint32_t overflow_level;        /* first level with a bucket over its planned capacity (~0: none) */
+    uint32_t first_outcome;         /* this rank's outcome of the first attempt: 0 ok, 1 capacity,
+                                       2 exchange, 3 other error (dist.hpp Outcome) */
+    uint64_t plan_digest;           /* hash of the planned bucket capacities (equal on every rank) */
+} sr_dist_host_result;
+int32_t sr_dist_host_protocol(const char* name, int32_t rank, int32_t world, const sr_dist_host_opts* opts,
+                              sr_dist_host_result* out);
+
 /* Versions: runtime = what the loaded library reports, compiled = the headers the engine was built
  * against (RCCL: NCCL_VERSION_CODE; HIP: HIP_VERSION). A mismatch means another process-wide copy
  * of the runtime (e.g. one bundled with a Python framework) was loaded first. */

@@ -72,6 +72,38 @@ class sr_stats(ctypes.Structure):
         return {name: getattr(self, name) for name, _ in self._fields_}
 
 
+class sr_dist_host_opts(ctypes.Structure):
+    _fields_ = [
+        ("struct_size", ctypes.c_uint32),
+        ("rm_count", ctypes.c_int32),
+        ("cmin", ctypes.c_uint64),
+        ("corrupt_level", ctypes.c_int32),
+        ("capacity_fail_at_end", ctypes.c_int32),
+        ("fail_at_end", ctypes.c_int32),
+        ("plan_div", ctypes.c_int32),
+    ]
+
+
+class sr_dist_host_result(ctypes.Structure):
+    _fields_ = [
+        ("unique", ctypes.c_uint64),
+        ("state_count", ctypes.c_uint64),
+        ("local_unique", ctypes.c_uint64),
+        ("max_depth", ctypes.c_uint32),
+        ("levels", ctypes.c_uint32),
+        ("attempts", ctypes.c_uint32),
+        ("restarts", ctypes.c_uint32),
+        ("fallbacks", ctypes.c_uint32),
+        ("disagreements", ctypes.c_uint32),
+        ("overflow_level", ctypes.c_uint32),
+        ("first_outcome", ctypes.c_uint32),
+        ("plan_digest", ctypes.c_uint64),
+    ]
+
+    def as_dict(self):
+        return {name: getattr(self, name) for name, _ in self._fields_}
+
+
 # (name, restype, argtypes) of every exported entry point; tests check this list against the header.
 _P = ctypes.c_void_p
 _I64P = ctypes.POINTER(ctypes.c_int64)
@@ -124,6 +156,8 @@ SIGNATURES = [
     ("sr_dist_barrier", ctypes.c_int32, [_P]),
     ("sr_dist_allreduce_f64", ctypes.c_int32, [_P, ctypes.POINTER(ctypes.c_double), ctypes.c_int32, ctypes.c_int32]),
     ("sr_dist_free", None, [_P]),
+    ("sr_dist_host_protocol", ctypes.c_int32, [ctypes.c_char_p, ctypes.c_int32, ctypes.c_int32,
+                                               ctypes.POINTER(sr_dist_host_opts), ctypes.POINTER(sr_dist_host_result)]),
     ("sr_rccl_version", ctypes.c_int32, [ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32)]),
     ("sr_hip_runtime_version", ctypes.c_int32, [ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32)]),
     ("sr_device_synchronize", ctypes.c_int32, [ctypes.c_int32]),

@@ -17,7 +17,7 @@ SRC = os.path.join(CDIR, "engine.hip")
 UNITS = ["engine.hip", "reg_basic.hip", "reg_two_phase.hip", "reg_increment.hip", "reg_increment_lock.hip",
          "reg_paxos.hip", "reg_paxos_wide.hip", "reg_ping_pong.hip", "reg_registers.hip"]
 CSRC = [os.path.join(CDIR, f) for f in UNITS + ["registry.hpp", "engine.hpp", "kernels.hpp", "kernels_dist.hpp",
-                                                "dist.hpp", "models.hpp", "device.hpp", "paxos.hpp", "dgraph.hpp",
+                                                "dist.hpp", "dist_host.hpp", "models.hpp", "device.hpp", "paxos.hpp", "dgraph.hpp",
                                                 "actor.hpp"]]
 HEADERS = [os.path.join(ROOT, "include", f) for f in ("stateright_gpu.h", "stateright_gpu_model.hpp")]
 OUT = os.path.join(HERE, "libstateright_gpu.so")

@@ -79,6 +79,140 @@ enum class RedOp { Min, Max, Sum };
 // this rank (ERR_EXCHANGE or ERR_PEER_TIMEOUT); DistEngine::run turns it into a fallback.
 constexpr int ERR_CODE_EXCHANGE = -101;
 
+// ---- The host side of the level protocol as pure functions: the pipelined engine (lag_loop,
+// DistEngine::run) calls these, and so does the GPU-free protocol run over the shared-memory
+// transport (dist_host.hpp, tests/test_dist_host_protocol.py), which drives them from two
+// processes with rows of its own. ----
+
+// A partition's row of a level: T words of records sent to each partition, then these fields
+// (from index T), then one word per property: the rank of its first discovery in the new
+// frontier (~0: none). Every rank receives every row.
+enum RowField : u32 {
+    ROW_N = 0,        // states of the frontier the partition produced (its next level)
+    ROW_SUCC = 1,     // successors counted (state_count increments)
+    ROW_LOCAL = 2,    // states the partition claimed itself before the exchange
+    ROW_ERR = 3,      // ErrBits of the partition's route and insert
+    ROW_ENABLED = 4,  // enabled action slots of the expanded parents
+    ROW_ROOTS = 5,    // level 0: distinct init states
+    ROW_DISC = 6,
+};
+inline size_t row_words(u32 T, u32 nprops) { return (size_t)T + ROW_DISC + nprops; }
+
+// A level's error bits (OR over every row), acted on by every rank at the same level and in this
+// order: an exchange error wins over the capacity errors (a corrupt record can overflow a bucket,
+// and a capacity restart would keep the direct exchange).
+inline void throw_row_errors(u64 glob_err, u32 level) {
+    if (glob_err & ERR_EXCHANGE)
+        throw Error(ERR_CODE_EXCHANGE, "direct exchange: a receive slot failed its sequence tag or checksum (level " +
+                                           std::to_string(level) + ")");
+    if (glob_err & ERR_TABLE_FULL) throw Error(SR_ERR_CAPACITY, "visited set probe limit exceeded");
+    if (glob_err & ERR_FRONTIER_OVERFLOW) throw Error(SR_ERR_CAPACITY, "frontier or send bucket overflow");
+}
+
+// What the pipelined plan knows, the same on every rank: exact frontier sizes up to the last rows
+// read (n_last), an upper bound of the next one (n_hi: local claims + records received), the
+// growth of the last exact step, and the largest records per (source, owner) pair per frontier
+// state (pair_ratio).
+struct LevelPlan {
+    std::vector<u64> n_last, n_hi;
+    double growth = 1.0, pair_ratio = 0.0;
+    bool have_rows = false;
+    u64 glob_prev = 0;  // the last level's global frontier (growth is measured against it)
+    struct Sums {
+        u64 n = 0, succ = 0, err = 0, roots = 0, enabled = 0, maxpair = 0, recs = 0, local = 0;
+    };
+    // Global totals of a level's rows (T rows of RW words).
+    static Sums sums(const u64* all, u32 T, size_t RW) {
+        Sums s;
+        for (u32 q = 0; q < T; ++q) {
+            const u64* row = all + (size_t)q * RW;
+            s.n += row[T + ROW_N];
+            s.succ += row[T + ROW_SUCC];
+            s.local += row[T + ROW_LOCAL];
+            s.err |= row[T + ROW_ERR];
+            s.enabled += row[T + ROW_ENABLED];
+            s.roots += row[T + ROW_ROOTS];
+            for (u32 d = 0; d < T; ++d) {
+                s.maxpair = std::max<u64>(s.maxpair, row[d]);
+                s.recs += row[d];
+            }
+        }
+        return s;
+    }
+    // The plan after a level's rows (read after throw_row_errors accepted them).
+    void absorb(const u64* all, u32 T, size_t RW, const Sums& s) {
+        for (u32 q = 0; q < T; ++q) {
+            u64 r = 0;
+            for (u32 s2 = 0; s2 < T; ++s2) r += all[(size_t)s2 * RW + q];
+            n_hi[q] = all[(size_t)q * RW + T + ROW_LOCAL] + r;  // upper bound of partition q's next frontier
+            n_last[q] = all[(size_t)q * RW + T + ROW_N];
+        }
+        if (s.n) {
+            pair_ratio = (double)s.maxpair / (double)s.n;
+            if (glob_prev) growth = (double)s.n / (double)glob_prev;
+            have_rows = true;
+        }
+        glob_prev = s.n;
+    }
+    // Bucket capacity (records per pair) of the level `ahead` (1 or 2) levels past the last rows:
+    // the growth of the last exact step with a margin, compounded once per level of look-ahead.
+    u64 bucket_cap(u32 ahead, u64 cmin) const {
+        const double g = growth * 1.1;
+        u64 glob_fr = 0;
+        for (size_t q = 0; q < n_last.size(); ++q) {
+            const u64 c1 = have_rows ? std::min<u64>(n_hi[q], (u64)((double)n_last[q] * g) + 64) : n_last[q];
+            glob_fr += ahead == 2 ? (u64)((double)c1 * g) : c1;
+        }
+        return have_rows ? std::max<u64>(cmin, (u64)(pair_ratio * (double)glob_fr * 1.15) + 256) : cmin;
+    }
+};
+
+// The outcome of one check attempt on one rank, voted on by every rank (the max and min of the
+// codes over the ranks): the direct exchange's failures are seen by one owner only, so no rank may
+// decide alone.
+enum Outcome : int { OUT_OK = 0, OUT_CAPACITY = 1, OUT_EXCHANGE = 2, OUT_ERROR = 3 };
+inline int outcome_of(int error_code) {
+    return error_code == SR_ERR_CAPACITY ? OUT_CAPACITY : error_code == ERR_CODE_EXCHANGE ? OUT_EXCHANGE : OUT_ERROR;
+}
+enum class VoteAction { Done, Fallback, Restart, Fail };
+struct VoteDecision {
+    VoteAction act = VoteAction::Done;
+    bool disagree = false;  // a capacity restart that some rank did not see (it travels in the rows)
+    int code = 0;           // Fail: the error code to throw
+    std::string why;        // Fallback / Restart / Fail: the reason
+};
+// Every rank takes the same action (hi and lo are the same everywhere); only the message of a
+// failure depends on the rank's own outcome.
+inline VoteDecision decide_after_vote(int code, int hi, int lo, int attempt, int ecode, const std::string& what) {
+    VoteDecision d;
+    if (hi == OUT_ERROR) {
+        d.act = VoteAction::Fail;
+        d.code = code == OUT_ERROR ? ecode : SR_ERR_HIP;
+        d.why = code == OUT_ERROR ? what : std::string("partitioned search: another rank failed");
+    } else if (hi == OUT_EXCHANGE) {  // a corrupt exchange somewhere (only this falls back)
+        if (attempt >= 3) {
+            d.act = VoteAction::Fail;
+            d.code = SR_ERR_HIP;
+            d.why = "partitioned search: the exchange failed repeatedly: " + what;
+        } else {
+            d.act = VoteAction::Fallback;
+            d.why = code == OUT_EXCHANGE ? what : std::string("another rank's exchange failed");
+        }
+    } else if (hi == OUT_CAPACITY) {
+        // Capacity errors travel in the rows and reach every rank at the same level, so a rank that
+        // finished cleanly (lo == 0) means they did not: said, and restarted like the others.
+        d.disagree = lo != hi;
+        d.why = code ? what : std::string("another rank ran out of capacity");
+        if (attempt >= 3) {
+            d.act = VoteAction::Fail;
+            d.code = code ? ecode : SR_ERR_CAPACITY;
+        } else {
+            d.act = VoteAction::Restart;
+        }
+    }
+    return d;
+}
+
 // A device buffer as another rank can name it (direct exchange): its address in the exporting
 // process, the hipMalloc allocation around it, and an IPC handle of that allocation.
 struct PeerBlob {
@@ -760,28 +894,36 @@ struct ShmComm final : Comm {
             if (spin > 4096) sched_yield();
         }
     }
+    // host_only: the GPU-free protocol run (dist_host.hpp) passes host buffers and no stream; the
+    // collectives are then plain copies through the segment.
+    bool host_only = false;
     void d2h(void* dst, const void* src, size_t b, hipStream_t s) {
-        if (b) SR_HIP(hipMemcpyAsync(dst, src, b, hipMemcpyDeviceToHost, s));
+        if (b && host_only) std::memcpy(dst, src, b);
+        else if (b) SR_HIP(hipMemcpyAsync(dst, src, b, hipMemcpyDeviceToHost, s));
     }
     void h2d(void* dst, const void* src, size_t b, hipStream_t s) {
-        if (b) SR_HIP(hipMemcpyAsync(dst, src, b, hipMemcpyHostToDevice, s));
+        if (b && host_only) std::memcpy(dst, src, b);
+        else if (b) SR_HIP(hipMemcpyAsync(dst, src, b, hipMemcpyHostToDevice, s));
+    }
+    void drain(hipStream_t s) {
+        if (!host_only) SR_HIP(stream_sync(s));
     }
     void all_to_all(const u64* send, u64* recv, u64 count, hipStream_t s) override {
         need(count * 8 * (size_t)world);
         d2h(slot(rank), send, count * 8 * world, s);
-        SR_HIP(stream_sync(s));
+        drain(s);
         sync();
         for (int q = 0; q < world; ++q) h2d(recv + (u64)q * count, slot(q) + (size_t)rank * count * 8, count * 8, s);
-        SR_HIP(stream_sync(s));
+        drain(s);
         sync();
     }
     void all_gather(const u64* mine, u64* all, u64 count, hipStream_t s) override {
         need(count * 8);
         d2h(slot(rank), mine, count * 8, s);
-        SR_HIP(stream_sync(s));
+        drain(s);
         sync();
         for (int q = 0; q < world; ++q) h2d(all + (u64)q * count, slot(q), count * 8, s);
-        SR_HIP(stream_sync(s));
+        drain(s);
         sync();
     }
     void exchange(const std::vector<const u64*>& send, const std::vector<u64>& scount, const std::vector<u64*>& recv,
@@ -797,7 +939,7 @@ struct ShmComm final : Comm {
             d2h(slot(rank) + off, send[q], scount[q] * 8, s);
             off += scount[q] * 8;
         }
-        SR_HIP(stream_sync(s));
+        drain(s);
         sync();
         for (int q = 0; q < world; ++q) {
             const u64* m = reinterpret_cast<const u64*>(slot(q));
@@ -806,22 +948,22 @@ struct ShmComm final : Comm {
                                             " words, rank " + std::to_string(rank) + " expects " + std::to_string(rcount[q]));
             h2d(recv[q], slot(q) + m[rank], rcount[q] * 8, s);
         }
-        SR_HIP(stream_sync(s));
+        drain(s);
         sync();
     }
     void broadcast(u64* buf, u64 count, int root, hipStream_t s) override {
         need(count * 8);
         if (rank == root) d2h(slot(root), buf, count * 8, s);
-        SR_HIP(stream_sync(s));
+        drain(s);
         sync();
         if (rank != root) h2d(buf, slot(root), count * 8, s);
-        SR_HIP(stream_sync(s));
+        drain(s);
         sync();
     }
     void all_reduce(u64* buf, u64 count, RedOp op, hipStream_t s) override {
         need(count * 8);
         d2h(slot(rank), buf, count * 8, s);
-        SR_HIP(stream_sync(s));
+        drain(s);
         sync();
         std::vector<u64> v(count);
         std::memcpy(v.data(), slot(0), count * 8);
@@ -832,13 +974,13 @@ struct ShmComm final : Comm {
         }
         sync();  // every rank has read every slot
         h2d(buf, v.data(), count * 8, s);
-        SR_HIP(stream_sync(s));
+        drain(s);
     }
     bool peer_capable() const override { return direct_env_on(); }
     bool distinct_devices() const override { return devices_distinct; }
     void share(const void* mine, size_t b, void* all, hipStream_t s) override {
         need(b);
-        SR_HIP(stream_sync(s));
+        drain(s);
         std::memcpy(slot(rank), mine, b);
         sync();
         for (int q = 0; q < world; ++q) std::memcpy(static_cast<char*>(all) + (size_t)q * b, slot(q), b);
@@ -1095,7 +1237,7 @@ class DistEngine final : public EngineBase {
             try {
                 run_once();
             } catch (const Error& e) {
-                code = e.code == SR_ERR_CAPACITY ? 1 : e.code == ERR_CODE_EXCHANGE ? 2 : 3;
+                code = outcome_of(e.code);
                 what = e.what();
                 ecode = e.code;
                 if (!vote) {
@@ -1116,29 +1258,22 @@ class DistEngine final : public EngineBase {
                 comm_->all_reduce(dv.p, 2, RedOp::Max, stream_);
                 SR_HIP(hipMemcpyAsync(v, dv.p, sizeof(v), hipMemcpyDeviceToHost, stream_));
                 SR_HIP(stream_sync(stream_));
-                const int hi = (int)v[0], lo = (int)~v[1];
-                if (hi == 3) {
-                    if (code == 3) throw Error(ecode, what);
-                    throw Error(SR_ERR_HIP, "partitioned search: another rank failed");
-                }
-                if (hi == 2) {  // a corrupt exchange somewhere (only this falls back)
-                    if (attempt >= 3) throw Error(SR_ERR_HIP, "partitioned search: the exchange failed repeatedly: " + what);
-                    exchange_fallback(code == 2 ? what : std::string("another rank's exchange failed"));
+                const VoteDecision d = decide_after_vote(code, (int)v[0], (int)~v[1], attempt, ecode, what);
+                if (d.act == VoteAction::Fail) throw Error(d.code, d.why);
+                if (d.act == VoteAction::Fallback) {
+                    exchange_fallback(d.why);
                     continue;
                 }
-                if (hi == 0) {
+                if (d.act == VoteAction::Done) {
                     gather_paths();
                     gather_visits();
                     return;
                 }
-                // hi == 1: a capacity restart on every rank. Capacity errors travel in the rows and
-                // reach every rank at the same level, so a rank that finished cleanly (lo == 0)
-                // means they did not: said, and restarted like the others (the direct exchange kept).
-                if (lo != hi)
+                // a capacity restart on every rank (the direct exchange kept)
+                if (d.disagree)
                     std::fprintf(stderr, "[sr] rank %d: the ranks disagree on a capacity restart (this rank: %s); restarting on every rank\n",
                                  comm_->rank, code ? what.c_str() : "finished");
-                if (attempt >= 3) throw Error(code ? ecode : SR_ERR_CAPACITY, code ? what : std::string("another rank ran out of capacity"));
-                if (!code) what = "another rank ran out of capacity";
+                what = d.why;
             } else if (code == 0) {
                 gather_paths();
                 gather_visits();
@@ -1536,20 +1671,13 @@ class DistEngine final : public EngineBase {
             SR_HIP(hipGetLastError());
             wait_rows(rseq, RW * T_);
             const std::vector<u64>& all = rows_;
-            u64 glob_n = 0, glob_succ = 0, glob_err = 0, glob_roots = 0;
-            u64 glob_enabled = 0;
+            const LevelPlan::Sums sm = LevelPlan::sums(all.data(), T_, RW);
+            const u64 glob_n = sm.n, glob_succ = sm.succ, glob_roots = sm.roots, glob_enabled = sm.enabled;
             for (u32 q = 0; q < T_; ++q) {
-                const u64* row = &all[q * RW];
-                glob_enabled += row[T_ + 4];
                 gl_lstart_[q].push_back(gl_off_[q]);  // arena offset of this level in partition q
-                gl_off_[q] += row[T_ + 0];
-                glob_n += row[T_ + 0];
-                glob_succ += row[T_ + 1];
-                glob_err |= row[T_ + 3];
-                glob_roots += row[T_ + 5];
+                gl_off_[q] += all[q * RW + T_ + ROW_N];
             }
-            if (glob_err & ERR_TABLE_FULL) throw Error(SR_ERR_CAPACITY, "visited set probe limit exceeded");
-            if (glob_err & ERR_FRONTIER_OVERFLOW) throw Error(SR_ERR_CAPACITY, "frontier or send bucket overflow");
+            throw_row_errors(sm.err, level);
             for (auto& p : parts_) {
                 const u64* row = &all[p.id * RW];
                 if (level > lvl0_) {
@@ -2024,18 +2152,18 @@ class DistEngine final : public EngineBase {
                 SR_HIP(hipMemsetAsync(ds.p, 0, (size_t)NSHARD * MAX_PARTS * 8, stream_));
             }
         const u64 cmin = lag_cmin_;
-        glob_prev_ = 0;
-        // What the plan knows (the same on every rank): exact frontier sizes up to the last rows
-        // processed, an upper bound of the next one (local claims + records received), the growth
-        // of the last exact step, and records per (source, destination) pair per frontier state.
-        std::vector<u64> n_last(T_, 0), n_hi(T_, 0), n_plan(T_, 0);
+        // What the plan knows, the same on every rank (LevelPlan).
+        LevelPlan lp;
+        lp.n_last.assign(T_, 0);
+        lp.n_hi.assign(T_, 0);
+        std::vector<u64>& n_last = lp.n_last;
+        std::vector<u64>& n_hi = lp.n_hi;
+        std::vector<u64> n_plan(T_, 0);
         u64 glob0 = 0;
         for (auto& p : parts_) glob0 += p.n;
         if (comm_) glob0 *= T_;  // level 0 (roots): a rank knows only its own share
         for (u32 q = 0; q < T_; ++q) n_last[q] = std::max<u64>(1, glob0 / T_);
-        double growth = (double)std::min<u32>(D_, 32);  // first levels: no measurement yet
-        double pair_ratio = 0.0;
-        bool have_rows = false;
+        lp.growth = (double)std::min<u32>(D_, 32);  // first levels: no measurement yet
         u64 C0 = cmin;
         const bool head_start = lvl0_ > 0;
         if (head_start) {
@@ -2045,12 +2173,14 @@ class DistEngine final : public EngineBase {
                 n_last[q] = head_n_ / T_ + 1;
                 n_hi[q] = (u64)((double)n_last[q] * std::max(1.0, head_growth_) * 2.0) + 64;
             }
-            growth = head_growth_;
-            pair_ratio = head_spp_ / ((double)T_ * (double)T_);
-            have_rows = true;
-            glob_prev_ = head_prev_n_;  // the level before: the growth of the first rows is measured from it
-            C0 = std::max<u64>(cmin, (u64)(pair_ratio * (double)head_n_ * 1.3) + 256);
+            lp.growth = head_growth_;
+            lp.pair_ratio = head_spp_ / ((double)T_ * (double)T_);
+            lp.have_rows = true;
+            lp.glob_prev = head_prev_n_;  // the level before: the growth of the first rows is measured from it
+            C0 = std::max<u64>(cmin, (u64)(lp.pair_ratio * (double)head_n_ * 1.3) + 256);
         }
+        const bool& have_rows = lp.have_rows;
+        const double& growth = lp.growth;
         for (u32 q = 0; q < T_; ++q) n_plan[q] = n_last[q];
         lag_enqueue(0, C0, undiscovered, n_plan);
         std::vector<u32> seq0(parts_.size());
@@ -2061,9 +2191,7 @@ class DistEngine final : public EngineBase {
         auto plan_enqueue = [&](u32 ahead) {
             // growth of the last exact step with a margin (no floor at 1: shrinking tails shrink the
             // buckets too); it compounds once per level of look-ahead
-            const double g = growth * 1.1;
             const double gc = std::max(1.0, growth) * 1.3;  // capacities: cheap, so generous
-            u64 glob_fr = 0;
             for (auto& p : parts_) {
                 // the frontier after the last rows (<= its upper bound), the target level's
                 // frontier and the states it will claim
@@ -2077,11 +2205,7 @@ class DistEngine final : public EngineBase {
                 if (p.arena_cap < need) ensure_arena(p, std::max<u64>(need + need / 4, p.arena_cap * 2), p.arena_cap);
                 n_plan[p.id] = fr;
             }
-            for (u32 q = 0; q < T_; ++q) {
-                const u64 c1 = have_rows ? std::min<u64>(n_hi[q], (u64)((double)n_last[q] * g) + 64) : n_last[q];
-                glob_fr += ahead == 2 ? (u64)((double)c1 * g) : c1;
-            }
-            C = have_rows ? std::max<u64>(cmin, (u64)(pair_ratio * (double)glob_fr * 1.15) + 256) : cmin;
+            C = lp.bucket_cap(ahead, cmin);
             lag_enqueue(enq++, C, undiscovered, n_plan);
         };
         for (u32 level = lvl0_;; ++level) {
@@ -2100,20 +2224,11 @@ class DistEngine final : public EngineBase {
             }
             rows_.assign(pub->rows, pub->rows + RW * T_);
             const std::vector<u64>& all = rows_;
-            u64 glob_n = 0, glob_succ = 0, glob_err = 0, glob_roots = 0, glob_enabled = 0, maxpair = 0, recs = 0;
+            const LevelPlan::Sums sm = LevelPlan::sums(all.data(), T_, RW);
+            const u64 glob_n = sm.n, glob_succ = sm.succ, glob_err = sm.err, recs = sm.recs;
             for (u32 q = 0; q < T_; ++q) {
-                const u64* row = &all[q * RW];
-                glob_enabled += row[T_ + 4];
                 gl_lstart_[q].push_back(gl_off_[q]);
-                gl_off_[q] += row[T_ + 0];
-                glob_n += row[T_ + 0];
-                glob_succ += row[T_ + 1];
-                glob_err |= row[T_ + 3];
-                glob_roots += row[T_ + 5];
-                for (u32 d = 0; d < T_; ++d) {
-                    maxpair = std::max<u64>(maxpair, row[d]);
-                    recs += row[d];
-                }
+                gl_off_[q] += all[q * RW + T_ + ROW_N];
             }
             // A failed exchange check, a bucket over its capacity, an arena or a visited set too
             // small: the sender's (or, one level later, the receiver's) error bit is in these rows on
@@ -2123,19 +2238,13 @@ class DistEngine final : public EngineBase {
             // stall the vote until SR_PEER_TIMEOUT_MS. An exchange error wins over a
             // capacity error (a corrupt record can overflow a bucket; a capacity restart would keep
             // the direct exchange).
-            auto exchange_error = [&](u32 lv) {
-                return Error(ERR_CODE_EXCHANGE, "direct exchange: a receive slot failed its sequence tag or checksum (level " +
-                                                    std::to_string(lv) + ")");
-            };
-            if (glob_err & ERR_EXCHANGE) throw exchange_error(level);
-            if (glob_err & ERR_TABLE_FULL) throw Error(SR_ERR_CAPACITY, "visited set probe limit exceeded");
-            if (glob_err & ERR_FRONTIER_OVERFLOW) throw Error(SR_ERR_CAPACITY, "frontier or send bucket overflow");
+            throw_row_errors(glob_err, level);
             // The last level's insert has no later rows: its own check is read where the search
             // ends (the vote then makes every rank redo the check).
             auto own_exchange_check = [&] {
                 u32 own_err = 0;
                 for (size_t i = 0; i < parts_.size(); ++i) own_err |= ctx_->parts[parts_[i].res].pub[(seq0[i] + (level - lvl0_)) & 1]->err;
-                if (own_err & ERR_EXCHANGE) throw exchange_error(level);
+                throw_row_errors(own_err & ERR_EXCHANGE, level);
             };
             if (glob_err & ERR_PEER_TIMEOUT) {
                 auto& d = ctx_->dx;
@@ -2152,18 +2261,13 @@ class DistEngine final : public EngineBase {
                                         ", last sequence " + std::to_string(d.fseq) + ", flags [" + fl + "], check started at " +
                                         std::to_string(d.fseq_start) + (d.reused ? " reusing" : " after set-up") + ")");
             }
-            for (u32 q = 0; q < T_; ++q) {
-                u64 r = 0;
-                for (u32 s2 = 0; s2 < T_; ++s2) r += all[s2 * RW + q];
-                n_hi[q] = all[q * RW + T_ + 2] + r;  // upper bound of partition q's next frontier
-                n_last[q] = all[q * RW + T_ + 0];
-            }
+            lp.absorb(all.data(), T_, RW, sm);  // n_last, n_hi; growth and pair ratio when the level had states
             for (auto& p : parts_) {
                 if (level > lvl0_) p.uniq += n_last[p.id];
                 p.n = n_last[p.id];
                 p.lstart.push_back(p.lstart.back() + p.n);
             }
-            if (level == 0) unique_total = glob_roots;  // (a replicated head sets it instead)
+            if (level == 0) unique_total = sm.roots;  // (a replicated head sets it instead)
             u32 newly = 0;
             for (int pr = 0; pr < M::NPROPS; ++pr) {
                 if (!(undiscovered >> pr & 1)) continue;
@@ -2184,21 +2288,15 @@ class DistEngine final : public EngineBase {
                 const double us = std::chrono::duration<double, std::micro>(Clock::now() - t_trace_).count();
                 std::fprintf(stderr, "[sr-lag] level %u n=%llu succ=%llu maxpair=%llu C(next)=%llu  %.1f us since last\n",
                              level, (unsigned long long)glob_n, (unsigned long long)glob_succ,
-                             (unsigned long long)maxpair, (unsigned long long)C, us);
+                             (unsigned long long)sm.maxpair, (unsigned long long)C, us);
                 t_trace_ = Clock::now();
             }
             stats.records_routed += recs;
             if (glob_n) {
-                en_ratio_ = std::max(1.0, (double)glob_enabled / (double)glob_n);
+                en_ratio_ = std::max(1.0, (double)sm.enabled / (double)glob_n);
                 rec_ratio_ = (double)recs / (double)glob_n;
-                u64 lnew = 0;
-                for (u32 q = 0; q < T_; ++q) lnew += all[q * RW + T_ + 2];
-                lnew_ratio_ = (double)lnew / (double)glob_n;
-                pair_ratio = (double)maxpair / (double)glob_n;
-                if (glob_prev_) growth = (double)glob_n / (double)glob_prev_;
-                have_rows = true;
+                lnew_ratio_ = (double)sm.local / (double)glob_n;
             }
-            glob_prev_ = glob_n;
             if (glob_n == 0) {  // frontier exhausted everywhere: `is_done` (bfs.rs:307-311)
                 own_exchange_check();
                 reference_done = true;
@@ -2393,7 +2491,6 @@ class DistEngine final : public EngineBase {
     // the outcome vote of the direct exchange (SR_DX_VOTE=0 skips it: measurements only)
     bool vote_ = !(std::getenv("SR_DX_VOTE") && std::atoi(std::getenv("SR_DX_VOTE")) == 0);
     u32 send_cache_max_parts_ = std::getenv("SR_SEND_CACHE") ? (u32)std::atoi(std::getenv("SR_SEND_CACHE")) : 4;
-    u64 glob_prev_ = 0;        // pipelined mode: global frontier of the last level read
     // replicated head (SR_HEAD_MAX: largest head frontier; 0 disables)
     u64 head_max_ = std::getenv("SR_HEAD_MAX") ? std::strtoull(std::getenv("SR_HEAD_MAX"), nullptr, 10) : 65536;
     bool head_ok_ = true, head_failed_ = false, head_done_ = false;

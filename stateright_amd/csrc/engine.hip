@@ -5,6 +5,7 @@
 #include "dgraph.hpp"
 #include "paxos.hpp"
 #include "actor.hpp"
+#include "dist_host.hpp"
 
 namespace sr {
 
@@ -684,6 +685,29 @@ sr_dist* sr_dist_shm_init(int32_t rank, int32_t world, const char* name, int32_t
     } catch (const std::exception& x) {
         set_error(x.what());
         return nullptr;
+    }
+}
+
+int32_t sr_dist_host_protocol(const char* name, int32_t rank, int32_t world, const sr_dist_host_opts* opts,
+                              sr_dist_host_result* out) {
+    try {
+        if (world < 1 || rank < 0 || rank >= world || !name || !opts || !out) throw Error(SR_ERR_ARG, "bad host protocol run");
+        sr_dist_host_opts o;
+        std::memset(&o, 0, sizeof(o));
+        std::memcpy(&o, opts, std::min<size_t>(sizeof(o), opts->struct_size ? opts->struct_size : sizeof(o)));
+        if (o.rm_count < 1 || o.rm_count > 7) throw Error(SR_ERR_UNSUPPORTED, "host protocol run: rm_count must be in 1..=7");
+        ShmComm c(rank, world, std::string(name), -1, (size_t)1 << 24, false);
+        c.host_only = true;
+        DistHostRun run(c, o);
+        const int r = run.run();
+        *out = run.r;
+        return r;
+    } catch (const Error& x) {
+        set_error(x.what());
+        return x.code;
+    } catch (const std::exception& x) {
+        set_error(x.what());
+        return SR_ERR_ARG;
     }
 }
 
