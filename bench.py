@@ -568,6 +568,10 @@ def main():
             "gaps_ms": max(0.0, span_ms - big - small) if prof else None,
             "kernel_us": [round(ms * 1e3, 1) for ms, _ in prof],
             "frontier": [fr for _, fr in prof],
+            # visited-set loads and CAS claims of each launch (counting pass): DESIGN.md §3's
+            # attribution of the level times
+            "probes": [int(p) for p, _ in per_launch] if len(per_launch) == len(prof) else None,
+            "cas": [int(c) for _, c in per_launch] if len(per_launch) == len(prof) else None,
         } if prof else None,
         "engine": {k: st[k] for k in ("levels", "table_capacity", "rehashes", "level_loop_sec", "total_sec",
                                       "restarts", "pipelined", "records_routed", "head_levels")},

@@ -367,6 +367,10 @@ class Engine final : public EngineBase {
                 pessimistic_ = true;
                 grow_factor_ *= 4;
                 (void)stream_sync(stream_);
+                rehash_pending_ = false;  // (a failed enqueued rehash is this restart's cause, or moot)
+                retired_keys_.clear();
+                retired_arena_.clear();
+                retired_u32_.clear();
                 init_counters();
             }
         }
@@ -501,6 +505,7 @@ class Engine final : public EngineBase {
     // (cand) are remapped to the new table, since the rehash moves every entry.
     // min_slots: grow to at least this many slots (one rehash, however many doublings that is).
     void grow_table(u32* cand = nullptr, u64 cand_n = 0, u64 min_slots = 0) {
+        check_async_growth();  // an earlier asynchronous rehash's outcome first (aux_ is reused)
         const auto tg = Clock::now();
         DBuf<u64> ok, om;
         ok.swap(keys_);
@@ -531,6 +536,52 @@ class Engine final : public EngineBase {
             std::fprintf(stderr, "[sr] visited set %llu -> %llu slots in %.3f ms\n", (unsigned long long)old_cap,
                          (unsigned long long)cap_, secs(tg, Clock::now()) * 1e3);
     }
+
+    // The same growth ENQUEUED behind the level in flight, without waiting for it (the early growth
+    // of the pipelined loop, FAST order): the rehash reads the whole old table, so it needs nothing
+    // from the host, and the next level is launched on the new table right behind it. The old table
+    // is retired until the stream has passed the rehash (retire / release_retired), and the rehash's
+    // error word is read at the next synchronous point (check_async_growth): an entry that did not
+    // fit the new table fails the check with a capacity error, and the check restarts.
+    void grow_table_async(u64 min_slots) {
+        check_async_growth_pending_first();
+        retired_keys_.emplace_back();
+        retired_keys_.back().swap(keys_);
+        const TableView from = make_table_view(m_, retired_keys_.back().p, nullptr, cap_);
+        const u64 old_cap = cap_;
+        if (!aux_.p) aux_.alloc(o_.device, 2);
+        u64 f = 2;
+        while (old_cap * f < min_slots) f *= 2;
+        alloc_table(old_cap * f);
+        SR_HIP(hipMemsetAsync(aux_.p, 0, sizeof(u32), stream_));
+        rehash<<<blocks_for(old_cap, 256), 256, 0, stream_>>>(from, old_cap, view(), aux_.p);
+        SR_HIP(hipGetLastError());
+        rehash_pending_ = true;
+        stats.rehashes++;
+        if (o_.verbose)
+            std::fprintf(stderr, "[sr] visited set %llu -> %llu slots enqueued\n", (unsigned long long)old_cap,
+                         (unsigned long long)cap_);
+    }
+    // (an asynchronous growth is enqueued only while none is pending)
+    void check_async_growth_pending_first() {
+        if (rehash_pending_) check_async_growth();
+    }
+    // The outcome of an enqueued rehash (waits for the stream) and the retired buffers released.
+    void check_async_growth() {
+        if (!rehash_pending_ && retired_keys_.empty() && retired_arena_.empty()) return;
+        SR_HIP(stream_sync(stream_));
+        retired_keys_.clear();
+        retired_arena_.clear();
+        retired_u32_.clear();
+        if (!rehash_pending_) return;
+        rehash_pending_ = false;
+        u32 err = 0;
+        SR_HIP(hipMemcpy(&err, aux_.p, sizeof(u32), hipMemcpyDeviceToHost));
+        if (err) throw Error(SR_ERR_CAPACITY, "an enqueued rehash exceeded the new table's probe limit");
+    }
+    bool rehash_pending_ = false;
+    std::vector<DBuf<u64>> retired_keys_, retired_arena_;
+    std::vector<DBuf<u32>> retired_u32_;
 
     // Growth during a check (no capacity hint, or one too small: the path a user of the reference
     // gets, whose DashMap grows as it goes, src/checker/bfs.rs:26) takes a few large steps rather
@@ -573,7 +624,9 @@ class Engine final : public EngineBase {
 
     // The BFS-tree arena holds every level's states (visit order) and their parent ranks; grows
     // by copying the used prefix.
-    void ensure_arena(u64 states, u64 used) {
+    // async: the copy is enqueued behind the work in flight and the old buffers retired until the
+    // stream has passed it (check_async_growth), instead of waiting here.
+    void ensure_arena(u64 states, u64 used, bool async = false) {
         if (arena_cap_ >= states) return;
         const auto ta = Clock::now();
         // (growth steps of 4: each copies the arena so far and stops the level pipeline)
@@ -596,7 +649,16 @@ class Engine final : public EngineBase {
         arena_cap_ = cap;
         // the old buffers go back to the pool when na/np/ne leave scope: wait until no enqueued work
         // reads them (a first allocation has none, and the start of a check does not wait here)
-        if (had) SR_HIP(stream_sync(stream_));
+        if (had && async) {
+            retired_arena_.emplace_back();
+            retired_arena_.back().swap(na);
+            retired_u32_.emplace_back();
+            retired_u32_.back().swap(np);
+            retired_u32_.emplace_back();
+            retired_u32_.back().swap(ne);
+        } else if (had) {
+            SR_HIP(stream_sync(stream_));
+        }
         if (o_.verbose && had)
             std::fprintf(stderr, "[sr] arena -> %llu states (%llu copied) in %.3f ms (allocation %.3f ms)\n",
                          (unsigned long long)cap, (unsigned long long)used, secs(ta, Clock::now()) * 1e3, alloc_ms);
@@ -786,7 +848,10 @@ class Engine final : public EngineBase {
         // hinted: room for every state plus one level's worth of planning slack (a regrowth copies
         // the whole arena mid-run)
         const u64 slack = huge ? o_.capacity_hint / 10 * 3 : o_.capacity_hint / 2;
-        ensure_arena(std::max<u64>(std::max<u64>(1u << 16, (1u << 22) / W), (o_.capacity_hint + slack + 1024) * grow_factor_), 0);
+        // (without a hint: 2^24 words, 128 MiB + its parent ranks, never cleared and pooled across
+        // checks, so that the early table growth needs no arena copy behind it: 2pc N=9 fits)
+        const u64 arena0 = o_.capacity_hint ? (1u << 22) / W : (1u << 24) / W;
+        ensure_arena(std::max<u64>(std::max<u64>(1u << 16, arena0), (o_.capacity_hint + slack + 1024) * grow_factor_), 0);
         lstart_.assign({0, (u64)k});
         lvisited_.clear();
         const u32 und0 = ((1u << M::NPROPS) - 1) & ~emask_;
@@ -1055,6 +1120,21 @@ class Engine final : public EngineBase {
             const u64 nb_next = lstart_.back();
             // launch shape: a tight estimate (the grid strides over any excess)
             const u64 shape = (u64)((double)n * std::max(ratio_, 0.05) * 1.1) + 64;
+            // Early growth (no capacity hint): a visited set that the next three levels
+            // are projected to outgrow is grown now, while the level in flight is small. The rehash
+            // then moves few entries and the stop costs one small level's latency, instead of both
+            // at the first level that no longer fits (2pc N=9: ~1 M entries and a pipeline stop at
+            // level 9, 0.1 ms per check).
+            if (ahead.empty() && !pessimistic_ && !o_.capacity_hint && n <= early_grow_max_ &&
+                (double)(unique + est1 + est2 + est3) >= lmax_ * (double)cap_) {
+                // (enqueued behind the level in flight: no host wait; the whole old arena is copied,
+                // since the host does not know yet how much of it that level fills)
+                const u64 want = unique + est1 + est2 + est3;
+                grow_table_async(growth_slots((u64)((double)want / lmax_) + 1));
+                // (the arena only as far as the projection needs: it starts at 2^24 words)
+                if (nb_next + est1 + est2 + est3 > arena_cap_) ensure_arena(nb_next + est1 + est2 + est3, arena_cap_, true);
+                if (o_.verbose) std::fprintf(stderr, "[sr] early growth at a frontier of %llu states\n", (unsigned long long)n);
+            }
             // enqueue the next level before waiting for this one
             if (ahead.empty()) {
                 const bool spec = !pessimistic_ && (double)(unique + est1 + est2) < lmax_ * (double)cap_ &&
@@ -1110,6 +1190,7 @@ class Engine final : public EngineBase {
         SR_HIP(hipEventRecord(ctx_->done, stream_));
         release_table();
         drain(ctx_->done);
+        check_async_growth();
         return order_dependent;
     }
 
@@ -1408,8 +1489,12 @@ class Engine final : public EngineBase {
     int probe_loop() const {
         if (probe_batch_) return probe_batch_ < 0 ? -4 : 1;
         constexpr bool queue_ok = W == 1 || !has_qkey<M>::value;  // not multi-word quotient tables
+        if (queue_ok && W < 4 && queue_ratio_ > 0 && ratio_ >= queue_ratio_) return -4;  // (measurement knob)
         return queue_ok && W < 4 && cap_ >= (1ull << 27) ? -4 : 1;
     }
+    // SR_QUEUE_RATIO: the per-lane queues also for levels after one that made at least this many new
+    // states per parent (the claim-heavy ascending levels; 0: off)
+    double queue_ratio_ = std::getenv("SR_QUEUE_RATIO") ? std::atof(std::getenv("SR_QUEUE_RATIO")) : 0.0;
     int ppw_env_ = -1;
     bool table_recycle_ = true;  // the visited set is returned zeroed (~Engine)
     u32 grid_max_[3] = {0, 0, 0};  // cap on expand_fast's grid per form (rounds, queue, wide no-prefetch);
@@ -1419,6 +1504,10 @@ class Engine final : public EngineBase {
     // The pipelined loop enqueues a second level ahead (chained) while the next frontier is
     // estimated at <= this many states (SR_CHAIN_MAX; 0: never).
     u64 chain_max_ = 16384;
+    // Early growth of an unhinted visited set happens while the frontier is at most this large
+    // (SR_EARLY_GROW_MAX; 0: never).
+    u64 early_grow_max_ = std::getenv("SR_EARLY_GROW_MAX") ? std::strtoull(std::getenv("SR_EARLY_GROW_MAX"), nullptr, 10)
+                                                           : (u64)1 << 17;
     int table_kind_ = 0;  // DevicePool memory kind of the visited set (SR_TABLE_KIND, measurement knob)
     // the no-prefetch form exists for wide states only (it is the prefetching kernel otherwise)
     template <class L>
