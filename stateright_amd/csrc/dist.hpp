@@ -2562,7 +2562,11 @@ class DistEngine final : public EngineBase {
     bool insert_machines_ = !(std::getenv("SR_INSERT_MACHINES") && std::atoi(std::getenv("SR_INSERT_MACHINES")) == 0);
     int route_queue_env_ = std::getenv("SR_ROUTE_QUEUE") ? std::atoi(std::getenv("SR_ROUTE_QUEUE")) : -1;
     u32 rflags() const {
-        const u32 ls = lstage_words_ ? lstage_words_ / W : 0u;  // SR_LSTAGE_WORDS: the local stage's size
+        // SR_LSTAGE_WORDS: the local stage's size; with an owner key 512 words for narrow states (more
+        // blocks per CU: config 4 at T = 8 13.4 -> 12.6 ms per rank, T = 4 29.6 -> 24.6 ms,
+        // profiles/r06_config4_stages.txt)
+        const u32 lw = lstage_words_ ? lstage_words_ : okey_ && W <= 2 ? 512u : 0u;
+        const u32 ls = lw ? lw / W : 0u;
         return self_rec() | (okey_ ? (u32)RF_LOCAL : 0u) | (ordered_flush() ? (u32)RF_ORDERED : 0u) | ls << RF_LSTAGE_SHIFT;
     }
     // The owner-ordered record flush when the owners are other devices (RF_ORDERED; SR_ORDERED_FLUSH
@@ -2617,7 +2621,7 @@ class DistEngine final : public EngineBase {
     // chunk of 4 x 32 parents then fits: 2pc N=11 at T = 8 routes in 41 instead of 69 ms per check)
     // (0 = that default; SR_RSTAGE_WORDS overrides)
     u32 rstage_words_ = std::getenv("SR_RSTAGE_WORDS") ? (u32)std::atoi(std::getenv("SR_RSTAGE_WORDS")) : 0u;
-    u32 rstage_words() const { return rstage_words_ ? rstage_words_ : self_rec() ? 2048u : 1024u; }
+    u32 rstage_words() const { return rstage_words_ ? rstage_words_ : self_rec() ? 2048u : okey_ && W <= 2 ? 512u : 1024u; }
     int route_ppw_env_ = std::getenv("SR_ROUTE_PPW_LOG2") ? std::atoi(std::getenv("SR_ROUTE_PPW_LOG2")) : -1;
     bool trace_ = std::getenv("SR_DIST_TRACE") != nullptr;
     Clock::time_point t_trace_ = Clock::now();

@@ -37,6 +37,26 @@ __device__ __host__ __forceinline__ u32 part_of(const M& m, const u64* s, u64 fp
     }
     return owner_of(fp, nparts);
 }
+// The route kernel's key of a successor for the LDS filter and the sent cache, and its owner. The
+// key must be injective wherever those are on: the fingerprint in fingerprint mode (the slot value),
+// the permuted key + 1 for one-word quotient tables (filter_key: no second hash per successor), the
+// fingerprint for multi-word quotient tables (their filter and sent cache are off; it serves the
+// owner only). The owner is part_of's, with the fingerprint computed only when it is needed (no
+// owner key) and the key is not already it.
+template <class M>
+__device__ __forceinline__ u64 route_key(const M&, const TableView& t, const ProbeKey& pk, const u64* s) {
+    if (!t.qbits) return pk.tag;
+    if (M::W == 1) return filter_key(t, pk);
+    return state_fp<M>(s);
+}
+template <class M>
+__device__ __forceinline__ u32 route_owner(const M& m, const TableView& t, const u64* s, u64 key, u32 nparts) {
+    if constexpr (has_owner_key<M>::value) {
+        u64 k;
+        if (m.owner_key(s, &k)) return owner_of(fmix64(k * 0x9E3779B97F4A7C15ull + 0x632BE59BD9B4E019ull), nparts);
+    }
+    return owner_of(t.qbits && M::W == 1 ? state_fp<M>(s) : key, nparts);
+}
 template <class M>
 inline bool uses_owner_key(const M& m) {
     if constexpr (has_owner_key<M>::value) {
@@ -395,14 +415,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W <
                         }
                         if (ok) {
                             const ProbeKey pk = probe_key(m, t, q);
-                            const u64 key = t.qbits ? state_fp<M>(q) : pk.tag;
+                            const u64 key = route_key(m, t, pk, q);
                             if (fmask) {  // block-local duplicate filter (see expand_fast)
-                                const u64 old = atomicExch(reinterpret_cast<unsigned long long*>(&filt[(u32)(key >> 40) & fmask]),
+                                const u64 old = atomicExch(reinterpret_cast<unsigned long long*>(&filt[filter_index(t, key) & fmask]),
                                                            (unsigned long long)key);
                                 ok = old != key;
                             }
                             if (ok) {
-                                own = part_of(m, q, key, nparts);
+                                own = route_owner(m, t, q, key, nparts);
                                 rem = self_rec || own != my_part;
                                 if (!rem) {
                                     vmask |= 1u << r;
@@ -568,16 +588,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(M::W <
                 // (the same value in fingerprint mode; the host turns the filter and the sent
                 // cache off for a quotient-mode table)
                 pk[j] = ok[j] ? probe_key(m, t, ns[j]) : ProbeKey{0, 0};
-                key[j] = !ok[j] ? 0 : t.qbits ? state_fp<M>(ns[j]) : pk[j].tag;
+                key[j] = !ok[j] ? 0 : route_key(m, t, pk[j], ns[j]);
                 if (fmask && ok[j]) {  // block-local duplicate filter (see expand_fast)
-                    const u64 old = atomicExch(reinterpret_cast<unsigned long long*>(&filt[(u32)(key[j] >> 40) & fmask]),
+                    const u64 old = atomicExch(reinterpret_cast<unsigned long long*>(&filt[filter_index(t, key[j]) & fmask]),
                                                (unsigned long long)key[j]);
                     if (old == key[j]) {
                         ++succ;
                         ok[j] = false;
                     }
                 }
-                own[j] = ok[j] ? part_of(m, ns[j], key[j], nparts) : my_part;
+                own[j] = ok[j] ? route_owner(m, t, ns[j], key[j], nparts) : my_part;
                 rem[j] = ok[j] && (SELF || self_rec || own[j] != my_part);
             }
             // One memory round trip per round: a local successor's visited-set probe and a remote
