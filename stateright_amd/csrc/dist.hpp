@@ -1135,6 +1135,11 @@ class DistEngine final : public EngineBase {
             filt_log2_ = 0;
             send_cache_max_parts_ = 0;
         }
+        // With an owner key most successors stay local and the routed ones are few: the sent cache's
+        // lookups (a memory round trip per remote successor, issued with the local probes) cost more
+        // than the duplicates it keeps off the link (config 4, 2pc N=11 at T = 2: 45.6 -> 36.9 ms per
+        // rank without it, T = 4: 24.5 -> 21.2; profiles/r06_config4_stages.txt).
+        if (okey_ && !std::getenv("SR_SEND_CACHE")) send_cache_max_parts_ = 0;
     }
     ~DistEngine() override {
         if (ctx_) {
