@@ -1564,7 +1564,7 @@ class DistEngine final : public EngineBase {
         if (comm_) rows_mine_.alloc(o_.device, RW);
         for (auto& p : parts_) {
             u64 cap = std::max<u64>((u64)(1u << 16) * grow_factor_, min_table_cap(m_));
-            while ((double)cap * std::min(0.5, lmax(cap)) < (double)per_part * grow_factor_) cap <<= 1;
+            while ((double)cap * std::min(part_load_, lmax(cap)) < (double)per_part * grow_factor_) cap <<= 1;
             p.uniq = 0;
             p.cap = cap;
             p.keys.alloc(o_.device, p.words());
@@ -1917,7 +1917,7 @@ class DistEngine final : public EngineBase {
         for (auto& p : parts_) {
             // sized from the global head (the same on every rank): a rank-local overflow here would
             // leave the other ranks waiting in the first all-to-all
-            while ((double)total > std::min(0.5, lmax(p.cap)) * (double)p.cap) grow_table(p);
+            while ((double)total > std::min(part_load_, lmax(p.cap)) * (double)p.cap) grow_table(p);
             ensure_arena(p, n + n / 4 + 4096, 0);
             SR_HIP(hipMemsetAsync(cnt.p, 0, 8, stream_));
             take_owned<M><<<blocks_for(total, 256), 256, 0, stream_>>>(m_, harena_.p, (u32)total, (u32)hlstart_[level], p.id, T_,
@@ -2582,6 +2582,10 @@ class DistEngine final : public EngineBase {
     }
     int ordered_env_ = std::getenv("SR_ORDERED_FLUSH") ? std::atoi(std::getenv("SR_ORDERED_FLUSH")) : -1;
     u32 lstage_words_ = std::getenv("SR_LSTAGE_WORDS") ? (u32)std::atoi(std::getenv("SR_LSTAGE_WORDS")) : 0u;
+    // planned load of a partition's visited set at its share of the hint (SR_PART_LOAD): 0.3, like the
+    // one-GPU table (config 4 at T = 8: 12.58 -> 11.65 ms per rank, T = 4: 21.3 -> 19.7;
+    // profiles/r06_table_load.txt)
+    double part_load_ = std::getenv("SR_PART_LOAD") ? std::atof(std::getenv("SR_PART_LOAD")) : 0.3;
     const bool okey_ = uses_owner_key(m_);  // states owned by the model's owner key (kernels_dist.hpp part_of)
     u32 self_rec_min_ = std::getenv("SR_SELF_RECORDS_MIN") ? (u32)std::atoi(std::getenv("SR_SELF_RECORDS_MIN")) : 5u;
     size_t route_lds() const {

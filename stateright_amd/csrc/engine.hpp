@@ -589,13 +589,17 @@ class Engine final : public EngineBase {
     // entry. A step multiplies the size by SR_GROW_STEP (default 8), within a share of the free
     // device memory (never below what the level needs).
     u64 growth_slots(u64 need_slots) const {
-        u64 target = std::max<u64>(need_slots, cap_ * grow_step_);
+        // the first growth of a check that started without a hint (the model has outgrown the
+        // default table) takes a larger step, SR_GROW_FIRST (measurement knob; 0: grow_step_)
+        const u64 step = !o_.capacity_hint && stats.rehashes == 0 && grow_first_ ? grow_first_ : grow_step_;
+        u64 target = std::max<u64>(need_slots, cap_ * step);
         size_t free_b = 0, total_b = 0;
         if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b) target = std::min<u64>(target, std::max<u64>(need_slots, free_b / 4 / 8));
         return target;
     }
     u64 grow_step_ = std::getenv("SR_GROW_STEP") && std::atoi(std::getenv("SR_GROW_STEP")) >= 2
                          ? (u64)std::atoi(std::getenv("SR_GROW_STEP")) : 8u;
+    u64 grow_first_ = std::getenv("SR_GROW_FIRST") ? (u64)std::atoi(std::getenv("SR_GROW_FIRST")) : 0u;
 
     // The growth threshold of the visited set: 0.8 load, or lower for a quotient-mode table whose
     // probe limit (set by its displacement bits) would otherwise be reached by the longest
@@ -1534,7 +1538,9 @@ class Engine final : public EngineBase {
         return m;
     }
     double en_ratio_ = 8.0;     // enabled action slots per expanded parent in the last level
-    double table_load_ = 0.5;
+    // planned load of the visited set at the capacity hint (SR_TABLE_LOAD): 0.3 with 4-byte slots (2pc
+    // N=9: 2^26 slots, 256 MiB, 1.615 -> 1.565 ms; N=10 8.64 -> 7.89 ms; profiles/r06_table_load.txt)
+    double table_load_ = 0.3;
     bool load_env_ = false;
     Ctx* ctx_ = nullptr;
     hipStream_t stream_ = nullptr;
