@@ -27,13 +27,29 @@ constexpr u64 PAR_SEARCH = ~0ull - 1;  // parent not recorded: search the previo
 
 // Owner partition of a fingerprint: the high 32 bits scaled to [0, T) (any T, uniform).
 __device__ __host__ __forceinline__ u32 owner_of(u64 fp, u32 nparts) { return (u32)(((fp >> 32) * (u64)nparts) >> 32); }
+// Owner partition of an owner key (a model's projection of the state): a multiplicative hash of the
+// key's 32-bit halves, scaled to [0, T). Round 6: against fmix64 of the key (SR_OKEY_HASH=0, a
+// build-time variant) it balances config 4's partitions better (max/mean 1.09 -> 1.03 at T = 8)
+// and costs fewer instructions per successor: critical path per rank T = 8 11.68 -> 10.83 ms,
+// T = 4 19.78 -> 18.66 (profiles/r06_config4_stages.txt).
+#ifndef SR_OKEY_HASH
+#define SR_OKEY_HASH 1
+#endif
+__device__ __host__ __forceinline__ u32 key_owner(u64 key, u32 nparts) {
+#if SR_OKEY_HASH
+    const u32 h = (u32)key * 0x9E3779B1u ^ (u32)(key >> 32) * 0x85EBCA77u;
+    return (u32)(((u64)h * nparts) >> 32);
+#else
+    return owner_of(fmix64(key * 0x9E3779B97F4A7C15ull + 0x632BE59BD9B4E019ull), nparts);
+#endif
+}
 // Owner partition of state s (fingerprint fp): by the model's owner key when it has one
 // (models.hpp has_owner_key; mixed, then scaled like a fingerprint), else by the fingerprint.
 template <class M>
 __device__ __host__ __forceinline__ u32 part_of(const M& m, const u64* s, u64 fp, u32 nparts) {
     if constexpr (has_owner_key<M>::value) {
         u64 key;
-        if (m.owner_key(s, &key)) return owner_of(fmix64(key * 0x9E3779B97F4A7C15ull + 0x632BE59BD9B4E019ull), nparts);
+        if (m.owner_key(s, &key)) return key_owner(key, nparts);
     }
     return owner_of(fp, nparts);
 }
@@ -53,7 +69,7 @@ template <class M>
 __device__ __forceinline__ u32 route_owner(const M& m, const TableView& t, const u64* s, u64 key, u32 nparts) {
     if constexpr (has_owner_key<M>::value) {
         u64 k;
-        if (m.owner_key(s, &k)) return owner_of(fmix64(k * 0x9E3779B97F4A7C15ull + 0x632BE59BD9B4E019ull), nparts);
+        if (m.owner_key(s, &k)) return key_owner(k, nparts);
     }
     return owner_of(t.qbits && M::W == 1 ? state_fp<M>(s) : key, nparts);
 }

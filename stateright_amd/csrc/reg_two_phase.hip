@@ -5,16 +5,21 @@ namespace sr {
 // 2pc's owner key for the partitioned search (TwoPhase::okey_rms): the tuples of this many RMs.
 // More RMs balance the partitions better, fewer keep more successors local (DESIGN.md §6 measures
 // the trade-off). SR_OWNER_RMS overrides it; 0 owns states by fingerprint.
-static int two_phase_owner_rms(int n) {
+// Round 6 (multiplicative owner hash, profiles/r06_config4_stages.txt), config 4 per-rank critical
+// path: T = 8: 4 RMs 10.85 ms, 3: 13.24, 5: 11.66; T = 4: 4 RMs 18.73, 5: 19.63; T = 2: 4 RMs 35.03,
+// 5: 33.45 (two partitions need the finer key for balance).
+static int two_phase_owner_rms(int n, int parts) {
     if (const char* e = std::getenv("SR_OWNER_RMS")) return std::max(0, std::min(n, std::atoi(e)));
-    return n <= 7 ? (n + 1) / 2 : 4;  // N=11 at T=8: 0.33 of successors cross, per-level balance 1.14
+    if (n <= 7) return (n + 1) / 2;
+    return parts == 2 ? std::min(n, 5) : 4;
 }
 
 std::unique_ptr<EngineBase> reg_two_phase(const EngineArgs& a) {
     a.need(1);
     const i64 n = a.p[0];
     if (n < 1 || n > 14) throw Error(SR_ERR_UNSUPPORTED, "2pc: rm_count must be in 1..=14 (4n+4 <= 63 bits)");
-    const TwoPhase m{(int)n, two_phase_owner_rms((int)n)};
+    const int parts = !a.dist ? 1 : a.comm ? a.comm->world : a.vparts;
+    const TwoPhase m{(int)n, two_phase_owner_rms((int)n, parts)};
     if (a.o->symmetry) return make_for(Canon<TwoPhase>(m), a);
     // The engines of the bench configurations with the rm count compiled in (TwoPhaseT<NC>: the
     // per-rm loops unroll with constant shifts): BASELINE configs[2] (N = 9, 10) on one GPU and
