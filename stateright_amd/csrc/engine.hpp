@@ -315,6 +315,10 @@ class Engine final : public EngineBase {
         // The LDS duplicate filter must be injective on states (kernels.hpp filter_key): one-word
         // states in either mode; a multi-word quotient-mode table runs without it.
         if (!filter_exact(m_)) filt_log2_ = 0;
+        // 4-byte entries where they are exact: twice the entries in the same LDS (SR_FILTER_COMPACT=0: off)
+        if (filt_log2_ && (!std::getenv("SR_FILTER_COMPACT") || std::atoi(std::getenv("SR_FILTER_COMPACT"))) &&
+            filter_compact_ok(m_, filt_log2_ + 1))
+            filt_log2_ += 1, filt_compact_ = true;
         if (const char* e = std::getenv("SR_PIPELINE")) pipeline_ = std::atoi(e) != 0;
         if (const char* e = std::getenv("SR_QUERY_LOG2")) query_mask_ = (1ull << std::atoi(e)) - 1;
         if (const char* e = std::getenv("SR_GRID_MAX")) grid_env_ = (u32)std::max(0, std::atoi(e));  // <= 0: unset
@@ -1254,7 +1258,7 @@ class Engine final : public EngineBase {
         if (cap) return cap;
         if (grid_env_) return cap = grid_env_;
         int per_cu = 0, cus = 0;
-        const size_t dyn = filt_log2_ ? (8u << filt_log2_) : 0u;
+        const size_t dyn = filt_bytes();
         const void* k = form == 1 ? (const void*)expand_fast<M, -4, 0> : (const void*)expand_fast<M, 1, 0>;
         if constexpr (W >= 4)
             if (nopf) k = (const void*)expand_fast<M, 1, 0, false, true>;
@@ -1308,9 +1312,9 @@ class Engine final : public EngineBase {
         const u32 svc = sw.pub || sw.zero ? 1u : 0u;  // the extra service workgroup (SlotWork)
         timed([&] {
             auto launch = [&](auto kern) {
-                kern<<<grid + svc, 64 * WPB, filt_log2_ ? (8u << filt_log2_) : 0u, stream_>>>(
+                kern<<<grid + svc, 64 * WPB, filt_bytes(), stream_>>>(
                     m_, arena_.p + fbase * W, 0u, n, view(), arena_.p + nbase * W, apar_.p + nbase, ncap, lc,
-                    undiscovered, nullptr, sq, 0u, ppw_log2, filt_log2_, sw);
+                    undiscovered, nullptr, sq, 0u, ppw_log2, filt_arg(), sw);
             };
             if (o_.counters) launch(expand_fast<M, 1, 0, true>);
             else if (nopf) launch_nopf(launch);
@@ -1390,9 +1394,9 @@ class Engine final : public EngineBase {
                     }
                     timed([&] {
                         auto launch = [&](auto kern) {
-                            kern<<<grid, 64 * WPB, filt_log2_ ? (8u << filt_log2_) : 0u, stream_>>>(
+                            kern<<<grid, 64 * WPB, filt_bytes(), stream_>>>(
                                 m_, cur(), ulo, uhi, view(), next, npar, ncap, lc_d_, undiscovered, hcd(sq), sq,
-                                last ? 1u : 0u, ppw_log2, filt_log2_, sw);
+                                last ? 1u : 0u, ppw_log2, filt_arg(), sw);
                         };
                         if (o_.counters) launch(expand_fast<M, 1, 0, true>);
                         else if (nopf) launch_nopf(launch);
@@ -1526,6 +1530,9 @@ class Engine final : public EngineBase {
     bool slot_published_ = true;      // its publish is done or enqueued
     std::map<u32, size_t> seq_launch_;  // launch sequence number -> index in launch_frontier
     u32 filt_log2_ = W >= 4 ? 10 : 9;  // block-local duplicate filter (SR_FILTER_LOG2 sweep in profiles/)
+    bool filt_compact_ = false;         // ... in 4-byte entries (kernels.hpp FILT_COMPACT)
+    size_t filt_bytes() const { return filt_log2_ ? (size_t)(filt_compact_ ? 4u : 8u) << filt_log2_ : 0u; }
+    u32 filt_arg() const { return filt_log2_ | (filt_compact_ ? FILT_COMPACT : 0u); }
     bool pessimistic_ = false;  // size chunks for max out-degree new states per parent
     u64 grow_factor_ = 1;       // initial-capacity multiplier after a capacity restart
     double ratio_ = 1.0;        // new states per expanded parent in the last level

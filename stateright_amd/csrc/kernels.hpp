@@ -280,6 +280,26 @@ inline bool filter_exact(const M& m) {
     const TableView v = make_table_view(m, nullptr, nullptr, min_table_cap(m), true);
     return !v.qbits || (M::W == 1 && v.bbits <= 63);
 }
+// Compact filter (expand_fast's filt_log2 argument | FILT_COMPACT): 4-byte entries for one-word
+// quotient tables whose filter key fk (<= 2^B) loses at most 30 bits past the entry index: entry
+// fk & (2^L - 1) holds (fk >> L) | 2^31 (never 0, the empty entry), exact for B - L <= 30. Twice the
+// entries in the same LDS (2pc N=9, B = 40: 1024 entries in 4 KB instead of 512).
+constexpr u32 FILT_COMPACT = 0x100;
+template <class M>
+inline bool filter_compact_ok(const M& m, u32 log2_entries) {
+    if (M::W != 1 || !filter_exact(m)) return false;
+    const TableView v = make_table_view(m, nullptr, nullptr, min_table_cap(m), true);
+    return v.qbits && v.bbits <= 30 + log2_entries;
+}
+// The block-local filter's lookup-and-insert of key fk: whether fk was there (a duplicate).
+__device__ __forceinline__ bool filter_seen(u64* filt, bool compact, u32 flog, u32 fmask, const TableView& t, u64 fk) {
+    if (compact) {
+        const u32 e = (u32)(fk >> flog) | 0x80000000u;
+        return atomicExch(reinterpret_cast<u32*>(filt) + ((u32)fk & fmask), e) == e;
+    }
+    return atomicExch(reinterpret_cast<unsigned long long*>(&filt[filter_index(t, fk) & fmask]), (unsigned long long)fk) ==
+           (unsigned long long)fk;
+}
 
 constexpr u32 NO_PARENT = 0xffffffffu;
 
@@ -934,9 +954,13 @@ __global__ void __launch_bounds__(64 * expand_wpb<M>()) __attribute__((amdgpu_wa
         lc->unique = sw.ubase + (hi - lo);
     }
     SR_TL(1);
+    // (the compact filter only for one-word quotient tables: FILT_COMPACT)
+    const bool fcompact = M::W == 1 && has_qkey<M>::value && (filt_log2 & FILT_COMPACT) != 0;
+    filt_log2 &= FILT_COMPACT - 1;
     const u32 fmask = filt_log2 ? (1u << filt_log2) - 1 : 0;
+    const u32 fwords = !fmask ? 0u : fcompact ? (fmask + 1) / 2 : fmask + 1;  // u64 words of LDS
     if (lo + (u64)blockIdx.x * chunk < hi)  // blocks past the frontier only take their ticket
-        for (u32 i = threadIdx.x; i < (fmask ? fmask + 1 : 0u); i += blockDim.x) filt[i] = 0;
+        for (u32 i = threadIdx.x; i < fwords; i += blockDim.x) filt[i] = 0;
     // One level: parents [lo, hi) of `frontier` into `next`.
     auto level = [&](const u64* __restrict__ frontier, u32 lo, u32 hi, u64* __restrict__ next,
                      u32* __restrict__ next_par, u32 next_cap, LevelCounters* lc, u32 undiscovered) {
@@ -1155,12 +1179,8 @@ __global__ void __launch_bounds__(64 * expand_wpb<M>()) __attribute__((amdgpu_wa
                         }
                         if (ok) {
                             const ProbeKey k = probe_key(m, t, q);
-                            if (fmask) {  // block-local duplicate filter (see the round loop below)
-                                const u64 fk = filter_key(t, k);
-                                const u64 old = atomicExch(reinterpret_cast<unsigned long long*>(&filt[filter_index(t, fk) & fmask]),
-                                                           (unsigned long long)fk);
-                                ok = old != fk;
-                            }
+                            if (fmask)  // block-local duplicate filter (see the round loop below)
+                                ok = !filter_seen(filt, fcompact, filt_log2, fmask, t, filter_key(t, k));
                             if (!FP_ONLY) kh[FP_ONLY ? 0 : r] = k.home;
                             kt[r] = k.tag;
                         }
@@ -1271,10 +1291,7 @@ __global__ void __launch_bounds__(64 * expand_wpb<M>()) __attribute__((amdgpu_wa
                 // (Keyed on filter_key, injective on states; the host turns the filter off for
                 // multi-word quotient-mode tables.)
                 if (fmask && ok[j]) {
-                    const u64 fk = filter_key(t, pk[j]);
-                    const u64 old = atomicExch(reinterpret_cast<unsigned long long*>(&filt[filter_index(t, fk) & fmask]),
-                                               (unsigned long long)fk);
-                    if (old == fk) {
+                    if (filter_seen(filt, fcompact, filt_log2, fmask, t, filter_key(t, pk[j]))) {
                         ++succ;
                         ok[j] = false;
                     }
