@@ -101,8 +101,7 @@ class DevicePool {
     // (hipDeviceMallocFinegrained), which a system-scope acquire makes coherent with stores that
     // ANOTHER device issued over xGMI while a kernel runs (the direct exchange's flags and receive
     // buffers: its owner's L2 must not serve a line it cached before a peer's store); kind 2:
-    // uncached device memory (hipDeviceMallocUncached: no line of it is held dirty in an L2); kind 3:
-    // physically contiguous device memory (hipDeviceMallocContiguous: larger translation fragments).
+    // uncached device memory (hipDeviceMallocUncached: no line of it is held dirty in an L2).
     void* alloc(int dev, size_t bytes, int kind = 0) {
         bytes = round(bytes);
         {
@@ -120,7 +119,6 @@ class DevicePool {
         auto raw = [&]() {
             return kind == 1   ? hipExtMallocWithFlags(&p, bytes, hipDeviceMallocFinegrained)
                    : kind == 2 ? hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached)
-                   : kind == 3 ? hipExtMallocWithFlags(&p, bytes, hipDeviceMallocContiguous)
                                : hipMalloc(&p, bytes);
         };
         const auto t0 = std::chrono::steady_clock::now();
