@@ -1245,11 +1245,13 @@ class Engine final : public EngineBase {
         return launch_expand(fbase, (u32)n, false, n, undiscovered);
     }
 
-    // expand_fast's grid is capped at two full residencies of the device (resident blocks per CU
-    // at its LDS footprint x CUs); the kernel strides over any further parents. Whole residencies
-    // avoid a partial last wave of workgroups. The measured gain is small and of the order of the
-    // ±3% run-to-run noise (`profiles/r01_grid_sweep.jsonl`, `r01_gridcap_default.jsonl`); the cap
-    // is printed with verbose=1. SR_GRID_MAX > 0 overrides it (<= 0 or unparsable: the default).
+    // expand_fast's grid is capped at whole residencies of the device (resident blocks per CU at
+    // its LDS footprint x CUs, grid_res_ of them: one for one-word states, two otherwise); the
+    // kernel strides over any further parents. Whole residencies avoid a partial last wave of
+    // workgroups, and for 2pc one residency, every block starting at once and striding with its
+    // prefetch, beats two (round 6, `profiles/r06_grid_cap.txt`: N=9 1.556 -> 1.520 ms, N=10 7.93 ->
+    // 7.76, N=11 50.7 -> 50.5; 1.17 / 0.83 residencies were slower); the cap is printed with
+    // verbose=1. SR_GRID_MAX > 0 overrides it (<= 0 or unparsable: the default).
     // The cap is cached per kernel form (the probe loop switches to the queue form once
     // the table grows past 2^27 slots, whose occupancy differs from the rounds form's).
     u32 expand_grid_cap(bool nopf = false) {
@@ -1264,8 +1266,8 @@ class Engine final : public EngineBase {
             if (nopf) k = (const void*)expand_fast<M, 1, 0, false, true>;
         SR_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 64 * WPB, dyn));
         SR_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, o_.device));
-        cap = per_cu > 0 && cus > 0 ? (u32)(2 * per_cu * cus) : ~0u;
-        if (o_.verbose) std::fprintf(stderr, "[sr] expand grid cap %u blocks (%d per CU x %d CUs x 2)%s\n", cap, per_cu, cus, nopf ? " [no prefetch]" : "");
+        cap = per_cu > 0 && cus > 0 ? (u32)(grid_res_ * per_cu * cus) : ~0u;
+        if (o_.verbose) std::fprintf(stderr, "[sr] expand grid cap %u blocks (%d per CU x %d CUs x %u)%s\n", cap, per_cu, cus, grid_res_, nopf ? " [no prefetch]" : "");
         return cap;
     }
     // Wide states: the kernel without the register prefetch of the next chunk's parents when every
@@ -1505,6 +1507,11 @@ class Engine final : public EngineBase {
     double queue_ratio_ = std::getenv("SR_QUEUE_RATIO") ? std::atof(std::getenv("SR_QUEUE_RATIO")) : 0.0;
     int ppw_env_ = -1;
     bool table_recycle_ = true;  // the visited set is returned zeroed (~Engine)
+    // residencies per expand grid (expand_grid_cap; SR_GRID_RES, measurement knob): one for
+    // one-word states, two for wider ones (increment_lock N=11 33.3 -> 36.8 ms and paxos C=3 0.625 ->
+    // 0.648 ms with one: the claim-heavy levels and the wide no-prefetch form want the larger grid)
+    u32 grid_res_ = std::getenv("SR_GRID_RES") && std::atoi(std::getenv("SR_GRID_RES")) > 0 ? (u32)std::atoi(std::getenv("SR_GRID_RES"))
+                                                                                             : (W == 1 ? 1u : 2u);
     u32 grid_max_[3] = {0, 0, 0};  // cap on expand_fast's grid per form (rounds, queue, wide no-prefetch);
                                    // 0 = not computed yet (two device residencies, or SR_GRID_MAX)
     u32 grid_env_ = 0;       // SR_GRID_MAX
