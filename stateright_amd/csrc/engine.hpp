@@ -319,6 +319,12 @@ class Engine final : public EngineBase {
         if (filt_log2_ && (!std::getenv("SR_FILTER_COMPACT") || std::atoi(std::getenv("SR_FILTER_COMPACT"))) &&
             filter_compact_ok(m_, filt_log2_ + 1))
             filt_log2_ += 1, filt_compact_ = true;
+        // residencies per expand grid (expand_grid_cap): one for one-word states, four for
+        // multi-word quotient tables without the filter (increment_lock: every successor claims),
+        // two otherwise (profiles/r06_grid_cap.txt). SR_GRID_RES (measurement knob) overrides.
+        grid_res_ = W == 1 ? 1u : filt_log2_ ? 2u : 4u;
+        if (const char* e = std::getenv("SR_GRID_RES"))
+            if (std::atoi(e) > 0) grid_res_ = (u32)std::atoi(e);
         if (const char* e = std::getenv("SR_PIPELINE")) pipeline_ = std::atoi(e) != 0;
         if (const char* e = std::getenv("SR_QUERY_LOG2")) query_mask_ = (1ull << std::atoi(e)) - 1;
         if (const char* e = std::getenv("SR_GRID_MAX")) grid_env_ = (u32)std::max(0, std::atoi(e));  // <= 0: unset
@@ -1246,11 +1252,12 @@ class Engine final : public EngineBase {
     }
 
     // expand_fast's grid is capped at whole residencies of the device (resident blocks per CU at
-    // its LDS footprint x CUs, grid_res_ of them: one for one-word states, two otherwise); the
-    // kernel strides over any further parents. Whole residencies avoid a partial last wave of
-    // workgroups, and for 2pc one residency, every block starting at once and striding with its
-    // prefetch, beats two (round 6, `profiles/r06_grid_cap.txt`: N=9 1.556 -> 1.520 ms, N=10 7.93 ->
-    // 7.76, N=11 50.7 -> 50.5; 1.17 / 0.83 residencies were slower); the cap is printed with
+    // its LDS footprint x CUs, grid_res_ of them); the kernel strides over any further parents.
+    // Whole residencies avoid a partial last wave of workgroups. For 2pc one residency (every block
+    // starting at once and striding with its prefetch) beats two: N=9 1.556 -> 1.520 ms, N=10 7.93
+    // -> 7.76, N=11 50.7 -> 50.5 (1.17 / 0.83 residencies were slower); increment_lock, whose every
+    // successor claims a slot, wants more blocks in flight (N=11 32.8 -> 31.9 ms with four, 36.8 with
+    // one); paxos stays at two (round 6, `profiles/r06_grid_cap.txt`). The cap is printed with
     // verbose=1. SR_GRID_MAX > 0 overrides it (<= 0 or unparsable: the default).
     // The cap is cached per kernel form (the probe loop switches to the queue form once
     // the table grows past 2^27 slots, whose occupancy differs from the rounds form's).
@@ -1507,11 +1514,7 @@ class Engine final : public EngineBase {
     double queue_ratio_ = std::getenv("SR_QUEUE_RATIO") ? std::atof(std::getenv("SR_QUEUE_RATIO")) : 0.0;
     int ppw_env_ = -1;
     bool table_recycle_ = true;  // the visited set is returned zeroed (~Engine)
-    // residencies per expand grid (expand_grid_cap; SR_GRID_RES, measurement knob): one for
-    // one-word states, two for wider ones (increment_lock N=11 33.3 -> 36.8 ms and paxos C=3 0.625 ->
-    // 0.648 ms with one: the claim-heavy levels and the wide no-prefetch form want the larger grid)
-    u32 grid_res_ = std::getenv("SR_GRID_RES") && std::atoi(std::getenv("SR_GRID_RES")) > 0 ? (u32)std::atoi(std::getenv("SR_GRID_RES"))
-                                                                                             : (W == 1 ? 1u : 2u);
+    u32 grid_res_ = 2;  // residencies per expand grid (set in the constructor)
     u32 grid_max_[3] = {0, 0, 0};  // cap on expand_fast's grid per form (rounds, queue, wide no-prefetch);
                                    // 0 = not computed yet (two device residencies, or SR_GRID_MAX)
     u32 grid_env_ = 0;       // SR_GRID_MAX
