@@ -319,10 +319,9 @@ class Engine final : public EngineBase {
         if (filt_log2_ && (!std::getenv("SR_FILTER_COMPACT") || std::atoi(std::getenv("SR_FILTER_COMPACT"))) &&
             filter_compact_ok(m_, filt_log2_ + 1))
             filt_log2_ += 1, filt_compact_ = true;
-        // residencies per expand grid (expand_grid_cap): one for one-word states, four for
-        // multi-word quotient tables without the filter (increment_lock: every successor claims),
-        // two otherwise (profiles/r06_grid_cap.txt). SR_GRID_RES (measurement knob) overrides.
-        grid_res_ = W == 1 ? 1u : filt_log2_ ? 2u : 4u;
+        // residencies per expand grid (expand_grid_cap): one for one-word states, two otherwise
+        // (profiles/r06_grid_cap.txt). SR_GRID_RES (measurement knob) overrides.
+        grid_res_ = W == 1 ? 1u : 2u;
         if (const char* e = std::getenv("SR_GRID_RES"))
             if (std::atoi(e) > 0) grid_res_ = (u32)std::atoi(e);
         if (const char* e = std::getenv("SR_PIPELINE")) pipeline_ = std::atoi(e) != 0;
@@ -1255,10 +1254,9 @@ class Engine final : public EngineBase {
     // its LDS footprint x CUs, grid_res_ of them); the kernel strides over any further parents.
     // Whole residencies avoid a partial last wave of workgroups. For 2pc one residency (every block
     // starting at once and striding with its prefetch) beats two: N=9 1.556 -> 1.520 ms, N=10 7.93
-    // -> 7.76, N=11 50.7 -> 50.5 (1.17 / 0.83 residencies were slower); increment_lock, whose every
-    // successor claims a slot, wants more blocks in flight (N=11 32.8 -> 31.9 ms with four, 36.8 with
-    // one); paxos stays at two (round 6, `profiles/r06_grid_cap.txt`). The cap is printed with
-    // verbose=1. SR_GRID_MAX > 0 overrides it (<= 0 or unparsable: the default).
+    // -> 7.76, N=11 50.7 -> 50.5 (1.17 / 0.83 residencies were slower); increment_lock (36.8 ms with
+    // one against 33.3) and paxos stay at two (round 6, `profiles/r06_grid_cap.txt`). The cap is
+    // printed with verbose=1. SR_GRID_MAX > 0 overrides it (<= 0 or unparsable: the default).
     // The cap is cached per kernel form (the probe loop switches to the queue form once
     // the table grows past 2^27 slots, whose occupancy differs from the rounds form's).
     u32 expand_grid_cap(bool nopf = false) {

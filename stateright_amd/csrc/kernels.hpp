@@ -36,7 +36,8 @@ constexpr int MAX_PARTS = 64;  // visited-set partitions (one per GPU, or virtua
 #ifndef SR_WIDE_PPW_LOG2_MAX
 #define SR_WIDE_PPW_LOG2_MAX 5
 #endif
-// expand_fast's LDS stage of new states, in 64-bit words (its size sets the blocks per CU).
+// expand_fast's LDS stage of new narrow states (W < 4), in states per 4 waves (its size sets the
+// blocks per CU; until round 6 it was in 64-bit words, i.e. half as many two-word states).
 #ifndef SR_STAGE_WORDS
 #define SR_STAGE_WORDS 1024
 #endif
@@ -845,7 +846,9 @@ __global__ void __launch_bounds__(64 * expand_wpb<M>()) __attribute__((amdgpu_wa
                                                    HostCounters* hc, u32 seq, u32 reset, u32 ppw_log2,
                                                    u32 filt_log2, SlotWork sw) {
     constexpr int W = M::W, MW = M::MW;
-    constexpr int STAGE = (W >= 4 ? SR_WIDE_STAGE_WORDS : SR_STAGE_WORDS * expand_wpb<M>() / 4) / W;
+    // (narrow states: SR_STAGE_WORDS states per 4 waves whatever W; increment_lock's two-word states,
+    // every successor new, flush half as often as with that many words: N=10 3.63 -> 3.32 ms)
+    constexpr int STAGE = W >= 4 ? SR_WIDE_STAGE_WORDS / W : SR_STAGE_WORDS * expand_wpb<M>() / 4;
     extern __shared__ u64 filt[];       // 2^filt_log2 fingerprints (dynamic LDS; 0 = no filter)
     __shared__ u64 stage[STAGE * W];
     __shared__ u32 stage_par[STAGE];
