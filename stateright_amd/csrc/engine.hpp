@@ -1275,6 +1275,13 @@ class Engine final : public EngineBase {
         if (o_.verbose) std::fprintf(stderr, "[sr] expand grid cap %u blocks (%d per CU x %d CUs x %u)%s\n", cap, per_cu, cus, grid_res_, nopf ? " [no prefetch]" : "");
         return cap;
     }
+    // A level of more than DYN_MIN_RATIO chunks per workgroup takes the kernel with dynamic chunks
+    // (kernels.hpp SR_DYN_CHUNKS; the kernel checks the real frontier again). Narrow states only: the
+    // wide kernels' registers set their residency.
+    bool deep_level(u64 chunks, u32 grid) const {
+        return SR_DYN_CHUNKS && W < 4 && dyn_env_ && grid >= DYN_SHARDS && chunks > (u64)DYN_MIN_RATIO * grid;
+    }
+    bool dyn_env_ = !std::getenv("SR_DYN") || std::atoi(std::getenv("SR_DYN")) != 0;  // SR_DYN=0: measurement knob
     // Wide states: the kernel without the register prefetch of the next chunk's parents when every
     // chunk of the level has its own workgroup within that kernel's grid cap (DESIGN.md §3 "Wide
     // states"); the prefetching kernel when workgroups stride over chunks. SR_WIDE_NOPF=0/1 forces.
@@ -1299,6 +1306,7 @@ class Engine final : public EngineBase {
         const u32 chunks = std::max<u32>(1, blocks_for((shape + (1u << ppw_log2) - 1) >> ppw_log2, WPB));
         const bool nopf = use_nopf(chunks);
         const u32 grid = std::min(expand_grid_cap(nopf), chunks);
+        const bool deep = deep_level(chunks, grid);
         seq_launch_[sq] = launch_frontier.size();
         // a slotted launch: it counts into its own slot and is published by its successor
         SlotWork sw = slot_work(dev_n);
@@ -1325,6 +1333,7 @@ class Engine final : public EngineBase {
             };
             if (o_.counters) launch(expand_fast<M, 1, 0, true>);
             else if (nopf) launch_nopf(launch);
+            else if (deep) probe_loop() < 0 ? launch(expand_fast<M, -4, 0, false, false, true>) : launch(expand_fast<M, 1, 0, false, false, true>);
             else if (probe_loop() < 0) launch(expand_fast<M, -4, 0>);
             else launch(expand_fast<M, 1, 0>);
         }, n);
@@ -1407,6 +1416,8 @@ class Engine final : public EngineBase {
                         };
                         if (o_.counters) launch(expand_fast<M, 1, 0, true>);
                         else if (nopf) launch_nopf(launch);
+                        else if (deep_level(chunks, grid))
+                            probe_loop() < 0 ? launch(expand_fast<M, -4, 0, false, false, true>) : launch(expand_fast<M, 1, 0, false, false, true>);
                         else if (probe_loop() < 0) launch(expand_fast<M, -4, 0>);
                         else launch(expand_fast<M, 1, 0>);
                     });

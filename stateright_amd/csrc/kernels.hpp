@@ -41,6 +41,16 @@ constexpr int MAX_PARTS = 64;  // visited-set partitions (one per GPU, or virtua
 #ifndef SR_STAGE_WORDS
 #define SR_STAGE_WORDS 1024
 #endif
+// expand_fast's dynamic chunks: on a level of many chunks per workgroup (> DYN_MIN_RATIO), each
+// workgroup takes three chunks statically and then pulls the next ones from a counter, so that the
+// workgroups finish the level together (0: static striding only).
+#ifndef SR_DYN_CHUNKS
+#define SR_DYN_CHUNKS 1
+#endif
+constexpr u32 DYN_SHARDS = 8;
+#ifndef DYN_MIN_RATIO
+#define DYN_MIN_RATIO 6
+#endif
 // expand_fast's waves per workgroup for narrow states (W < 4): the block-local duplicate filter
 // is shared by the workgroup, so its reach is the parents of a whole chunk (waves x ppw).
 #ifndef SR_NARROW_WPB
@@ -336,6 +346,12 @@ struct LevelCounters {
     // Written by a slotted launch of the pipelined loop for a launch chained to it (SlotWork.chain):
     u64 next_base;         // arena offset of the frontier this launch produces
     u64 unique;            // unique states inserted before this launch's claims (its frontier included)
+    // expand_fast's dynamic chunks (SR_DYN_CHUNKS): chunks handed out past the static ones, one
+    // counter per XCD-sized shard of the workgroups (a line each), and the workgroups done with them
+    // (the last one zeroes them all for the slot's next launch)
+    alignas(128) u32 chunk_next[DYN_SHARDS][32];
+    u32 chunk_done;
+    u32 pad5[31];
 };
 static_assert(offsetof(LevelCounters, err) == offsetof(LevelCounters, claims) + 4, "claims/err pair");
 static_assert(offsetof(LevelCounters, prev_err) == offsetof(LevelCounters, prev_claims) + 4, "prev pair");
@@ -839,7 +855,7 @@ __device__ u64* g_timeline;
 // the kernel's time.
 // Wide states (W >= 4: paxos, the actor models) run three waves per SIMD (<= 168 VGPRs): their
 // levels are latency-bound, and paxos' device-side history search had pushed them to two.
-template <class M, int PB, int POL, bool STATS = false, bool NOPF = false>
+template <class M, int PB, int POL, bool STATS = false, bool NOPF = false, bool DYN = false>
 __global__ void __launch_bounds__(64 * expand_wpb<M>()) __attribute__((amdgpu_waves_per_eu(M::W >= 4 ? SR_WIDE_WAVES : PB < 0 ? 6 : 1))) expand_fast(M m, const u64* __restrict__ frontier, u32 lo, u32 hi,
                                                    TableView t, u64* __restrict__ next, u32* __restrict__ next_par,
                                                    u32 next_cap, LevelCounters* lc, u32 undiscovered,
@@ -985,7 +1001,26 @@ __global__ void __launch_bounds__(64 * expand_wpb<M>()) __attribute__((amdgpu_wa
             for (int i = 0; i < W; ++i) pst[wid][lane * W + i] = nxt[i];
         }
     }
-    for (u64 c0 = c_first; c0 < hi; c0 += cstride) {
+    // Dynamic chunks (SR_DYN_CHUNKS): with more than three chunks per workgroup, chunks 0 .. 3 nblk - 1
+    // are static (workgroup b takes b, b + nblk, b + 2 nblk) and later ones are pulled from the
+    // workgroup's shard counter (blockIdx % DYN_SHARDS; shard x hands out chunks 3 nblk + x + 8 i).
+    // Thread 0 issues a pull at the end of chunk j and uses its result at the end of chunk j + 1,
+    // as the chunk after next, so no wave waits for it (a returning atomic in flight holds every
+    // later vmcnt wait of its wave). The chunk after next reaches the workgroup through LDS at the
+    // chunk-end barrier. c_next: the chunk whose parents the prefetch loads (hi: none).
+    const u64 nchunks = hi > lo ? ((u64)hi - lo + chunk - 1) / chunk : 0;
+    // (only on levels of more than DYN_MIN_RATIO chunks per workgroup: the pulls cost each workgroup
+    // a little on every chunk, and with few chunks per workgroup the static stride balances well
+    // enough: 2pc N=9's big levels, 3.1-3.5 chunks per workgroup, were 5-8 us slower with them)
+    // (DYN: a separate instantiation, chosen by the host for levels it expects to be that deep, so the
+    // other levels run a kernel without this code and its registers)
+    const bool dyn = DYN && SR_DYN_CHUNKS && nblk >= DYN_SHARDS && nchunks > (u64)DYN_MIN_RATIO * nblk;  // (every shard has workgroups)
+    const u32 dshard = blockIdx.x % DYN_SHARDS;
+    __shared__ u64 s_cnext;
+    u64 c_next = c_first + cstride;
+    u32 kpend = 0;            // (thread 0) the pull in flight
+    bool pend = false, first_chunk = true;
+    for (u64 c0 = c_first; c0 < hi;) {
         const u32 wave0 = (u32)(c0 + ((u64)wid << ppw_log2));  // first parent of the wave
         const u32 r = wave0 + lane;
         u32 cnt = 0;
@@ -993,7 +1028,8 @@ __global__ void __launch_bounds__(64 * expand_wpb<M>()) __attribute__((amdgpu_wa
         if constexpr (PF) {
 #pragma unroll
             for (int i = 0; i < W; ++i) s[i] = nxt[i];
-            if (lane < (int)ppw && r + cstride < hi) load_state<W>(frontier, r + cstride, nxt);
+            const u64 rn = c_next + ((u64)wid << ppw_log2) + lane;
+            if (lane < (int)ppw && rn < hi) load_state<W>(frontier, rn, nxt);
         } else if (c0 != c_first && lane < (int)ppw && r < hi) {
             load_state<W>(frontier, r, s);  // (the wave's previous parents were last read by its own rounds)
 #pragma unroll
@@ -1365,7 +1401,28 @@ __global__ void __launch_bounds__(64 * expand_wpb<M>()) __attribute__((amdgpu_wa
         // stage once it is half full: otherwise it stays full after the first chunks and every
         // later append becomes a per-wave atomic on the one claims counter (2pc N=11: 478 ms per
         // check instead of 80).
+        if (dyn && threadIdx.x == 0) {
+            u64 cn = hi;  // the chunk after c_next
+            if (first_chunk) {
+                cn = c_first + 2 * cstride;  // static
+            } else if (pend) {
+                const u64 k = 3ull * nblk + dshard + (u64)DYN_SHARDS * kpend;
+                if (k < nchunks) cn = lo + k * chunk;
+            }
+            pend = cn < hi;
+            if (pend) {  // used at the next chunk end
+                // (an offset the compiler cannot prove uniform: the atomic optimizer would otherwise
+                // turn the pull into a wave reduction whose result is waited for at once)
+                u32 zoff;
+                asm volatile("v_mov_b32 %0, 0" : "=v"(zoff));
+                kpend = atomicAdd(&lc->chunk_next[dshard][0] + zoff, 1u);
+            }
+            s_cnext = cn;
+        }
+        first_chunk = false;
         __syncthreads();
+        c0 = c_next;
+        c_next = dyn ? s_cnext : c_next + cstride;  // (s_cnext is rewritten only after the next chunk-end barrier)
         if (stage_n >= (u32)STAGE / 2) {
             const u32 nst = min(stage_n, (u32)STAGE);
             if (threadIdx.x == 0) base = atomicAdd(&lc->claims, nst);
@@ -1387,6 +1444,12 @@ __global__ void __launch_bounds__(64 * expand_wpb<M>()) __attribute__((amdgpu_wa
             __syncthreads();
             if (threadIdx.x == 0) stage_n = 0;
         }
+    }
+    if (dyn && threadIdx.x == 0 && atomicAdd(&lc->chunk_done, 1u) == nblk - 1) {
+        // every workgroup has pulled its last chunk: the counters back to zero for the slot's next launch
+#pragma unroll
+        for (u32 x = 0; x < DYN_SHARDS; ++x) atomicExch(&lc->chunk_next[x][0], 0u);
+        atomicExch(&lc->chunk_done, 0u);
     }
     SR_TL(6);
     const bool repair = (sw.flags & SLOT_REPAIR) != 0;  // successors were counted by the first pass
