@@ -1,8 +1,8 @@
-"""Kernel-name helpers for the rocprofv3 CSV tools: expand_fast<M, PB, POL, STATS, NOPF> dispatches of
+"""Kernel-name helpers for the rocprofv3 CSV tools: expand_fast<M, PB, POL, STATS, NOPF, DYN> dispatches of
 the counting pass (STATS = true, bench.py's last check) are excluded from rates and traffic."""
 import re
 
-_ARGS = re.compile(r"expand_fast<.*?, (-?\d+), (\d+), (true|false)(?:, (true|false))?>(?:\(|$)")
+_ARGS = re.compile(r"expand_fast<.*?, (-?\d+), (\d+), (true|false)((?:, (?:true|false))*)>(?:\(|$)")
 
 
 def is_expand_fast(name):
