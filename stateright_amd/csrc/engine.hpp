@@ -498,10 +498,14 @@ class Engine final : public EngineBase {
   private:
     TableView view() const { return make_table_view(m_, keys_.p, fifo_ ? meta_.p : nullptr, cap_); }
 
-    void alloc_table(u64 cap) {
+    // zero = false: the caller writes every slot (rehash_ranges), so no clear is enqueued.
+    void alloc_table(u64 cap, bool zero = true) {
         cap_ = cap;
         lmax_ = max_load(cap);
-        keys_.alloc_zero(o_.device, table_words(make_table_view(m_, nullptr, nullptr, cap), cap), stream_, table_kind_);
+        const u64 words = table_words(make_table_view(m_, nullptr, nullptr, cap), cap);
+        table_unzeroed_ = false;
+        if (zero) keys_.alloc_zero(o_.device, words, stream_, table_kind_);
+        else keys_.alloc(o_.device, words, table_kind_);
         if (fifo_) {
             meta_.alloc(o_.device, cap);
             SR_HIP(hipMemsetAsync(meta_.p, 0xff, cap * sizeof(u64), stream_));
@@ -525,10 +529,7 @@ class Engine final : public EngineBase {
         u64 f0 = 2;
         while (old_cap * f0 < min_slots) f0 *= 2;
         for (u64 f = f0;; f *= 2) {
-            alloc_table(old_cap * f);
-            SR_HIP(hipMemsetAsync(aux_.p, 0, sizeof(u32), stream_));
-            rehash<<<blocks_for(old_cap, 256), 256, 0, stream_>>>(from, old_cap, view(), aux_.p);
-            SR_HIP(hipGetLastError());
+            launch_rehash(from, old_cap, f);
             u32 err = 0;
             SR_HIP(hipMemcpyAsync(&err, aux_.p, sizeof(u32), hipMemcpyDeviceToHost, stream_));
             SR_HIP(stream_sync(stream_));
@@ -561,16 +562,53 @@ class Engine final : public EngineBase {
         if (!aux_.p) aux_.alloc(o_.device, 2);
         u64 f = 2;
         while (old_cap * f < min_slots) f *= 2;
-        alloc_table(old_cap * f);
-        SR_HIP(hipMemsetAsync(aux_.p, 0, sizeof(u32), stream_));
-        rehash<<<blocks_for(old_cap, 256), 256, 0, stream_>>>(from, old_cap, view(), aux_.p);
-        SR_HIP(hipGetLastError());
+        launch_rehash(from, old_cap, f);
         rehash_pending_ = true;
         stats.rehashes++;
         if (o_.verbose)
             std::fprintf(stderr, "[sr] visited set %llu -> %llu slots enqueued\n", (unsigned long long)old_cap,
                          (unsigned long long)cap_);
     }
+    // Allocates the table of old_cap * f slots and enqueues the rehash of `from` into it (error bits
+    // in aux_[0]): range by range without a clear (rehash_ranges + rehash_spill) when the new homes
+    // of a range of old homes are a range (quotient mode, f = 2^(from.qbits - to.qbits)) and no meta
+    // moves along (FAST order), else a clear plus one CAS insertion per entry (rehash).
+    // SR_REHASH_RANGES=0 (measurement knob) always takes the latter.
+    void launch_rehash(const TableView& from, u64 old_cap, u64 f) {
+        const u64 cap = old_cap * f;
+        const TableView to0 = make_table_view(m_, nullptr, nullptr, cap);
+        u32 lg = 0;
+        while ((1ull << lg) < f) ++lg;
+        const u64 S = to0.s32 ? rebuild_slots<u32>() : rebuild_slots<u64>();
+        const bool ranges = rehash_ranges_ && !from.meta && from.qbits && to0.qbits &&
+                            from.qbits == to0.qbits + lg && f <= S && cap % S == 0;
+        alloc_table(cap, !ranges);
+        table_unzeroed_ = ranges;
+        SR_HIP(hipMemsetAsync(aux_.p, 0, sizeof(u32), stream_));
+        if (ranges) {
+            const u64 nranges = cap / S, spill_cap = nranges + 65536;
+            if (spill_.n < spill_cap + 1) spill_.alloc(o_.device, spill_cap + 1);
+            SR_HIP(hipMemsetAsync(spill_.p, 0, sizeof(u64), stream_));
+            if (to0.s32)
+                rehash_ranges<u32><<<(u32)nranges, REBUILD_BLOCK, 0, stream_>>>(from, old_cap, view(), lg, spill_.p,
+                                                                               spill_cap, aux_.p);
+            else
+                rehash_ranges<u64><<<(u32)nranges, REBUILD_BLOCK, 0, stream_>>>(from, old_cap, view(), lg, spill_.p,
+                                                                               spill_cap, aux_.p);
+            SR_HIP(hipGetLastError());
+            rehash_spill<<<256, 256, 0, stream_>>>(from, view(), spill_.p, spill_cap, aux_.p);
+        } else {
+            rehash<<<blocks_for(old_cap, 256), 256, 0, stream_>>>(from, old_cap, view(), aux_.p);
+        }
+        SR_HIP(hipGetLastError());
+    }
+    bool rehash_ranges_ = !std::getenv("SR_REHASH_RANGES") || std::atoi(std::getenv("SR_REHASH_RANGES")) != 0;
+    DBuf<u64> spill_;  // rehash_ranges' spill list: [0] count, then old slot indices
+    // The visited set was built by rehash_ranges (allocated without a clear): released without one
+    // too, since the next unhinted check grows into its tables the same way (a hinted check clears
+    // what it takes).
+    bool table_unzeroed_ = false;
+
     // (an asynchronous growth is enqueued only while none is pending)
     void check_async_growth_pending_first() {
         if (rehash_pending_) check_async_growth();
@@ -1042,6 +1080,7 @@ class Engine final : public EngineBase {
         stats.total_sec = secs(t_start, t_end);
         stats.table_capacity = cap_;
         release_table();  // (the pipelined loop released it already)
+        free_unzeroed_table();
         return order_dependent && !fifo_;
     }
 
@@ -1204,6 +1243,7 @@ class Engine final : public EngineBase {
         release_table();
         drain(ctx_->done);
         check_async_growth();
+        free_unzeroed_table();
         return order_dependent;
     }
 
@@ -1229,7 +1269,13 @@ class Engine final : public EngineBase {
     // a clear at its start. Kept for the displacement scan of a counting run (sr_opts.counters),
     // and in FIFO order. SR_TABLE_RECYCLE=0: an ordinary free, each check clears its own table.
     void release_table() {
-        if (table_recycle_ && !fifo_ && !o_.counters) keys_.release_zero(stream_);
+        if (table_recycle_ && !fifo_ && !o_.counters && !table_unzeroed_) keys_.release_zero(stream_);
+    }
+    // A table built by rehash_ranges goes back to the pool as it is, once the stream is idle.
+    void free_unzeroed_table() {
+        if (!table_recycle_ || fifo_ || o_.counters || !table_unzeroed_ || !keys_.p) return;
+        SR_HIP(stream_sync(stream_));
+        keys_.reset();
     }
 
     // Launch of the level whose frontier (n states) ends the arena, after the previous one is done:

@@ -1758,6 +1758,96 @@ template <int = 0> __global__ void rehash(TableView from, u64 from_cap, TableVie
     if (to.meta) to.meta[slot] = from.meta[i];
 }
 
+// Growth of a quotient-mode table (no meta) by g = 2^lg, built range by range with no clear of the
+// new table before it: a key's home is the top bits of its permuted key, so new slots [r S, (r+1) S)
+// receive exactly the entries whose OLD home is in [r S / g, (r+1) S / g), and those sit in the old
+// table between that range's first home and the first vacant old slot past its last. Workgroup r
+// inserts them by linear probing into S slots of LDS and writes the whole range, zeros included,
+// with 16-byte stores: one pass over each table instead of a clear plus a CAS per entry into a
+// table too large for any cache (increment_lock N=11 unhinted, 2^28 -> 2^31 slots: 2.8 ms of clear
+// and 6.2 ms of rehash, profiles/r06_nohint_inclock11_trace.txt). Any order of insertion leaves a
+// valid linear-probing table (every slot between a key's home and its slot is occupied). An entry
+// whose probe runs past the range end goes to spill[1..] (spill[0] counts them) and is inserted by
+// rehash_spill, with CAS, once every range is written. err: ERR_TABLE_FULL if a displacement
+// reaches the new probe limit or the spill list overflows (the host then grows further).
+// S: the slots of a range, 32 KB of LDS (8192 four-byte or 4096 eight-byte slots). The old slots
+// are read REBUILD_ROWS rows of the workgroup at a time, all loads in flight together, over the
+// range's homes plus one row at first (one barrier when that row holds a vacant slot, as it nearly
+// always does), then one row more per round.
+constexpr u32 REBUILD_BLOCK = 256;
+constexpr u32 REBUILD_ROWS = 4;
+constexpr u32 REBUILD_BYTES = 32768;
+template <class T>
+constexpr u32 rebuild_slots() { return REBUILD_BYTES / sizeof(T); }
+template <class T>
+__global__ void __launch_bounds__(REBUILD_BLOCK)
+    rehash_ranges(TableView from, u64 from_cap, TableView to, u32 lg, u64* spill, u64 spill_cap, u32* err) {
+    constexpr u32 S = rebuild_slots<T>();
+    __shared__ uint4 lds4[REBUILD_BYTES / 16];
+    T* lds = reinterpret_cast<T*>(lds4);
+    for (u32 j = threadIdx.x; j < REBUILD_BYTES / 16; j += REBUILD_BLOCK) lds4[j] = make_uint4(0, 0, 0, 0);
+    __syncthreads();
+    const u64 r0 = (u64)blockIdx.x * S;
+    const u64 a = r0 >> lg, span = S >> lg;  // old homes [a, a + span)
+    const u64 omask = from_cap - 1, dmask = (1ull << from.dbits) - 1;
+    u64 lo = 0, hi = span + REBUILD_BLOCK;
+    for (;;) {
+        bool done = false;
+        for (u64 base = lo; base < hi; base += REBUILD_ROWS * REBUILD_BLOCK) {
+            u64 v[REBUILD_ROWS];
+#pragma unroll
+            for (u32 r = 0; r < REBUILD_ROWS; ++r) {
+                const u64 off = base + r * REBUILD_BLOCK + threadIdx.x;
+                v[r] = off < hi ? slot_load(from, (a + off) & omask) : 1ull;  // (1: outside the window)
+            }
+#pragma unroll
+            for (u32 r = 0; r < REBUILD_ROWS; ++r) {
+                const u64 off = base + r * REBUILD_BLOCK + threadIdx.x, i = (a + off) & omask;
+                if (off >= hi) continue;
+                if (!v[r]) {
+                    done |= off >= span;  // a vacant slot past the last home ends the range's entries
+                    continue;
+                }
+                if (((i - ((v[r] & dmask) - 1) - a) & omask) >= span) continue;  // homed elsewhere
+                const ProbeKey k = quot_probe(to, quot_decode(from, i, v[r]));
+                u64 j = k.home - r0;
+                if (j >= S) {
+                    atomicOr(err, (u32)ERR_TABLE_FULL);  // (not homed in this range: cannot happen)
+                    continue;
+                }
+                for (u64 d = 0;; ++d, ++j) {
+                    if (d >= to.plimit) {
+                        atomicOr(err, (u32)ERR_TABLE_FULL);
+                        break;
+                    }
+                    if (j >= S) {
+                        const u64 q = atomicAdd(reinterpret_cast<unsigned long long*>(spill), 1ull);
+                        if (q < spill_cap) spill[1 + q] = i;
+                        else atomicOr(err, (u32)ERR_TABLE_FULL);
+                        break;
+                    }
+                    if (atomicCAS(&lds[j], (T)0, (T)(k.tag + d)) == (T)0) break;
+                }
+            }
+        }
+        if (__syncthreads_or(done) || hi >= from_cap) break;
+        lo = hi;
+        hi += REBUILD_BLOCK;
+    }
+    uint4* out = reinterpret_cast<uint4*>(reinterpret_cast<T*>(to.keys) + r0);
+    for (u32 j = threadIdx.x; j < REBUILD_BYTES / 16; j += REBUILD_BLOCK) out[j] = lds4[j];
+}
+// The entries rehash_ranges spilled past their range's end, inserted into the finished table.
+template <int = 0>
+__global__ void rehash_spill(TableView from, TableView to, const u64* spill, u64 spill_cap, u32* err) {
+    const u64 n = min(spill[0], spill_cap);
+    for (u64 q = (u64)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += (u64)gridDim.x * blockDim.x) {
+        const u64 i = spill[1 + q];
+        bool is_new;
+        (void)find_or_claim(to, reprobe(from, to, i, slot_load(from, i)), &is_new, err);
+    }
+}
+
 // Longest linear-probe displacement over the occupied slots (sr_stats.max_displacement): quotient
 // mode stores 1 + the displacement in the low dbits; a fingerprint's home is fp & mask.
 template <int = 0> __global__ void __launch_bounds__(256) table_max_disp(TableView t, u64 cap, u32* out) {

@@ -280,6 +280,38 @@ def test_growth_from_small_table(step, monkeypatch):
     assert c.stats()["rehashes"] >= (2 if step == "2" else 1)
 
 
+@pytest.mark.parametrize("ranges", ["0", "1"])
+@pytest.mark.parametrize("step", ["2", "8", "64"])
+def test_rehash_by_ranges(step, ranges, monkeypatch):
+    # Growth of a quotient table range by range (kernels.hpp rehash_ranges: no clear, LDS insertion,
+    # entries past a range's end spilled and inserted afterwards) against the CAS rehash: steps of 2
+    # leave the new table at up to half load (many spills), 64 at a few percent. One-word keys in
+    # 4-byte slots (2pc) and two-word keys in 8-byte slots (increment_lock); exact counts.
+    monkeypatch.setenv("SR_GROW_STEP", step)
+    monkeypatch.setenv("SR_REHASH_RANGES", ranges)
+    n = 9
+    c = sr.TwoPhaseSys(n).checker().order("fast").spawn_bfs().join()
+    assert c.unique_state_count() == 6 ** n + 4 ** n + 2 ** n
+    assert 3 * c.state_count() == 4 * n * 6 ** n + 3 * (n + 1) * 4 ** n + 3 * n * 2 ** n + 6
+    assert c.stats()["rehashes"] >= 1
+    expect = 1 + 4 * sum(math.factorial(n) // math.factorial(n - k) for k in range(1, n + 1))
+    c = sr.IncrementLock(n).checker().order("fast").spawn_bfs().join()
+    assert c.unique_state_count() == c.state_count() == expect
+    assert c.max_depth() == 4 * n
+    assert c.stats()["rehashes"] >= 1
+
+
+def test_rehash_by_ranges_probe_limit(monkeypatch):
+    # A probe limit of 6 slots (SR_DISP_LIMIT): range rebuilds that meet it report a full table and
+    # the growth goes on to a larger table; counts stay exact.
+    monkeypatch.setenv("SR_DISP_LIMIT", "6")
+    monkeypatch.setenv("SR_GROW_STEP", "2")
+    n = 7
+    c = sr.TwoPhaseSys(n).checker().order("fast").spawn_bfs().join()
+    assert c.unique_state_count() == 6 ** n + 4 ** n + 2 ** n
+    assert 3 * c.state_count() == 4 * n * 6 ** n + 3 * (n + 1) * 4 ** n + 3 * n * 2 ** n + 6
+
+
 def test_paxos_golden():
     # examples/paxos.rs:268-290 (BFS): assert_properties, assert_discovery of the reference's
     # "value chosen" path, unique_state_count 16_668.
