@@ -1503,18 +1503,51 @@ class DistEngine final : public EngineBase {
         return ev[i];
     }
 
-    void grow_table(Part& p) {
+    // The load at which a partition's visited set grows: the probe limit's (lmax) for a hinted
+    // check, whose tables are planned at part_load_ from the start; without a hint the tables start
+    // at the default size and grow once a level would take them past 1.5 part_load_ (to part_load_,
+    // in one step: want = the states the level may leave in it), rather than running the rest of
+    // the check at up to lmax (2pc N=9 on one rank ended at 0.62 load: expand_route 2.61 ms per
+    // check against 1.98 hinted, profiles/r06_partitioned_nohint.txt).
+    double grow_at(u64 cap) const {
+        return o_.capacity_hint ? lmax(cap) : std::min(lmax(cap), 1.5 * part_load_);
+    }
+    void grow_table(Part& p, u64 want = 0) {
         DBuf<u64> ok;
         ok.swap(p.keys);
         const u64 old_cap = p.cap;
-        p.cap *= 2;
+        u64 f = 2;
+        if (!o_.capacity_hint)
+            while ((double)want > std::min(part_load_, lmax(old_cap * f)) * (double)(old_cap * f) && f < 64) f *= 2;
+        p.cap = old_cap * f;
+        const TableView from = make_table_view(m_, ok.p, nullptr, old_cap), to0 = make_table_view(m_, nullptr, nullptr, p.cap);
+        u32 lg = 0;
+        while ((1ull << lg) < f) ++lg;
+        const u64 S = to0.s32 ? rebuild_slots<u32>() : rebuild_slots<u64>();
+        // range by range as in Engine::launch_rehash (no clear of the new table), else clear + CAS
+        const bool ranges = from.qbits && to0.qbits && from.qbits == to0.qbits + lg && f <= S && p.cap % S == 0;
         p.keys.alloc(o_.device, p.words());
-        SR_HIP(hipMemsetAsync(p.keys.p, 0, p.words() * 8, stream_));
-        rehash<<<blocks_for(old_cap, 256), 256, 0, stream_>>>(make_table_view(m_, ok.p, nullptr, old_cap), old_cap, p.view(), &p.lc->err);
+        if (ranges) {
+            const u64 nranges = p.cap / S, spill_cap = nranges + 65536;
+            if (spill_.n < spill_cap + 1) spill_.alloc(o_.device, spill_cap + 1);
+            SR_HIP(hipMemsetAsync(spill_.p, 0, sizeof(u64), stream_));
+            if (to0.s32)
+                rehash_ranges<u32><<<(u32)nranges, REBUILD_BLOCK, 0, stream_>>>(from, old_cap, p.view(), lg, spill_.p,
+                                                                               spill_cap, &p.lc->err);
+            else
+                rehash_ranges<u64><<<(u32)nranges, REBUILD_BLOCK, 0, stream_>>>(from, old_cap, p.view(), lg, spill_.p,
+                                                                               spill_cap, &p.lc->err);
+            SR_HIP(hipGetLastError());
+            rehash_spill<<<256, 256, 0, stream_>>>(from, p.view(), spill_.p, spill_cap, &p.lc->err);
+        } else {
+            SR_HIP(hipMemsetAsync(p.keys.p, 0, p.words() * 8, stream_));
+            rehash<<<blocks_for(old_cap, 256), 256, 0, stream_>>>(from, old_cap, p.view(), &p.lc->err);
+        }
         SR_HIP(hipGetLastError());
         SR_HIP(stream_sync(stream_));
         stats.rehashes++;
     }
+    DBuf<u64> spill_;  // rehash_ranges' spill list
 
     void init_counters(Part& p) {
         LevelCounters z;
@@ -1640,7 +1673,8 @@ class DistEngine final : public EngineBase {
                 // most successors are duplicates)
                 const double g = std::min((double)d_eff, std::max(1.0, growth) * 1.5);
                 const u64 expect_new = (u64)((double)glob_est * g / (double)T_) + 1024;
-                while ((double)(p.uniq + p.n_hi + expect_new) > lmax(p.cap) * (double)p.cap) grow_table(p);
+                const u64 want = p.uniq + p.n_hi + expect_new;
+                while ((double)want > grow_at(p.cap) * (double)p.cap) grow_table(p, want);
                 const u64 nb = p.lstart.back();  // arena offset of the frontier being expanded
                 const u64 n_plan = pessimistic_ ? p.n_hi : std::min(p.n_hi, p.n_est * 2 + 1024);
                 // records per destination: last level's records per parent (measured), with slack
@@ -2205,7 +2239,8 @@ class DistEngine final : public EngineBase {
                 const u64 fr = ahead == 2 ? (u64)((double)c1 * gc) + 1024 : c1;
                 const u64 nw = (u64)((double)fr * gc) + 1024;
                 const u64 before = ahead == 2 ? hi : 0;  // a frontier between the rows and the target
-                while ((double)(p.uniq + before + hi + fr + nw) > lmax(p.cap) * (double)p.cap) grow_table(p);
+                const u64 want = p.uniq + before + hi + fr + nw;
+                while ((double)want > grow_at(p.cap) * (double)p.cap) grow_table(p, want);
                 const u64 need = p.lstart.back() + hi + (ahead == 2 ? fr : 0) + nw + 1024;
                 if (p.arena_cap < need) ensure_arena(p, std::max<u64>(need + need / 4, p.arena_cap * 2), p.arena_cap);
                 n_plan[p.id] = fr;
