@@ -1790,7 +1790,8 @@ __global__ void __launch_bounds__(REBUILD_BLOCK)
     const u64 r0 = (u64)blockIdx.x * S;
     const u64 a = r0 >> lg, span = S >> lg;  // old homes [a, a + span)
     const u64 omask = from_cap - 1, dmask = (1ull << from.dbits) - 1;
-    u64 lo = 0, hi = span + REBUILD_BLOCK;
+    // window [lo, hi) of offsets past a, never more than the old table (no slot is read twice)
+    u64 lo = 0, hi = min<u64>(span + REBUILD_BLOCK, from_cap);
     for (;;) {
         bool done = false;
         for (u64 base = lo; base < hi; base += REBUILD_ROWS * REBUILD_BLOCK) {
@@ -1832,7 +1833,7 @@ __global__ void __launch_bounds__(REBUILD_BLOCK)
         }
         if (__syncthreads_or(done) || hi >= from_cap) break;
         lo = hi;
-        hi += REBUILD_BLOCK;
+        hi = min<u64>(hi + REBUILD_BLOCK, from_cap);
     }
     uint4* out = reinterpret_cast<uint4*>(reinterpret_cast<T*>(to.keys) + r0);
     for (u32 j = threadIdx.x; j < REBUILD_BYTES / 16; j += REBUILD_BLOCK) out[j] = lds4[j];
