@@ -677,11 +677,22 @@ class Engine final : public EngineBase {
     // by copying the used prefix.
     // async: the copy is enqueued behind the work in flight and the old buffers retired until the
     // stream has passed it (check_async_growth), instead of waiting here.
+    // The arena's growth step (SR_ARENA_STEP, default 8; 4 until round 6: unhinted 2pc N=10 8.17-8.19 ->
+    // 7.95-8.00 ms, increment_lock N=11 33.9-34.9 -> 32.8-32.9, profiles/r06_arena_step.txt).
+    u64 arena_step_ = std::getenv("SR_ARENA_STEP") && std::atoi(std::getenv("SR_ARENA_STEP")) >= 2
+                          ? (u64)std::atoi(std::getenv("SR_ARENA_STEP")) : 8u;
     void ensure_arena(u64 states, u64 used, bool async = false) {
         if (arena_cap_ >= states) return;
         const auto ta = Clock::now();
-        // (growth steps of 4: each copies the arena so far and stops the level pipeline)
-        u64 cap = std::max<u64>(states, arena_cap_ * (arena_cap_ ? 4 : 1));
+        // (each growth step copies the arena so far and stops the level pipeline; a step never takes
+        // more than half the device's free memory, nor less than `states`)
+        u64 cap = std::max<u64>(states, arena_cap_ * (arena_cap_ ? arena_step_ : 1));
+        if (cap > states) {
+            size_t fr = 0, tot = 0;
+            const u64 per = W * sizeof(u64) + sizeof(u32) + (emask_ ? sizeof(u32) : 0);
+            if (hipMemGetInfo(&fr, &tot) == hipSuccess) cap = std::max<u64>(states, std::min<u64>(cap, fr / 2 / per));
+            else (void)hipGetLastError();
+        }
         DBuf<u64> na;
         DBuf<u32> np, ne;
         na.alloc(o_.device, cap * W);
@@ -1286,7 +1297,7 @@ class Engine final : public EngineBase {
         const u64 fbase = lstart_[lstart_.size() - 2];
         if (need > lmax_ * (double)cap_) {
             grow_table(nullptr, 0, growth_slots((u64)(need / lmax_) + 1));
-            // The arena takes its next step (x4) with the table: a table that had to grow holds nearly
+            // The arena takes its next step (x8) with the table: a table that had to grow holds nearly
             // as many states as the arena (both start at 2^22), and the arena's own step, a copy and
             // a second stop of the level pipeline, would follow a level later (2pc N=9 without a
             // hint: levels 9 and 10).
