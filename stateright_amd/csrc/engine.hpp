@@ -677,10 +677,12 @@ class Engine final : public EngineBase {
     // by copying the used prefix.
     // async: the copy is enqueued behind the work in flight and the old buffers retired until the
     // stream has passed it (check_async_growth), instead of waiting here.
-    // The arena's growth step (SR_ARENA_STEP, default 8; 4 until round 6: unhinted 2pc N=10 8.17-8.19 ->
-    // 7.95-8.00 ms, increment_lock N=11 33.9-34.9 -> 32.8-32.9, profiles/r06_arena_step.txt).
+    // The arena's growth step (SR_ARENA_STEP; default 8 for states of <= 2 words, 4 for wider ones, as
+    // every model until round 6): unhinted 2pc N=10 8.17-8.24 -> 7.93-8.00 ms, increment_lock N=11
+    // 33.9-35.0 -> 32.5-33.3; paxos C=6 (W = 12) 3.02-3.04 -> 3.20-3.21 with 8, so it keeps 4
+    // (profiles/r06_arena_step.txt).
     u64 arena_step_ = std::getenv("SR_ARENA_STEP") && std::atoi(std::getenv("SR_ARENA_STEP")) >= 2
-                          ? (u64)std::atoi(std::getenv("SR_ARENA_STEP")) : 8u;
+                          ? (u64)std::atoi(std::getenv("SR_ARENA_STEP")) : W <= 2 ? 8u : 4u;
     void ensure_arena(u64 states, u64 used, bool async = false) {
         if (arena_cap_ >= states) return;
         const auto ta = Clock::now();
@@ -1297,7 +1299,7 @@ class Engine final : public EngineBase {
         const u64 fbase = lstart_[lstart_.size() - 2];
         if (need > lmax_ * (double)cap_) {
             grow_table(nullptr, 0, growth_slots((u64)(need / lmax_) + 1));
-            // The arena takes its next step (x8) with the table: a table that had to grow holds nearly
+            // The arena takes its next step (x8 / x4) with the table: a table that had to grow holds nearly
             // as many states as the arena (both start at 2^22), and the arena's own step, a copy and
             // a second stop of the level pipeline, would follow a level later (2pc N=9 without a
             // hint: levels 9 and 10).
